@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the DPEngine.aggregate hot path on MI355X (BASELINE.json).
+
+Workload (BASELINE.json configs[1], SURVEY §8(d) "C2"): per GPU N = 1e8 rows,
+P = 1e5 partitions (pk uniform), U = 1e6 privacy ids (pid uniform, ~100 rows
+each), value fp64 ~ N(5, 3) clipped to [0, 10]; COUNT + SUM + MEAN, Laplace,
+max_partitions_contributed = 8, max_contributions_per_partition = 2,
+min/max value 0/10, eps = 1, delta = 1e-6, private partitions (truncated
+geometric).  Weak scaling: every rank holds its own 1e8 rows of its own 1e6
+privacy ids (rows sharded by privacy id), partitions are global; the one
+cross-GPU step is an RCCL reduce-scatter of the per-partition accumulators,
+after which each rank selects and noises its slice of partitions.
+
+A step = one full aggregate over the resident batch: contribution bounding
+(L0 + Linf sampling), per-partition reduction, [reduce-scatter], partition
+selection, compaction and noisy metrics, ending with the kept-partition count
+on the host.  Inputs are resident in HBM before timing starts.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N > 1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+# workload constants (C2)
+ROWS_PER_GPU = 100_000_000
+PRIVACY_IDS_PER_GPU = 1_000_000
+PARTITIONS = 100_000
+L0, LINF = 8, 2
+MIN_VALUE, MAX_VALUE = 0.0, 10.0
+EPS, DELTA = 1.0, 1e-6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=ROWS_PER_GPU, help="rows per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=600_000)
+    return ap.parse_args()
+
+
+def build_plan():
+    """Noise / selection parameters exactly as DPEngine + NaiveBudgetAccountant
+    derive them for this AggregateParams (3 mechanisms of weight 1: MEAN's
+    count and normalized-sum Laplace mechanisms + the GENERIC selection)."""
+    from pipelinedp_amd import _native as N
+    from pipelinedp_amd import dp_computations as dpc
+    from pipelinedp_amd import executor as X
+    eps_each = EPS / 3
+    mid = dpc.compute_middle(MIN_VALUE, MAX_VALUE)
+    b_count = dpc.laplace_diversity(eps_each, L0 * LINF)
+    b_nsum = dpc.laplace_diversity(eps_each, L0 * (MAX_VALUE - MIN_VALUE) / 2 * LINF)
+    bounding = X.BoundingSpec(l0=L0, linf=LINF, value_kind=N.VALUE_F64, flags=N.ACC_NSUM,
+                              min_value=MIN_VALUE, max_value=MAX_VALUE, middle=mid)
+    selection = X.SelectionSpec(strategy=N.SELECT_TRUNCATED_GEOMETRIC,
+                                keep_prob=dpc.truncated_geometric_keep_table(eps_each, DELTA, L0))
+    ops = [X.MetricOpSpec(kind=N.OP_MEAN, noise_kind=N.NOISE_LAPLACE, out_col=(0, 1, 2),
+                          scale=(b_count, b_nsum), middle=mid)]
+    return bounding, selection, ops
+
+
+def cpu_baseline(sample_rows):
+    """Row-wise restatement of LocalBackend DPEngine.aggregate (the reference's
+    single-threaded CPU path) on a bounded sample of the same workload."""
+    from oracle import local_backend_port as port
+    rng = np.random.default_rng(1)
+    U = max(1, sample_rows // 100)
+    pid = rng.integers(0, U, sample_rows)
+    pk = rng.integers(0, PARTITIONS, sample_rows)
+    val = np.clip(rng.normal(5.0, 3.0, sample_rows), MIN_VALUE, MAX_VALUE)
+    rows = list(zip(pid.tolist(), pk.tolist(), val.tolist()))
+    t0 = time.perf_counter()
+    out = port.aggregate_count_sum_mean(rows, l0=L0, linf=LINF, min_value=MIN_VALUE,
+                                        max_value=MAX_VALUE, eps=EPS, delta=DELTA)
+    dt = time.perf_counter() - t0
+    return {"value": sample_rows / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{sample_rows} rows of the same workload (U={U}, P={PARTITIONS}), "
+                      f"oracle/local_backend_port.py row-wise LocalBackend restatement, "
+                      f"{dt:.1f} s, {len(out)} partitions kept"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from pipelinedp_amd import executor as X
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local_rank)
+
+    n = args.rows
+    U = max(1, (PRIVACY_IDS_PER_GPU * n) // ROWS_PER_GPU)
+    P = PARTITIONS
+    bounding, selection, ops = build_plan()
+
+    g = torch.Generator(device=device)
+    g.manual_seed(1000 + rank)
+    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+    pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
+    value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
+        MIN_VALUE, MAX_VALUE)
+    torch.cuda.synchronize()
+
+    P_pad = ((P + world - 1) // world) * world
+    slice_len = P_pad // world
+    ws = X.BoundWorkspace()
+    acc = X.new_accumulators(P_pad, bounding, device)
+    seed_base = int.from_bytes(os.urandom(8), "little")
+
+    def step(i, timer=None):
+        for t in acc.values():
+            if t is not None:
+                t.zero_()
+        X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
+                           seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
+                           check_keys=False, timer=timer)
+        if world > 1:
+            if timer is not None:
+                timer.mark("exchange")
+            part = {}
+            for k, t in acc.items():
+                if t is None:
+                    continue
+                out = torch.empty(slice_len, dtype=t.dtype, device=device)
+                dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM)
+                part[k] = out
+            mine = {k: part.get(k) for k in acc}
+            if timer is not None:
+                timer.mark("end_exchange")
+        else:
+            mine = acc
+        _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
+                                          seed_select=seed_base ^ (i * 7919 + 1),
+                                          seed_noise=seed_base ^ (i * 104729 + 2),
+                                          partition_offset=rank * slice_len, timer=timer)
+        return n_kept
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timer = X.StageTimer()
+    t0 = time.perf_counter()
+    kept = 0
+    for i in range(args.steps):
+        kept = step(args.warmup + i, timer)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stages = {k: v / args.steps for k, v in timer.durations().items()}  # ms per step
+    # algorithmic bytes per launch of each stage (DESIGN.md "Kernels")
+    slots = U * L0
+    alg_bytes = {
+        "sketch": 16.0 * n,                       # pid + pk
+        "rows": 16.0 * n,                         # pid + pk
+        "reduce": slots * 12.0 + slots * LINF * 8.0 * 0.5 + P * 8.0 * 3,  # sketch+cnt, gathers, accs
+        "select": P * (8.0 + 1.0 + 8.0),
+    }
+    dom = max((k for k in stages if k in alg_bytes), key=lambda k: stages[k])
+    achieved = alg_bytes[dom] / (stages[dom] * 1e-3) / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+    total_rows = n * world * args.steps
+    value_rows_s = total_rows / elapsed
+    path_bytes = 24.0 * n + kept * (8 + 8 * 3 + 8 * 3)
+    result = {
+        "metric": "input rows/sec aggregated (whole node) + achieved HBM GB/s vs peak",
+        "value": value_rows_s,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device",
+        "config": {
+            "workload": "C2: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
+                        "(truncated geometric), L0=8, Linf=2",
+            "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
+            "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": {"sketch": "k_pair_sketch", "rows": "k_pair_rows", "reduce": "k_reduce_pairs",
+                       "select": "k_select+compact+noise", "exchange": "rccl"}.get(dom, dom),
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+        },
+        "path_roofline": {
+            "achieved": path_bytes / (ms_per_step * 1e-3) / 1e9,
+            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "bytes_per_step": path_bytes,
+        },
+        "stage_ms": stages,
+        "partitions_kept": kept,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,209 @@
+/*
+ * pipelinedp_amd.h — C ABI of the MI355X (gfx950) DPEngine.aggregate hot path.
+ *
+ * The reference (lagodiuk/PipelineDP 0.2.2rc2) is pure Python and has no C ABI;
+ * every entry point below replaces one stage of the reference's LocalBackend
+ * execution of DPEngine._aggregate (pipeline_dp/dp_engine.py:109-187).  The
+ * citation above each function names the reference code it replaces.
+ *
+ * Conventions
+ *  - Every function returns 0 on success and a negative PDP_E_* code on
+ *    failure; pdp_last_error() returns a thread-local message.  No C++
+ *    exception crosses this boundary.
+ *  - All array arguments are DEVICE pointers owned by the caller (allocated by
+ *    hipMalloc or by torch-ROCm).  `stream` is a hipStream_t passed as void*;
+ *    NULL means the legacy default stream.  Nothing here synchronises the
+ *    stream or allocates memory, so the sequence can be captured in a hipGraph.
+ *  - Keys are dense: privacy ids in [0, n_privacy_ids), partition keys in
+ *    [0, n_partitions).  The Python host layer dictionary-encodes other keys.
+ */
+#ifndef PIPELINEDP_AMD_H_
+#define PIPELINEDP_AMD_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDP_ABI_VERSION 1
+
+/* error codes */
+#define PDP_OK 0
+#define PDP_E_INVALID (-1)   /* bad argument / shape */
+#define PDP_E_HIP (-2)       /* a HIP runtime call failed */
+#define PDP_E_WORKSPACE (-3) /* workspace too small */
+#define PDP_E_UNSUPPORTED (-4)
+
+/* value column kinds */
+#define PDP_VALUE_NONE 0
+#define PDP_VALUE_F64 1
+#define PDP_VALUE_I64 2
+
+/* accumulator flags (pdp_bound_config.flags) */
+#define PDP_ACC_SUM 0x1            /* SumCombiner: sum of clipped values */
+#define PDP_ACC_NSUM 0x2           /* Mean/Variance: sum of (clip(v) - middle) */
+#define PDP_ACC_NSUM2 0x4          /* Variance: sum of (clip(v) - middle)^2 */
+#define PDP_SUM_PER_PARTITION 0x8  /* SumCombiner bounds_per_partition: clip(sum_pair) */
+#define PDP_SUM_INT 0x10           /* SUM accumulator is int64 (int values, int bounds) */
+
+/* One shard's contribution-bounding configuration. */
+typedef struct pdp_bound_config {
+  int64_t n_rows;        /* rows in this shard (< 2^32) */
+  int64_t n_privacy_ids; /* U: privacy ids are dense in [0, U) */
+  int64_t n_partitions;  /* P: partition keys are dense in [0, P) (< 2^32) */
+  int32_t l0;            /* max_partitions_contributed (1..PDP_MAX_L0) */
+  int32_t linf;          /* max_contributions_per_partition (1..PDP_MAX_LINF); 0 = keep all rows */
+  int32_t value_kind;    /* PDP_VALUE_* */
+  int32_t flags;         /* PDP_ACC_* | PDP_SUM_* */
+  double min_value;      /* per-value clipping bounds (SUM/MEAN/VARIANCE) */
+  double max_value;
+  double middle;         /* min_value + (max_value - min_value) / 2 */
+  double min_sum;        /* per-partition SUM bounds (PDP_SUM_PER_PARTITION) */
+  double max_sum;
+  int64_t row_offset;    /* global index of this shard's row 0 (row priorities) */
+  uint64_t seed;         /* sampling seed */
+} pdp_bound_config;
+
+#define PDP_MAX_L0 256
+#define PDP_MAX_LINF 256
+
+/* Per-partition accumulators, dense arrays of length n_partitions.  They are
+ * the columnar form of CompoundCombiner's accumulator (combiners.py:749-764):
+ * row_count, then the children's accumulators. */
+typedef struct pdp_partition_accumulators {
+  int64_t* privacy_id_count; /* kept (privacy_id, partition) pairs = row_count */
+  int64_t* count;            /* CountCombiner / Mean / Variance count */
+  void* sum;                 /* SumCombiner: double, or int64 with PDP_SUM_INT */
+  double* normalized_sum;    /* Mean/Variance: sum(clip(v) - middle) */
+  double* normalized_sum_sq; /* Variance: sum((clip(v) - middle)^2) */
+} pdp_partition_accumulators;
+
+int pdp_abi_version(void);
+const char* pdp_last_error(void);
+
+/* Bytes of device workspace pdp_bound_contributions needs for `cfg`. */
+int pdp_bound_workspace_bytes(const pdp_bound_config* cfg, uint64_t* bytes);
+
+/* Contribution bounding: per privacy id keep at most l0 distinct partitions,
+ * per (privacy id, partition) keep at most linf rows, both uniform samples
+ * without replacement drawn with counter-based hash priorities.
+ * Replaces SamplingCrossAndPerPartitionContributionBounder.bound_contributions
+ * (contribution_bounders.py:72-111) and, with linf = 0,
+ * SamplingCrossPartitionContributionBounder (contribution_bounders.py:168-201),
+ * i.e. LocalBackend.sample_fixed_per_key (pipeline_backend.py:531-547) twice.
+ * `pk_allowed` (nullable, u8[n_partitions]) drops rows of non-public
+ * partitions first (DPEngine._drop_partitions, dp_engine.py:290-296).
+ * The workspace is fully (re)initialised on `stream` by this call. */
+int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_id,
+                            const int64_t* partition_key, const void* value,
+                            const uint8_t* pk_allowed, void* workspace,
+                            uint64_t workspace_bytes, void* stream);
+
+/* The two phases of pdp_bound_contributions, exposed so that each kernel can
+ * be timed on its own: pdp_bound_sketch (re)initialises the workspace and
+ * builds the per-privacy-id bottom-l0 sketch ("Sample per privacy_id");
+ * pdp_bound_rows counts the rows of every kept pair and keeps its bottom-linf
+ * rows ("Sample per (privacy_id, partition_key)").  Same arguments as above. */
+int pdp_bound_sketch(const pdp_bound_config* cfg, const int64_t* privacy_id,
+                     const int64_t* partition_key, const uint8_t* pk_allowed, void* workspace,
+                     uint64_t workspace_bytes, void* stream);
+int pdp_bound_rows(const pdp_bound_config* cfg, const int64_t* privacy_id,
+                   const int64_t* partition_key, const void* value, const uint8_t* pk_allowed,
+                   void* workspace, uint64_t workspace_bytes, void* stream);
+
+/* Per-pair accumulators (CompoundCombiner.create_accumulator on the sampled
+ * values, combiners.py:749-753) merged per partition key
+ * (LocalBackend.combine_accumulators_per_key, pipeline_backend.py:555-565).
+ * `acc` arrays are ADDED to (zero them first, or chain shards). */
+int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value,
+                          const void* workspace, uint64_t workspace_bytes,
+                          const pdp_partition_accumulators* acc, void* stream);
+
+/* partition selection strategies */
+#define PDP_SELECT_ALL_NONEMPTY 0 /* keep every partition with row_count > 0 */
+#define PDP_SELECT_TRUNCATED_GEOMETRIC 1
+#define PDP_SELECT_LAPLACE_THRESHOLDING 2
+#define PDP_SELECT_GAUSSIAN_THRESHOLDING 3
+#define PDP_SELECT_PUBLIC 4       /* keep partitions with public_mask[p] != 0 */
+
+typedef struct pdp_select_config {
+  int64_t n_partitions;          /* length of the slice */
+  int64_t partition_offset;      /* global index of slice element 0 (RNG counter) */
+  int32_t strategy;              /* PDP_SELECT_* */
+  int32_t max_rows_per_privacy_id; /* n = ceil(row_count / this), dp_engine.py:346-353 */
+  int32_t pre_threshold;         /* 0 = none */
+  int32_t keep_table_len;        /* truncated geometric: keep_prob[0..len-1] */
+  const double* keep_prob;       /* device; prob of keep for n; n >= len uses [len-1] */
+  double noise_scale;            /* Laplace b or Gaussian sigma (thresholding) */
+  double threshold;              /* thresholding strategies */
+  const uint8_t* public_mask;    /* PDP_SELECT_PUBLIC */
+  uint64_t seed;
+} pdp_select_config;
+
+/* Private partition selection (dp_engine.py:315-371 → PyDP
+ * create_partition_strategy(...).should_keep / noised_value_if_should_keep,
+ * partition_selection.py:29-44).  Writes keep[p] in {0,1}; if `noised_count`
+ * is non-NULL the thresholding strategies also write the noised
+ * privacy-unit count (PostAggregationThresholdingCombiner, combiners.py:353-357). */
+int pdp_select_partitions(const pdp_select_config* cfg, const int64_t* row_count,
+                          uint8_t* keep, double* noised_count, void* stream);
+
+/* Stream compaction of keep flags into ascending partition indices.
+ * `out_count` (device int64[1]) receives the number kept.  Workspace bytes:
+ * pdp_compact_workspace_bytes. */
+int pdp_compact_workspace_bytes(int64_t n, uint64_t* bytes);
+int pdp_compact(const uint8_t* keep, int64_t n, int64_t* out_index, int64_t* out_count,
+                void* workspace, uint64_t workspace_bytes, void* stream);
+
+/* metric operations (one per combiner in CompoundCombiner order) */
+#define PDP_OP_COUNT 1            /* CountCombiner.compute_metrics, combiners.py:262-263 */
+#define PDP_OP_SUM 2              /* SumCombiner, combiners.py:416-417 */
+#define PDP_OP_PRIVACY_ID_COUNT 3 /* PrivacyIdCountCombiner, combiners.py:304-305 */
+#define PDP_OP_MEAN 4             /* MeanCombiner + MeanMechanism, dp_computations.py:562-568 */
+#define PDP_OP_VARIANCE 5         /* VarianceCombiner + compute_dp_var, dp_computations.py:306-365 */
+#define PDP_OP_THRESHOLDED_PID 6  /* PostAggregationThresholdingCombiner: copy noised_count */
+
+#define PDP_NOISE_LAPLACE 0
+#define PDP_NOISE_GAUSSIAN 1
+
+typedef struct pdp_metric_op {
+  int32_t kind;        /* PDP_OP_* */
+  int32_t noise_kind;  /* PDP_NOISE_* */
+  int32_t out_col[4];  /* output column for each produced metric, -1 = not produced.
+                          COUNT/SUM/PID: [0]; MEAN: mean,count,sum;
+                          VARIANCE: variance,count,sum,mean */
+  double scale[3];     /* noise parameter per mechanism (b or sigma):
+                          COUNT/SUM/PID: [0]; MEAN: count,nsum;
+                          VARIANCE: count,nsum,nsum2 */
+  double middle;       /* MEAN/VARIANCE: middle of [min_value, max_value] */
+  double min_value;    /* VARIANCE: for min_value == max_value shortcut */
+  double sq_min_value; /* VARIANCE: lower end of the squares interval */
+  int32_t degenerate;  /* VARIANCE: min_value == max_value */
+  int32_t pad;
+} pdp_metric_op;
+
+#define PDP_MAX_OPS 8
+
+/* Noise + compute_metrics for the kept partitions (CompoundCombiner.
+ * compute_metrics, combiners.py:766-788).  For each i < n_kept with
+ * p = index[i]: out[col * out_stride + i] = metric value (double).
+ * `n_kept_dev` (device int64[1], nullable) bounds i on device when n_kept is
+ * only known on device; pass n_kept = capacity then. */
+int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* index,
+                      int64_t n_kept, const int64_t* n_kept_dev, int64_t partition_offset,
+                      const pdp_partition_accumulators* acc, int32_t sum_is_int,
+                      const double* noised_count, double* out, int64_t out_stride,
+                      uint64_t seed, void* stream);
+
+/* Device error word: the bounding kernels set bit 0 when a key is outside
+ * [0, n_privacy_ids) x [0, n_partitions) (the row is skipped, never read out
+ * of bounds).  Reads it from the workspace of pdp_bound_contributions
+ * (synchronises `stream`). */
+int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PIPELINEDP_AMD_H_ */

@@ -1,0 +1,180 @@
+"""TEST INFRASTRUCTURE — regenerate tests/golden/*.json by running the reference.
+
+Runs only in the build container (it reads /root/reference, which never travels
+to the GPU box).  The reference imports with the python-dp stand-in in
+oracle/pydp_standin (PyDP is not installed; no permission denial was involved).
+
+For every case the reference's DPEngine.aggregate runs on LocalBackend with
+* CompoundCombiner.compute_metrics patched to return the raw accumulator
+  (pre-noise, exact), and
+* private partition selection patched to keep every partition,
+on inputs where no contribution sampling fires (every pid has <= L0 distinct
+partitions and every (pid, pk) <= Linf rows), so the expected per-partition
+accumulators are deterministic.  Sampling itself is pinned with inclusion
+counts of LocalBackend.sample_fixed_per_key under np.random.seed.
+
+Usage: python -m oracle.gen_golden   (from the repo root)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REFERENCE = "/root/reference"
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def _import_reference():
+    for p in (os.path.join(ROOT, "oracle", "pydp_standin"), ROOT, REFERENCE):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import pipeline_dp
+    return pipeline_dp
+
+
+def _py(x):
+    if isinstance(x, (tuple, list)):
+        return [_py(v) for v in x]
+    if isinstance(x, (np.integer,)):
+        return int(x)
+    if isinstance(x, (np.floating,)):
+        return float(x)
+    return x
+
+
+def _no_sampling_rows(rng, n_pids, l0, linf, n_partitions, value_fn, pid_fmt=None, pk_fmt=None):
+    rows = []
+    for u in range(n_pids):
+        d = int(rng.integers(1, l0 + 1))
+        pks = rng.choice(n_partitions, size=d, replace=False)
+        for k in pks:
+            for _ in range(int(rng.integers(1, linf + 1))):
+                pid = pid_fmt(u) if pid_fmt else u
+                pk = pk_fmt(int(k)) if pk_fmt else int(k)
+                rows.append([pid, pk, value_fn(rng)])
+    order = rng.permutation(len(rows))
+    return [rows[i] for i in order]
+
+
+CASES = [
+    dict(name="count_sum_int_movie", metrics=["COUNT", "SUM"], noise="LAPLACE", l0=2, linf=1,
+         min_value=1, max_value=5, n_pids=400, n_partitions=60, value="int1_5"),
+    dict(name="count_sum_mean_f64", metrics=["COUNT", "SUM", "MEAN"], noise="LAPLACE", l0=3, linf=2,
+         min_value=0.0, max_value=10.0, n_pids=500, n_partitions=80, value="normal5_3"),
+    dict(name="variance_pid_count", metrics=["VARIANCE", "PRIVACY_ID_COUNT"], noise="GAUSSIAN", l0=4,
+         linf=2, min_value=0.0, max_value=10.0, n_pids=300, n_partitions=50, value="normal5_4"),
+    dict(name="mean_variance_all", metrics=["VARIANCE", "MEAN", "COUNT", "SUM"], noise="LAPLACE", l0=2,
+         linf=3, min_value=-2.0, max_value=6.0, n_pids=300, n_partitions=40, value="normal2_3"),
+    dict(name="sum_per_partition_int", metrics=["SUM", "COUNT"], noise="LAPLACE", l0=3, linf=2,
+         min_sum=-3, max_sum=7, n_pids=300, n_partitions=30, value="int_m4_9"),
+    dict(name="privacy_id_count_only", metrics=["PRIVACY_ID_COUNT"], noise="LAPLACE", l0=2, linf=1,
+         n_pids=300, n_partitions=40, value="int1_5", rows_per_pair=4),
+    dict(name="public_partitions", metrics=["COUNT", "SUM", "PRIVACY_ID_COUNT"], noise="LAPLACE", l0=2,
+         linf=2, min_value=0, max_value=4, n_pids=200, n_partitions=30, value="int1_5",
+         public=[0, 1, 2, 3, 5, 8, 13, 21, 34, 55, 89]),
+    dict(name="string_keys", metrics=["COUNT", "SUM"], noise="LAPLACE", l0=2, linf=2, min_value=0.0,
+         max_value=3.0, n_pids=150, n_partitions=20, value="normal1_1", string_keys=True),
+]
+
+VALUE_FNS = {
+    "int1_5": lambda r: int(r.integers(1, 6)),
+    "int_m4_9": lambda r: int(r.integers(-4, 10)),
+    "normal5_3": lambda r: float(r.normal(5, 3)),
+    "normal5_4": lambda r: float(r.normal(5, 4)),
+    "normal2_3": lambda r: float(r.normal(2, 3)),
+    "normal1_1": lambda r: float(r.normal(1, 1)),
+}
+
+
+def run_case(pdp, case, seed):
+    from pipeline_dp import combiners, partition_selection
+
+    rng = np.random.default_rng(seed)
+    fmt_pid = (lambda u: f"user-{u}") if case.get("string_keys") else None
+    fmt_pk = (lambda k: f"item/{k}") if case.get("string_keys") else None
+    if case.get("rows_per_pair"):
+        rows = _no_sampling_rows(rng, case["n_pids"], case["l0"], case["rows_per_pair"],
+                                 case["n_partitions"], VALUE_FNS[case["value"]], fmt_pid, fmt_pk)
+    else:
+        rows = _no_sampling_rows(rng, case["n_pids"], case["l0"], case["linf"], case["n_partitions"],
+                                 VALUE_FNS[case["value"]], fmt_pid, fmt_pk)
+    kw = {}
+    for k in ("min_value", "max_value", "min_sum", "max_sum"):
+        if k in case:
+            kw[{"min_sum": "min_sum_per_partition", "max_sum": "max_sum_per_partition"}.get(k, k)] = case[k]
+    params = pdp.AggregateParams(metrics=[getattr(pdp.Metrics, m) for m in case["metrics"]],
+                                 noise_kind=getattr(pdp.NoiseKind, case["noise"]),
+                                 max_partitions_contributed=case["l0"],
+                                 max_contributions_per_partition=case["linf"], **kw)
+    accountant = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+    engine = pdp.DPEngine(accountant, pdp.LocalBackend())
+    extractors = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0],
+                                    partition_extractor=lambda r: r[1],
+                                    value_extractor=lambda r: r[2])
+
+    class KeepAll:
+
+        def should_keep(self, n):
+            return True
+
+    saved_cm = combiners.CompoundCombiner.compute_metrics
+    saved_ps = partition_selection.create_partition_selection_strategy
+    combiners.CompoundCombiner.compute_metrics = lambda self, acc: acc
+    partition_selection.create_partition_selection_strategy = lambda *a, **k: KeepAll()
+    try:
+        public = case.get("public")
+        out = engine.aggregate(rows, params, extractors, public_partitions=public)
+        accountant.compute_budgets()
+        result = sorted(([_py(pk), _py(acc)] for pk, acc in out), key=lambda t: str(t[0]))
+    finally:
+        combiners.CompoundCombiner.compute_metrics = saved_cm
+        partition_selection.create_partition_selection_strategy = saved_ps
+    budgets = [[m.mechanism_spec.mechanism_type.value, m.mechanism_spec.eps, m.mechanism_spec.delta]
+               for m in accountant._mechanisms]
+    return {"name": case["name"], "case": case, "rows": rows, "expected": result, "budgets": budgets}
+
+
+def sampling_fixture(pdp, trials=4000):
+    """Inclusion counts of the reference's sampling under np.random.seed."""
+    backend = pdp.LocalBackend()
+    np.random.seed(2024)
+    linf_counts = [0] * 5
+    for _ in range(trials):
+        for _, vals in backend.sample_fixed_per_key([("k", i) for i in range(5)], 2):
+            for v in vals:
+                linf_counts[v] += 1
+    from pipeline_dp import contribution_bounders
+    from pipeline_dp.report_generator import ReportGenerator
+
+    class P:
+        max_partitions_contributed = 2
+        max_contributions_per_partition = 1
+
+    l0_counts = [0] * 6
+    rows = [("u", k, 1.0) for k in range(6)]
+    for _ in range(trials):
+        out = contribution_bounders.SamplingCrossAndPerPartitionContributionBounder().bound_contributions(
+            rows, P, backend, ReportGenerator(None, "t"), lambda v: len(v))
+        for (pid, pk), _ in out:
+            l0_counts[pk] += 1
+    return {"trials": trials, "linf": {"rows": 5, "n": 2, "counts": linf_counts},
+            "l0": {"partitions": 6, "n": 2, "counts": l0_counts}}
+
+
+def main():
+    pdp = _import_reference()
+    os.makedirs(OUT, exist_ok=True)
+    for i, case in enumerate(CASES):
+        fx = run_case(pdp, case, seed=100 + i)
+        with open(os.path.join(OUT, f"{case['name']}.json"), "w") as f:
+            json.dump(fx, f)
+        print(case["name"], len(fx["rows"]), "rows", len(fx["expected"]), "partitions")
+    with open(os.path.join(OUT, "sampling_inclusion.json"), "w") as f:
+        json.dump(sampling_fixture(pdp), f)
+    print("sampling_inclusion written")
+
+
+if __name__ == "__main__":
+    main()

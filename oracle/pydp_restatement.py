@@ -1,0 +1,180 @@
+"""TEST INFRASTRUCTURE — restatement of the python-dp (PyDP) arithmetic.
+
+The reference imports PyDP (`python-dp~=1.1.5rc4`, requirements.dev.txt:15),
+a pybind11 wrapper over Google's differential-privacy C++ library.  PyDP is not
+vendored in /root/reference and is not installed here, so its published
+algorithms are restated from the library's documented behaviour and pinned
+against the known answers the reference's own tests hold:
+
+* GaussianMechanism(eps, delta, l2).std — analytic-Gaussian calibration, doubling
+  then bisection to 1e-3 relative, returning the upper end (reproduces 114.375,
+  88.06640625, 17.1826171875, 16.9125, 277.34375, 18.662109375,
+  37.53742639189524 exactly).
+* LaplaceMechanism(epsilon, sensitivity).diversity = sensitivity / epsilon.
+* create_partition_strategy("truncated_geometric" | "laplace" | "gaussian",
+  eps, delta, l0[, pre_threshold]) with should_keep / probability_of_keep /
+  noised_value_if_should_keep / threshold.
+  Parity unpinned: per-partition delta for l0 > 1 (1-(1-delta)^(1/l0) here),
+  pre_threshold for the thresholding strategies, PyDP's secure (granular)
+  noise samplers — checked distributionally only.
+
+Independent of pipelinedp_amd (this is the checker, not the product).
+"""
+import math
+
+import numpy as np
+
+_rng = np.random.default_rng()
+
+
+def _phi(x):
+    return 0.5 * math.erfc(-x / math.sqrt(2.0))
+
+
+def _gauss_delta(sigma, eps, l2):
+    a = l2 / (2.0 * sigma)
+    b = eps * sigma / l2
+    return _phi(a - b) - math.exp(eps) * _phi(-a - b)
+
+
+def calibrate_gaussian_sigma(eps, delta, l2):
+    lo, hi = 0.0, float(l2)
+    while _gauss_delta(hi, eps, l2) > delta:
+        lo, hi = hi, hi * 2.0
+    while hi - lo > 1e-3 * lo:
+        mid = lo * 0.5 + hi * 0.5
+        if _gauss_delta(mid, eps, l2) > delta:
+            lo = mid
+        else:
+            hi = mid
+    return hi
+
+
+class LaplaceMechanism:
+
+    def __init__(self, epsilon, sensitivity=1.0):
+        self.epsilon = float(epsilon)
+        self.sensitivity = float(sensitivity)
+        self.diversity = self.sensitivity / self.epsilon
+
+    def add_noise(self, value):
+        return float(value) + float(_rng.laplace(0.0, self.diversity))
+
+
+class GaussianMechanism:
+
+    def __init__(self, epsilon, delta, sensitivity=1.0):
+        self.epsilon = float(epsilon)
+        self.delta = float(delta)
+        self.sensitivity = float(sensitivity)
+        self.std = calibrate_gaussian_sigma(self.epsilon, self.delta, self.sensitivity)
+
+    @classmethod
+    def create_from_standard_deviation(cls, std):
+        m = cls.__new__(cls)
+        m.epsilon, m.delta, m.sensitivity, m.std = 0.0, 0.0, 0.0, float(std)
+        return m
+
+    def add_noise(self, value):
+        return float(value) + float(_rng.normal(0.0, self.std))
+
+
+def adjusted_delta(delta, l0):
+    return -math.expm1(math.log1p(-delta) / l0)
+
+
+_tg_cache = {}
+
+
+def truncated_geometric_table(eps, delta, l0):
+    key = (eps, delta, l0)
+    if key not in _tg_cache:
+        e, d = eps / l0, adjusted_delta(delta, l0)
+        p, table = 0.0, [0.0]
+        while p < 1.0 and len(table) < (1 << 22) and d > 0:
+            p = min(math.exp(e) * p + d, 1.0 - math.exp(-e) * (1.0 - p - d), 1.0)
+            table.append(p)
+        _tg_cache[key] = table
+    return _tg_cache[key]
+
+
+class _Strategy:
+
+    def __init__(self, epsilon, delta, l0, pre_threshold=None):
+        self.epsilon, self.delta, self.max_partitions_contributed = epsilon, delta, l0
+        self.pre_threshold = pre_threshold
+
+    def _shift(self, n):
+        if self.pre_threshold:
+            if n < self.pre_threshold:
+                return None
+            return n - (self.pre_threshold - 1)
+        return n
+
+
+class TruncatedGeometricStrategy(_Strategy):
+
+    def probability_of_keep(self, n):
+        n = self._shift(n)
+        if n is None or n <= 0:
+            return 0.0
+        t = truncated_geometric_table(self.epsilon, self.delta, self.max_partitions_contributed)
+        return t[min(int(n), len(t) - 1)]
+
+    def should_keep(self, n):
+        return _rng.random() < self.probability_of_keep(n)
+
+
+class _ThresholdingStrategy(_Strategy):
+    threshold = 0.0
+
+    def _noise(self):
+        raise NotImplementedError
+
+    def noised_value_if_should_keep(self, n):
+        m = self._shift(n)
+        if m is None:
+            return None
+        v = m + self._noise()
+        if v > self.threshold:
+            return v + (n - m)
+        return None
+
+    def should_keep(self, n):
+        return self.noised_value_if_should_keep(n) is not None
+
+
+class LaplaceThresholdingStrategy(_ThresholdingStrategy):
+
+    def __init__(self, epsilon, delta, l0, pre_threshold=None):
+        super().__init__(epsilon, delta, l0, pre_threshold)
+        self.diversity = l0 / epsilon
+        d = adjusted_delta(delta, l0)
+        if d > 0.5:
+            self.threshold = 1.0 + self.diversity * math.log(2.0 * (1.0 - d))
+        else:
+            self.threshold = 1.0 - self.diversity * math.log(2.0 * d)
+
+    def _noise(self):
+        return float(_rng.laplace(0.0, self.diversity))
+
+
+class GaussianThresholdingStrategy(_ThresholdingStrategy):
+
+    def __init__(self, epsilon, delta, l0, pre_threshold=None):
+        super().__init__(epsilon, delta, l0, pre_threshold)
+        from scipy.special import ndtri
+        noise_delta = delta / 2
+        self.sigma = calibrate_gaussian_sigma(epsilon, noise_delta, math.sqrt(l0))
+        d = adjusted_delta(delta - noise_delta, l0)
+        self.threshold = 1.0 - self.sigma * float(ndtri(d))
+
+    def _noise(self):
+        return float(_rng.normal(0.0, self.sigma))
+
+
+def create_partition_strategy(name, epsilon, delta, max_partitions_contributed, pre_threshold=None):
+    cls = {"truncated_geometric": TruncatedGeometricStrategy,
+           "laplace": LaplaceThresholdingStrategy,
+           "gaussian": GaussianThresholdingStrategy}[name]
+    return cls(epsilon, delta, max_partitions_contributed, pre_threshold)

@@ -1,0 +1,173 @@
+"""ctypes binding of the C ABI in include/pipelinedp_amd.h.
+
+The library is built in-tree (``__graft_entry__.build()``) as
+``pipelinedp_amd/lib/libpipelinedp_amd.so``.  There is no CPU fallback: if
+the library is missing or fails to load, :func:`lib` raises
+:class:`NativeLibraryError`.
+
+torch is imported before the library is loaded so that the library binds to
+the same ``libamdhip64.so.7`` instance torch uses (both carry that SONAME);
+device pointers and stream handles from torch are then valid here.
+"""
+import ctypes
+import os
+import threading
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                        "libpipelinedp_amd.so")
+
+# constants (include/pipelinedp_amd.h)
+ABI_VERSION = 1
+VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
+ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
+SELECT_ALL_NONEMPTY = 0
+SELECT_TRUNCATED_GEOMETRIC = 1
+SELECT_LAPLACE_THRESHOLDING = 2
+SELECT_GAUSSIAN_THRESHOLDING = 3
+SELECT_PUBLIC = 4
+OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID = 1, 2, 3, 4, 5, 6
+NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
+MAX_L0 = 256
+MAX_LINF = 256
+MAX_OPS = 8
+
+EXPORTED_SYMBOLS = (
+    "pdp_abi_version",
+    "pdp_last_error",
+    "pdp_bound_workspace_bytes",
+    "pdp_bound_contributions",
+    "pdp_bound_sketch",
+    "pdp_bound_rows",
+    "pdp_reduce_partitions",
+    "pdp_select_partitions",
+    "pdp_compact_workspace_bytes",
+    "pdp_compact",
+    "pdp_noise_metrics",
+    "pdp_bound_error_flags",
+)
+
+
+class NativeLibraryError(RuntimeError):
+    """The HIP library is missing, failed to load, or returned an error."""
+
+
+class BoundConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", ctypes.c_int64),
+        ("n_privacy_ids", ctypes.c_int64),
+        ("n_partitions", ctypes.c_int64),
+        ("l0", ctypes.c_int32),
+        ("linf", ctypes.c_int32),
+        ("value_kind", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("min_value", ctypes.c_double),
+        ("max_value", ctypes.c_double),
+        ("middle", ctypes.c_double),
+        ("min_sum", ctypes.c_double),
+        ("max_sum", ctypes.c_double),
+        ("row_offset", ctypes.c_int64),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class PartitionAccumulators(ctypes.Structure):
+    _fields_ = [
+        ("privacy_id_count", ctypes.c_void_p),
+        ("count", ctypes.c_void_p),
+        ("sum", ctypes.c_void_p),
+        ("normalized_sum", ctypes.c_void_p),
+        ("normalized_sum_sq", ctypes.c_void_p),
+    ]
+
+
+class SelectConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_partitions", ctypes.c_int64),
+        ("partition_offset", ctypes.c_int64),
+        ("strategy", ctypes.c_int32),
+        ("max_rows_per_privacy_id", ctypes.c_int32),
+        ("pre_threshold", ctypes.c_int32),
+        ("keep_table_len", ctypes.c_int32),
+        ("keep_prob", ctypes.c_void_p),
+        ("noise_scale", ctypes.c_double),
+        ("threshold", ctypes.c_double),
+        ("public_mask", ctypes.c_void_p),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class MetricOp(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("noise_kind", ctypes.c_int32),
+        ("out_col", ctypes.c_int32 * 4),
+        ("scale", ctypes.c_double * 3),
+        ("middle", ctypes.c_double),
+        ("min_value", ctypes.c_double),
+        ("sq_min_value", ctypes.c_double),
+        ("degenerate", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+    ]
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    P = ctypes.POINTER
+    vp, i64, u64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32
+    sig = {
+        "pdp_abi_version": (ctypes.c_int, []),
+        "pdp_last_error": (ctypes.c_char_p, []),
+        "pdp_bound_workspace_bytes": (ctypes.c_int, [P(BoundConfig), P(u64)]),
+        "pdp_bound_contributions": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, vp, u64, vp]),
+        "pdp_bound_sketch": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, u64, vp]),
+        "pdp_bound_rows": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, vp, u64, vp]),
+        "pdp_reduce_partitions": (ctypes.c_int, [P(BoundConfig), vp, vp, u64, P(PartitionAccumulators), vp]),
+        "pdp_select_partitions": (ctypes.c_int, [P(SelectConfig), vp, vp, vp, vp]),
+        "pdp_compact_workspace_bytes": (ctypes.c_int, [i64, P(u64)]),
+        "pdp_compact": (ctypes.c_int, [vp, i64, vp, vp, vp, u64, vp]),
+        "pdp_noise_metrics": (ctypes.c_int, [P(MetricOp), i32, vp, i64, vp, i64,
+                                             P(PartitionAccumulators), i32, vp, vp, i64, u64, vp]),
+        "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """Loads (once) and returns the native library; raises NativeLibraryError."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryError(
+                f"HIP library not built: {LIB_PATH} is missing. Run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` first. "
+                "pipelinedp_amd has no CPU fallback.")
+        import torch  # noqa: F401  (bind to torch's libamdhip64.so.7 first)
+        try:
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:
+            raise NativeLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        missing = [s for s in EXPORTED_SYMBOLS if not hasattr(handle, s)]
+        if missing:
+            raise NativeLibraryError(f"{LIB_PATH} lacks symbols {missing}")
+        _declare(handle)
+        if handle.pdp_abi_version() != ABI_VERSION:
+            raise NativeLibraryError("ABI version mismatch; rebuild the library")
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().pdp_last_error()
+        msg = msg.decode() if msg else ""
+        raise NativeLibraryError(f"{what} failed with code {rc}: {msg}")

@@ -1,0 +1,463 @@
+"""Host-side DP arithmetic: sensitivities, noise calibration, selection thresholds.
+
+Mirrors pipeline_dp/dp_computations.py (reference) for the functions on the
+aggregate path, and restates the arithmetic the reference delegates to
+python-dp (PyDP ~=1.1.5rc4, Google differential-privacy C++):
+
+* Gaussian sigma calibration (PyDP GaussianMechanism(eps, delta, l2).std,
+  called at dp_computations.py:116, 489-491): analytic-Gaussian delta(sigma),
+  doubling then bisection until hi - lo <= 1e-3 * lo, returning hi.
+* Laplace diversity b = l1 / eps (PyDP LaplaceMechanism.diversity,
+  dp_computations.py:439-440, 461).
+* Partition selection (partition_selection.py:29-44 -> PyDP
+  create_partition_strategy): truncated-geometric keep probability,
+  Laplace / Gaussian thresholding thresholds.
+
+These are scalars computed once per aggregation on the host; the per-partition
+work (noise draws, keep decisions) runs in the HIP kernels.
+"""
+import dataclasses
+import math
+from typing import Any, List, Optional, Tuple
+
+import numpy as np
+
+from pipelinedp_amd import aggregate_params as agg
+
+
+@dataclasses.dataclass
+class ScalarNoiseParams:
+    """dp_computations.py:28-60."""
+    eps: float
+    delta: float
+    min_value: Optional[float]
+    max_value: Optional[float]
+    min_sum_per_partition: Optional[float]
+    max_sum_per_partition: Optional[float]
+    max_partitions_contributed: int
+    max_contributions_per_partition: Optional[int]
+    noise_kind: agg.NoiseKind
+
+    def __post_init__(self):
+        assert (self.min_value is None) == (self.max_value is None), \
+            "min_value and max_value should be or both set or both None."
+        assert (self.min_sum_per_partition is None) == (self.max_sum_per_partition is None), \
+            "min_sum_per_partition and max_sum_per_partition should be or both set or both None."
+
+    def l0_sensitivity(self) -> int:
+        return self.max_partitions_contributed
+
+    @property
+    def bounds_per_contribution_are_set(self) -> bool:
+        return self.min_value is not None and self.max_value is not None
+
+    @property
+    def bounds_per_partition_are_set(self) -> bool:
+        return self.min_sum_per_partition is not None and self.max_sum_per_partition is not None
+
+
+def compute_squares_interval(min_value: float, max_value: float) -> Tuple[float, float]:
+    """dp_computations.py:63-68."""
+    if min_value < 0 < max_value:
+        return 0, max(min_value**2, max_value**2)
+    return min_value**2, max_value**2
+
+
+def compute_middle(min_value: float, max_value: float) -> float:
+    """dp_computations.py:71-75 (overflow-safe midpoint)."""
+    return min_value + (max_value - min_value) / 2
+
+
+def compute_l1_sensitivity(l0_sensitivity: float, linf_sensitivity: float) -> float:
+    return l0_sensitivity * linf_sensitivity
+
+
+def compute_l2_sensitivity(l0_sensitivity: float, linf_sensitivity: float) -> float:
+    return np.sqrt(l0_sensitivity) * linf_sensitivity
+
+
+# ----------------------------------------------------- Gaussian calibration --
+_SIGMA_RELATIVE_ACCURACY = 1e-3
+
+
+def _std_normal_cdf(x: float) -> float:
+    return 0.5 * math.erfc(-x / math.sqrt(2.0))
+
+
+def gaussian_delta(sigma: float, eps: float, l2_sensitivity: float) -> float:
+    """delta of the Gaussian mechanism with std sigma (analytic Gaussian,
+    Balle & Wang 2018): Phi(l2/(2s) - eps s/l2) - e^eps Phi(-l2/(2s) - eps s/l2)."""
+    a = l2_sensitivity / (2.0 * sigma)
+    b = eps * sigma / l2_sensitivity
+    return _std_normal_cdf(a - b) - math.exp(eps) * _std_normal_cdf(-a - b)
+
+
+def compute_sigma(eps: float, delta: float, l2_sensitivity: float) -> float:
+    """Smallest sigma (to 1e-3 relative, rounded up) with gaussian_delta <= delta.
+
+    Restates PyDP GaussianMechanism(eps, delta, l2).std (reference
+    dp_computations.py:106-116); reproduces the reference's known answers
+    114.375, 88.06640625, 17.1826171875, 16.9125, 277.34375, 18.662109375,
+    37.53742639189524 exactly."""
+    if eps <= 0:
+        raise ValueError(f"epsilon must be positive, but {eps} given")
+    if not 0 < delta < 1:
+        raise ValueError(f"delta must be in (0, 1) for the Gaussian mechanism, but {delta} given")
+    if l2_sensitivity <= 0:
+        raise ValueError(f"l2 sensitivity must be positive, but {l2_sensitivity} given")
+    lo, hi = 0.0, float(l2_sensitivity)
+    while gaussian_delta(hi, eps, l2_sensitivity) > delta:
+        lo = hi
+        hi *= 2.0
+    while hi - lo > _SIGMA_RELATIVE_ACCURACY * lo:
+        mid = lo * 0.5 + hi * 0.5
+        if gaussian_delta(mid, eps, l2_sensitivity) > delta:
+            lo = mid
+        else:
+            hi = mid
+    return hi
+
+
+def laplace_diversity(eps: float, l1_sensitivity: float) -> float:
+    if eps <= 0:
+        raise ValueError(f"epsilon must be positive, but {eps} given")
+    return l1_sensitivity / eps
+
+
+def equally_split_budget(eps: float, delta: float, no_mechanisms: int):
+    """dp_computations.py:232-260: equal shares, the last one takes the remainder."""
+    if no_mechanisms <= 0:
+        raise ValueError("The number of mechanisms must be a positive integer.")
+    eps_used = delta_used = 0
+    budgets = []
+    for _ in range(no_mechanisms - 1):
+        budget = (eps / no_mechanisms, delta / no_mechanisms)
+        eps_used += budget[0]
+        delta_used += budget[1]
+        budgets.append(budget)
+    budgets.append((eps - eps_used, delta - delta_used))
+    return budgets
+
+
+# -------------------------------------------------------------- sensitivities --
+@dataclasses.dataclass
+class Sensitivities:
+    """dp_computations.py:578-618."""
+    l0: Optional[int] = None
+    linf: Optional[float] = None
+    l1: Optional[float] = None
+    l2: Optional[float] = None
+
+    def __post_init__(self):
+        def check_is_positive(num: Any, name: str):
+            if num is not None and num <= 0:
+                raise ValueError(f"{name} must be positive, but {num} given.")
+
+        check_is_positive(self.l0, "L0")
+        check_is_positive(self.linf, "Linf")
+        check_is_positive(self.l1, "L1")
+        check_is_positive(self.l2, "L2")
+        if (self.l0 is None) != (self.linf is None):
+            raise ValueError("l0 and linf sensitivities must be either both set or both unset.")
+        if self.l0 is not None and self.linf is not None:
+            l1 = compute_l1_sensitivity(self.l0, self.linf)
+            if self.l1 is None:
+                self.l1 = l1
+            elif abs(l1 - self.l1) > 1e-12:
+                raise ValueError(f"L1={self.l1} != L0*Linf={l1}")
+            l2 = compute_l2_sensitivity(self.l0, self.linf)
+            if self.l2 is None:
+                self.l2 = l2
+            elif abs(l2 - self.l2) > 1e-12:
+                raise ValueError(f"L2={self.l2} != sqrt(L0)*Linf={l2}")
+
+
+def compute_sensitivities_for_count(params) -> Sensitivities:
+    """dp_computations.py:718-724."""
+    if params.max_contributions is not None:
+        return Sensitivities(l1=params.max_contributions, l2=params.max_contributions)
+    return Sensitivities(l0=params.max_partitions_contributed,
+                         linf=params.max_contributions_per_partition)
+
+
+def compute_sensitivities_for_privacy_id_count(params) -> Sensitivities:
+    """dp_computations.py:727-732."""
+    if params.max_contributions is not None:
+        return Sensitivities(l1=params.max_contributions, l2=math.sqrt(params.max_contributions))
+    return Sensitivities(l0=params.max_partitions_contributed, linf=1)
+
+
+def compute_sensitivities_for_sum(params) -> Sensitivities:
+    """dp_computations.py:735-748."""
+    l0_sensitivity = params.max_partitions_contributed
+    max_abs = lambda x, y: max(abs(x), abs(y))
+    if params.bounds_per_contribution_are_set:
+        max_abs_val = max_abs(params.min_value, params.max_value)
+        if params.max_contributions:
+            s = max_abs_val * params.max_contributions
+            return Sensitivities(l1=s, l2=s)
+        linf_sensitivity = max_abs_val * params.max_contributions_per_partition
+    else:
+        linf_sensitivity = max_abs(params.min_sum_per_partition, params.max_sum_per_partition)
+    return Sensitivities(l0=l0_sensitivity, linf=linf_sensitivity)
+
+
+def compute_sensitivities_for_normalized_sum(params) -> Sensitivities:
+    """dp_computations.py:762-771."""
+    max_abs_value = (params.max_value - params.min_value) / 2
+    if params.max_contributions:
+        s = max_abs_value * params.max_contributions
+        return Sensitivities(l1=s, l2=s)
+    return Sensitivities(l0=params.max_partitions_contributed,
+                         linf=max_abs_value * params.max_contributions_per_partition)
+
+
+# -------------------------------------------------------------- mechanisms --
+class AdditiveMechanism:
+    """Noise parameters of an additive mechanism (dp_computations.py:397-537).
+
+    add_noise() draws on the host for single values (API parity, e.g.
+    explain reports and tests); the per-partition noise of aggregate() is
+    drawn on the GPU with the same parameters."""
+
+    noise_kind: agg.NoiseKind
+
+    @property
+    def noise_parameter(self) -> float:
+        raise NotImplementedError
+
+    @property
+    def std(self) -> float:
+        raise NotImplementedError
+
+
+class LaplaceMechanism(AdditiveMechanism):
+
+    def __init__(self, epsilon: float, l1_sensitivity: float):
+        self._epsilon = epsilon
+        self._sensitivity = l1_sensitivity
+        self._diversity = laplace_diversity(epsilon, l1_sensitivity)
+
+    @classmethod
+    def create_from_epsilon(cls, epsilon: float, l1_sensitivity: float) -> "LaplaceMechanism":
+        return LaplaceMechanism(epsilon, l1_sensitivity)
+
+    @classmethod
+    def create_from_std_deviation(cls, normalized_stddev: float, l1_sensitivity: float):
+        b = normalized_stddev / math.sqrt(2)
+        return LaplaceMechanism(1 / b, l1_sensitivity)
+
+    def add_noise(self, value) -> float:
+        return float(value) + float(np.random.default_rng().laplace(0.0, self._diversity))
+
+    @property
+    def noise_kind(self) -> agg.NoiseKind:
+        return agg.NoiseKind.LAPLACE
+
+    @property
+    def noise_parameter(self) -> float:
+        return self._diversity
+
+    @property
+    def std(self) -> float:
+        return self._diversity * math.sqrt(2)
+
+    @property
+    def sensitivity(self) -> float:
+        return self._sensitivity
+
+    def describe(self) -> str:
+        return (f"Laplace mechanism:  parameter={self.noise_parameter}  eps="
+                f"{self._epsilon}  l1_sensitivity={self.sensitivity}")
+
+
+class GaussianMechanism(AdditiveMechanism):
+
+    def __init__(self, sigma: float, l2_sensitivity: float, epsilon: float = 0.0,
+                 delta: float = 0.0):
+        self._sigma = sigma
+        self._l2_sensitivity = l2_sensitivity
+        self._epsilon = epsilon
+        self._delta = delta
+
+    @classmethod
+    def create_from_epsilon_delta(cls, epsilon: float, delta: float, l2_sensitivity: float):
+        return GaussianMechanism(compute_sigma(epsilon, delta, l2_sensitivity), l2_sensitivity,
+                                 epsilon, delta)
+
+    @classmethod
+    def create_from_std_deviation(cls, normalized_stddev: float, l2_sensitivity: float):
+        return GaussianMechanism(normalized_stddev * l2_sensitivity, l2_sensitivity)
+
+    def add_noise(self, value) -> float:
+        return float(value) + float(np.random.default_rng().normal(0.0, self._sigma))
+
+    @property
+    def noise_kind(self) -> agg.NoiseKind:
+        return agg.NoiseKind.GAUSSIAN
+
+    @property
+    def noise_parameter(self) -> float:
+        return self._sigma
+
+    @property
+    def std(self) -> float:
+        return self._sigma
+
+    @property
+    def sensitivity(self) -> float:
+        return self._l2_sensitivity
+
+    def describe(self) -> str:
+        if self._epsilon > 0:
+            eps_delta_str = f"eps={self._epsilon}  delta={self._delta}  "
+        else:
+            eps_delta_str = ""
+        return (f"Gaussian mechanism:  parameter={self.noise_parameter}"
+                f"  {eps_delta_str}l2_sensitivity={self.sensitivity}")
+
+
+def create_additive_mechanism(mechanism_spec, sensitivities: Sensitivities) -> AdditiveMechanism:
+    """dp_computations.py:621-646."""
+    noise_kind = mechanism_spec.mechanism_type.to_noise_kind()
+    if noise_kind == agg.NoiseKind.LAPLACE:
+        if sensitivities.l1 is None:
+            raise ValueError("L1 or (L0 and Linf) sensitivities must be set for Laplace mechanism.")
+        if mechanism_spec.standard_deviation_is_set:
+            return LaplaceMechanism.create_from_std_deviation(mechanism_spec.noise_standard_deviation,
+                                                              sensitivities.l1)
+        return LaplaceMechanism.create_from_epsilon(mechanism_spec.eps, sensitivities.l1)
+    if noise_kind == agg.NoiseKind.GAUSSIAN:
+        if sensitivities.l2 is None:
+            raise ValueError("L2 or (L0 and Linf) sensitivities must be set for Gaussian mechanism.")
+        if mechanism_spec.standard_deviation_is_set:
+            return GaussianMechanism.create_from_std_deviation(
+                mechanism_spec.noise_standard_deviation, sensitivities.l2)
+        return GaussianMechanism.create_from_epsilon_delta(mechanism_spec.eps, mechanism_spec.delta,
+                                                           sensitivities.l2)
+    raise AssertionError(f"{noise_kind} not supported.")
+
+
+class MeanMechanism:
+    """dp_computations.py:540-575 (noise drawn on the GPU, see PDP_OP_MEAN)."""
+
+    def __init__(self, range_middle: float, count_mechanism: AdditiveMechanism,
+                 sum_mechanism: AdditiveMechanism):
+        self._range_middle = range_middle
+        self._count_mechanism = count_mechanism
+        self._sum_mechanism = sum_mechanism
+
+    @property
+    def range_middle(self):
+        return self._range_middle
+
+    @property
+    def count_mechanism(self):
+        return self._count_mechanism
+
+    @property
+    def sum_mechanism(self):
+        return self._sum_mechanism
+
+    def compute_mean(self, count: int, normalized_sum: float):
+        dp_count = self._count_mechanism.add_noise(count)
+        denominator = max(1.0, dp_count)
+        dp_normalized_sum = self._sum_mechanism.add_noise(normalized_sum)
+        dp_mean = self._range_middle + dp_normalized_sum / denominator
+        return dp_count, dp_mean * dp_count, dp_mean
+
+    def describe(self) -> str:
+        return (f"    a. Computed 'normalized_sum' = sum of (value - {self._range_middle})\n"
+                f"    b. Applied to 'count' {self._count_mechanism.describe()}\n"
+                f"    c. Applied to 'normalized_sum' {self._sum_mechanism.describe()}")
+
+
+def create_mean_mechanism(range_middle, count_spec, count_sensitivities, normalized_sum_spec,
+                          normalized_sum_sensitivities) -> MeanMechanism:
+    return MeanMechanism(range_middle, create_additive_mechanism(count_spec, count_sensitivities),
+                         create_additive_mechanism(normalized_sum_spec, normalized_sum_sensitivities))
+
+
+def noise_scale(noise_kind: agg.NoiseKind, eps: float, delta: float, l0: float, linf: float) -> float:
+    """Scale (Laplace b or Gaussian sigma) of _add_random_noise
+    (dp_computations.py:154-183) for (eps, delta, l0, linf)."""
+    if noise_kind == agg.NoiseKind.LAPLACE:
+        return laplace_diversity(eps, compute_l1_sensitivity(l0, linf))
+    if noise_kind == agg.NoiseKind.GAUSSIAN:
+        return compute_sigma(eps, delta, compute_l2_sensitivity(l0, linf))
+    raise ValueError("Noise kind must be either Laplace or Gaussian.")
+
+
+# ---------------------------------------------------------- partition selection --
+def adjusted_delta(delta: float, max_partitions_contributed: int) -> float:
+    """Per-partition delta: 1 - (1 - delta)^(1/l0), computed stably.
+
+    Parity note: for l0 = 1 this is delta exactly; for l0 > 1 the reference's
+    tests cannot distinguish it from delta / l0 (SURVEY §8(c) "parity unpinned")."""
+    return -math.expm1(math.log1p(-delta) / max_partitions_contributed)
+
+
+def truncated_geometric_keep_table(eps: float, delta: float, max_partitions_contributed: int,
+                                   max_len: int = 1 << 22) -> np.ndarray:
+    """pi[n] = probability that truncated-geometric selection keeps a partition
+    with n privacy units (PyDP "truncated_geometric", the optimal (eps, delta)
+    partition selection of Desfontaines et al.), n = 0..len-1; pi[len-1]
+    applies to every larger n.  eps' = eps / l0, delta' = adjusted_delta.
+    Recurrence: pi[0] = 0, pi[n] = min(e^eps' pi[n-1] + delta',
+    1 - e^-eps' (1 - pi[n-1] - delta'), 1)."""
+    if eps <= 0:
+        raise ValueError(f"epsilon must be positive, but {eps} given")
+    if not 0 <= delta < 1:
+        raise ValueError(f"delta must be in [0, 1), but {delta} given")
+    e = eps / max_partitions_contributed
+    d = adjusted_delta(delta, max_partitions_contributed)
+    ee, eme = math.exp(e), math.exp(-e)
+    table = [0.0]
+    p = 0.0
+    while len(table) < max_len:
+        p = min(ee * p + d, 1.0 - eme * (1.0 - p - d), 1.0)
+        table.append(p)
+        if p >= 1.0:
+            break
+        if d == 0.0 and len(table) > 1:  # delta = 0: never keep
+            break
+    return np.asarray(table, dtype=np.float64)
+
+
+def truncated_geometric_keep_probability(n: int, eps: float, delta: float,
+                                         max_partitions_contributed: int,
+                                         pre_threshold: Optional[int] = None) -> float:
+    """PyDP partition_selection strategy .probability_of_keep(n)."""
+    if pre_threshold:
+        if n < pre_threshold:
+            return 0.0
+        n = n - (pre_threshold - 1)
+    table = truncated_geometric_keep_table(eps, delta, max_partitions_contributed)
+    return float(table[min(n, len(table) - 1)])
+
+
+def laplace_thresholding_params(eps: float, delta: float, max_partitions_contributed: int):
+    """(b, threshold) of PyDP "laplace" partition selection:
+    b = l0 / eps, T = 1 - b ln(2 delta') (delta' <= 1/2), 1 + b ln(2 (1 - delta')) otherwise."""
+    b = max_partitions_contributed / eps
+    d = adjusted_delta(delta, max_partitions_contributed)
+    if d > 0.5:
+        return b, 1.0 + b * math.log(2.0 * (1.0 - d))
+    return b, 1.0 - b * math.log(2.0 * d)
+
+
+def _upper_std_normal_quantile(q: float) -> float:
+    """Phi^-1(1 - q), computed as -Phi^-1(q) to keep precision for tiny q."""
+    from scipy.special import ndtri
+    return -float(ndtri(q))
+
+
+def gaussian_thresholding_params(eps: float, delta: float, max_partitions_contributed: int):
+    """(sigma, threshold) of PyDP "gaussian" partition selection: delta split
+    half for the noise, half for the threshold; sigma calibrated with
+    l2 = sqrt(l0); T = 1 + sigma * Phi^-1(1 - delta_threshold')."""
+    noise_delta = delta / 2
+    threshold_delta = delta - noise_delta
+    sigma = compute_sigma(eps, noise_delta, math.sqrt(max_partitions_contributed))
+    d = adjusted_delta(threshold_delta, max_partitions_contributed)
+    return sigma, 1.0 + sigma * _upper_std_normal_quantile(d)

@@ -1,0 +1,328 @@
+"""Device-side execution of the aggregate hot path through the C ABI.
+
+Everything here works on torch-ROCm device tensors (torch is only the
+allocator/stream provider) and calls the HIP kernels of
+``csrc/pdp_kernels.hip`` through :mod:`pipelinedp_amd._native`.  There is no
+CPU fallback: every entry point raises :class:`NativeLibraryError` when the
+library is missing and ``RuntimeError`` when no GPU is present.
+
+Stage order (reference dp_engine.py:109-187):
+  bound_and_reduce  -> contribution bounding + per-partition accumulators
+  [all-reduce/reduce-scatter of accumulators across ranks: parallel.py]
+  select_and_noise  -> partition selection, compaction, compute_metrics noise
+"""
+import ctypes
+import dataclasses
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from pipelinedp_amd import _native as N
+
+
+@dataclasses.dataclass
+class BoundingSpec:
+    """Columnar form of the bounder + combiner-accumulator parameters."""
+    l0: int
+    linf: int                      # 0: keep every row of a kept pair
+    value_kind: int                # N.VALUE_*
+    flags: int                     # N.ACC_* | N.SUM_*
+    min_value: float = 0.0
+    max_value: float = 0.0
+    middle: float = 0.0
+    min_sum: float = 0.0
+    max_sum: float = 0.0
+
+    @property
+    def sum_is_int(self) -> bool:
+        return bool(self.flags & N.SUM_INT)
+
+
+@dataclasses.dataclass
+class SelectionSpec:
+    strategy: int                  # N.SELECT_*
+    max_rows_per_privacy_id: int = 1
+    pre_threshold: int = 0
+    keep_prob: Optional[np.ndarray] = None
+    noise_scale: float = 0.0
+    threshold: float = 0.0
+    want_noised_count: bool = False
+
+
+@dataclasses.dataclass
+class MetricOpSpec:
+    kind: int
+    noise_kind: int = N.NOISE_LAPLACE
+    out_col: Sequence[int] = (-1, -1, -1, -1)
+    scale: Sequence[float] = (0.0, 0.0, 0.0)
+    middle: float = 0.0
+    min_value: float = 0.0
+    sq_min_value: float = 0.0
+    degenerate: int = 0
+
+    def to_c(self) -> N.MetricOp:
+        op = N.MetricOp()
+        op.kind = self.kind
+        op.noise_kind = self.noise_kind
+        cols = list(self.out_col) + [-1] * (4 - len(self.out_col))
+        for i in range(4):
+            op.out_col[i] = int(cols[i])
+        sc = list(self.scale) + [0.0] * (3 - len(self.scale))
+        for i in range(3):
+            op.scale[i] = float(sc[i])
+        op.middle = float(self.middle)
+        op.min_value = float(self.min_value)
+        op.sq_min_value = float(self.sq_min_value)
+        op.degenerate = int(self.degenerate)
+        return op
+
+    def as_dict(self) -> dict:
+        cols = list(self.out_col) + [-1] * (4 - len(self.out_col))
+        return dict(kind=self.kind, noise_kind=self.noise_kind, out_col=cols,
+                    scale=list(self.scale) + [0.0] * (3 - len(self.scale)),
+                    middle=self.middle, min_value=self.min_value,
+                    sq_min_value=self.sq_min_value, degenerate=self.degenerate)
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("pipelinedp_amd needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+    return torch
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+def _stream(stream=None) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _check_col(t, name, dtypes, n, device):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch tensor on the GPU")
+    if t.dtype not in dtypes:
+        raise TypeError(f"{name} has dtype {t.dtype}, expected one of {dtypes}")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.dim() != 1 or t.shape[0] != n:
+        raise ValueError(f"{name} must be 1-D of length {n}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class StageTimer:
+    """Records HIP events (torch.cuda.Event on the launch stream) at stage
+    boundaries; durations() gives ms between consecutive marks."""
+
+    def __init__(self, stream=None):
+        self.stream = stream
+        self.marks = []
+
+    def mark(self, name):
+        torch = _torch()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(self.stream if self.stream is not None else torch.cuda.current_stream())
+        self.marks.append((name, ev))
+
+    def durations(self):
+        out = {}
+        for (name, a), (_, b) in zip(self.marks, self.marks[1:]):
+            if name.startswith("end_"):
+                continue
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+        return out
+
+
+def _mark(timer, name):
+    if timer is not None:
+        timer.mark(name)
+
+
+def new_accumulators(n_partitions: int, bounding: BoundingSpec, device) -> Dict[str, "torch.Tensor"]:
+    torch = _torch()
+    P = int(n_partitions)
+    acc = {
+        "privacy_id_count": torch.zeros(P, dtype=torch.int64, device=device),
+        "count": torch.zeros(P, dtype=torch.int64, device=device),
+        "sum": None,
+        "normalized_sum": None,
+        "normalized_sum_sq": None,
+    }
+    if bounding.flags & (N.ACC_SUM | N.SUM_PER_PARTITION):
+        acc["sum"] = torch.zeros(P, dtype=torch.int64 if bounding.sum_is_int else torch.float64, device=device)
+    if bounding.flags & N.ACC_NSUM:
+        acc["normalized_sum"] = torch.zeros(P, dtype=torch.float64, device=device)
+    if bounding.flags & N.ACC_NSUM2:
+        acc["normalized_sum_sq"] = torch.zeros(P, dtype=torch.float64, device=device)
+    return acc
+
+
+def _acc_struct(acc) -> N.PartitionAccumulators:
+    s = N.PartitionAccumulators()
+    s.privacy_id_count = _ptr(acc["privacy_id_count"])
+    s.count = _ptr(acc["count"])
+    s.sum = _ptr(acc["sum"])
+    s.normalized_sum = _ptr(acc["normalized_sum"])
+    s.normalized_sum_sq = _ptr(acc["normalized_sum_sq"])
+    return s
+
+
+def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, seed: int,
+                 row_offset: int = 0) -> N.BoundConfig:
+    c = N.BoundConfig()
+    c.n_rows = int(n_rows)
+    c.n_privacy_ids = int(n_privacy_ids)
+    c.n_partitions = int(n_partitions)
+    c.l0 = int(bounding.l0)
+    c.linf = int(bounding.linf)
+    c.value_kind = int(bounding.value_kind)
+    c.flags = int(bounding.flags)
+    c.min_value = float(bounding.min_value)
+    c.max_value = float(bounding.max_value)
+    c.middle = float(bounding.middle)
+    c.min_sum = float(bounding.min_sum)
+    c.max_sum = float(bounding.max_sum)
+    c.row_offset = int(row_offset)
+    c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    return c
+
+
+class BoundWorkspace:
+    """Reusable device workspace for pdp_bound_contributions."""
+
+    def __init__(self):
+        self.buf = None
+
+    def get(self, nbytes: int, device):
+        torch = _torch()
+        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        return self.buf
+
+
+def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
+                     bounding: BoundingSpec, seed: int, row_offset: int = 0, allowed=None,
+                     acc=None, workspace: Optional[BoundWorkspace] = None, stream=None,
+                     check_keys: bool = True, timer: Optional["StageTimer"] = None):
+    """Bounds contributions of one shard and ADDS its per-partition accumulators.
+
+    pid, pk: int64 device tensors of length n (dense keys); value: float64 or
+    int64 device tensor (or None for COUNT/PRIVACY_ID_COUNT only).
+    Returns the accumulator dict.
+    """
+    torch = _torch()
+    lib = N.lib()
+    device = pid.device
+    n = int(pid.shape[0])
+    _check_col(pid, "privacy_id", (torch.int64,), n, device)
+    _check_col(pk, "partition_key", (torch.int64,), n, device)
+    if bounding.value_kind == N.VALUE_F64:
+        _check_col(value, "value", (torch.float64,), n, device)
+    elif bounding.value_kind == N.VALUE_I64:
+        _check_col(value, "value", (torch.int64,), n, device)
+    else:
+        value = None
+    if allowed is not None:
+        _check_col(allowed, "pk_allowed", (torch.uint8,), int(n_partitions), device)
+    if bounding.l0 < 1 or bounding.l0 > N.MAX_L0:
+        raise NotImplementedError(f"max_partitions_contributed={bounding.l0} is outside the "
+                                  f"supported range [1, {N.MAX_L0}]")
+    if bounding.linf < 0 or bounding.linf > N.MAX_LINF:
+        raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
+                                  f"the supported range [1, {N.MAX_LINF}]")
+    cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset)
+    nbytes = ctypes.c_uint64(0)
+    N.check(lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)),
+            "pdp_bound_workspace_bytes")
+    ws = (workspace or BoundWorkspace()).get(nbytes.value, device)
+    if acc is None:
+        acc = new_accumulators(n_partitions, bounding, device)
+    st = _stream(stream)
+    _mark(timer, "sketch")
+    N.check(lib.pdp_bound_sketch(ctypes.byref(cfg), _ptr(pid), _ptr(pk), _ptr(allowed), _ptr(ws),
+                                 ws.numel(), st), "pdp_bound_sketch")
+    _mark(timer, "rows")
+    N.check(lib.pdp_bound_rows(ctypes.byref(cfg), _ptr(pid), _ptr(pk), _ptr(value), _ptr(allowed),
+                               _ptr(ws), ws.numel(), st), "pdp_bound_rows")
+    _mark(timer, "reduce")
+    if check_keys:
+        flags = ctypes.c_uint32(0)
+        N.check(lib.pdp_bound_error_flags(_ptr(ws), ctypes.byref(flags), st), "pdp_bound_error_flags")
+        if flags.value & 1:
+            raise ValueError("privacy_id / partition_key outside the dense key range "
+                             f"[0, {n_privacy_ids}) x [0, {n_partitions})")
+    N.check(lib.pdp_reduce_partitions(ctypes.byref(cfg), _ptr(value), _ptr(ws), ws.numel(),
+                                      ctypes.byref(_acc_struct(acc)), st),
+            "pdp_reduce_partitions")
+    _mark(timer, "end_bound")
+    return acc
+
+
+def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], n_cols: int,
+                     seed_select: int, seed_noise: int, partition_offset: int = 0,
+                     public_mask=None, stream=None, sync_count: bool = True,
+                     timer: Optional["StageTimer"] = None):
+    """Selects partitions and computes the noisy metrics of the kept ones.
+
+    Returns (index[n_kept] int64 device, out[n_cols, P] float64 device, n_kept)
+    where only the first n_kept columns of `out` are valid.  With
+    sync_count=False n_kept is returned as a device int64[1] tensor.
+    """
+    torch = _torch()
+    lib = N.lib()
+    rc = acc["privacy_id_count"]
+    device = rc.device
+    P = int(rc.shape[0])
+    st = _stream(stream)
+    keep = torch.empty(P, dtype=torch.uint8, device=device)
+    noised = torch.empty(P, dtype=torch.float64, device=device) if selection.want_noised_count else None
+    table = None
+    sc = N.SelectConfig()
+    sc.n_partitions = P
+    sc.partition_offset = int(partition_offset)
+    sc.strategy = int(selection.strategy)
+    sc.max_rows_per_privacy_id = int(selection.max_rows_per_privacy_id)
+    sc.pre_threshold = int(selection.pre_threshold or 0)
+    if selection.strategy == N.SELECT_TRUNCATED_GEOMETRIC:
+        table = torch.as_tensor(np.ascontiguousarray(selection.keep_prob, dtype=np.float64)).to(device)
+        sc.keep_table_len = int(table.numel())
+        sc.keep_prob = _ptr(table)
+    sc.noise_scale = float(selection.noise_scale)
+    sc.threshold = float(selection.threshold)
+    if selection.strategy == N.SELECT_PUBLIC:
+        if public_mask is None:
+            raise ValueError("public_mask is required for public partitions")
+        _check_col(public_mask, "public_mask", (torch.uint8,), P, device)
+        sc.public_mask = _ptr(public_mask)
+    sc.seed = int(seed_select) & 0xFFFFFFFFFFFFFFFF
+    _mark(timer, "select")
+    N.check(lib.pdp_select_partitions(ctypes.byref(sc), _ptr(rc), _ptr(keep), _ptr(noised), st),
+            "pdp_select_partitions")
+    cbytes = ctypes.c_uint64(0)
+    N.check(lib.pdp_compact_workspace_bytes(P, ctypes.byref(cbytes)), "pdp_compact_workspace_bytes")
+    cws = torch.empty(int(cbytes.value), dtype=torch.uint8, device=device)
+    index = torch.empty(max(P, 1), dtype=torch.int64, device=device)
+    n_kept_dev = torch.zeros(1, dtype=torch.int64, device=device)
+    N.check(lib.pdp_compact(_ptr(keep), P, _ptr(index), _ptr(n_kept_dev), _ptr(cws), cws.numel(), st),
+            "pdp_compact")
+    out = torch.empty((max(n_cols, 1), max(P, 1)), dtype=torch.float64, device=device)
+    if len(ops) > N.MAX_OPS:
+        raise NotImplementedError(f"at most {N.MAX_OPS} combiners are supported")
+    c_ops = (N.MetricOp * max(len(ops), 1))(*[o.to_c() for o in ops])
+    N.check(lib.pdp_noise_metrics(c_ops, len(ops), _ptr(index), P, _ptr(n_kept_dev),
+                                  int(partition_offset), ctypes.byref(_acc_struct(acc)),
+                                  1 if (acc["sum"] is not None and acc["sum"].dtype == torch.int64) else 0,
+                                  _ptr(noised), _ptr(out), out.shape[1],
+                                  int(seed_noise) & 0xFFFFFFFFFFFFFFFF, st),
+            "pdp_noise_metrics")
+    _mark(timer, "end_select")
+    if sync_count:
+        n_kept = int(n_kept_dev.item())
+        return index[:n_kept], out, n_kept
+    return index, out, n_kept_dev

@@ -1,0 +1,218 @@
+"""GPU parity of the HIP kernels (through the C ABI) against the CPU oracle.
+
+The oracle (oracle/columnar.py) reproduces the kernels' counter-based
+sampling priorities and Philox streams, so integer outputs (privacy-id counts,
+counts, int sums, keep decisions) must match bit-exactly and fp64 sums/noised
+metrics within 1e-9 relative (tolerance stated per assertion).
+"""
+import numpy as np
+import pytest
+
+from oracle import columnar as O
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_RTOL = 1e-9  # fp64 sums: relative to the sum of |terms| (order-dependent rounding)
+
+
+def _gen(seed, n, U, P, value_kind, skew=False):
+    rng = np.random.default_rng(seed)
+    pid = rng.integers(0, U, n, dtype=np.int64)
+    if skew:
+        pk = np.minimum(rng.zipf(1.3, n) - 1, P - 1).astype(np.int64)
+    else:
+        pk = rng.integers(0, P, n, dtype=np.int64)
+    if value_kind == O.VALUE_F64:
+        val = rng.normal(5.0, 3.0, n)
+    elif value_kind == O.VALUE_I64:
+        val = rng.integers(-3, 12, n, dtype=np.int64)
+    else:
+        val = None
+    return pid, pk, val
+
+
+def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+    import torch
+    from pipelinedp_amd import executor as X
+    tp = torch.as_tensor(pid).to(device)
+    tk = torch.as_tensor(pk).to(device)
+    tv = None if val is None else torch.as_tensor(val).to(device)
+    ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
+    acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
+                             allowed=ta, row_offset=row_offset)
+    torch.cuda.synchronize()
+    return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+
+
+def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+    return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0,
+                              linf=spec.linf, value_kind=spec.value_kind, flags=spec.flags,
+                              min_value=spec.min_value, max_value=spec.max_value,
+                              middle=spec.middle, min_sum=spec.min_sum, max_sum=spec.max_sum,
+                              seed=seed, row_offset=row_offset, allowed=allowed)
+
+
+def _abs_scale(pid, pk, val, P, lo, hi, mid):
+    """Per-partition sum of |terms| for the fp tolerance."""
+    s = np.zeros(P)
+    if val is not None:
+        np.add.at(s, pk, np.abs(np.clip(val.astype(np.float64), lo, hi)) + abs(mid) + 1.0)
+    return s + 1.0
+
+
+def _compare(got, want, scale):
+    np.testing.assert_array_equal(got["privacy_id_count"], want["privacy_id_count"])
+    np.testing.assert_array_equal(got["count"], want["count"])
+    for k in ("sum", "normalized_sum", "normalized_sum_sq"):
+        if got[k] is None:
+            continue
+        if got[k].dtype == np.int64:
+            np.testing.assert_array_equal(got[k], want[k])
+        else:
+            sc = scale if k != "normalized_sum_sq" else scale * scale
+            assert np.all(np.abs(got[k] - want[k]) <= FLOAT_RTOL * sc), k
+
+
+CASES = [
+    # (l0, linf, value_kind, flags, lo, hi, per-partition bounds)
+    (1, 1, O.VALUE_NONE, 0, 0, 0, None),
+    (2, 1, O.VALUE_F64, O.ACC_SUM, 0.0, 10.0, None),
+    (3, 2, O.VALUE_F64, O.ACC_NSUM, 0.0, 10.0, None),
+    (4, 3, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2, -1.0, 8.0, None),
+    (8, 2, O.VALUE_I64, O.ACC_SUM | O.SUM_INT, 0, 7, None),
+    (5, 0, O.VALUE_F64, O.SUM_PER_PARTITION, 0, 0, (-3.0, 20.0)),
+    (2, 0, O.VALUE_I64, O.SUM_PER_PARTITION | O.SUM_INT, 0, 0, (-3, 9)),
+    (2, 2, O.VALUE_I64, O.SUM_PER_PARTITION | O.SUM_INT, 0, 0, (0, 5)),
+    (16, 4, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM | O.ACC_NSUM2, 1.0, 6.0, None),
+    (256, 256, O.VALUE_F64, O.ACC_SUM, 0.0, 10.0, None),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
+@pytest.mark.parametrize("skew", [False, True])
+def test_bound_and_reduce_matches_oracle(device, case, skew):
+    from pipelinedp_amd import executor as X
+    l0, linf, vk, flags, lo, hi, pp = case
+    U, P, n = 700, 257, 40000
+    pid, pk, val = _gen(11 + l0 + linf, n, U, P, vk, skew)
+    mid = lo + (hi - lo) / 2 if vk != O.VALUE_NONE else 0.0
+    spec = X.BoundingSpec(l0=l0, linf=linf, value_kind=vk, flags=flags, min_value=lo, max_value=hi,
+                          middle=mid, min_sum=pp[0] if pp else 0.0, max_sum=pp[1] if pp else 0.0)
+    seed = 0x1234_5678_9ABC_DEF0 + l0
+    got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77)
+    want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77)
+    _compare(got, want, _abs_scale(pid, pk, val, P, lo, hi, mid))
+
+
+def test_no_sampling_keeps_everything(device):
+    """When l0 >= distinct partitions per pid and linf >= rows per pair nothing
+    is dropped: counts are the raw group counts (exact)."""
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(3)
+    U, P, n = 300, 50, 6000
+    pid = rng.integers(0, U, n)
+    pk = rng.integers(0, P, n)
+    val = rng.normal(2, 1, n)
+    spec = X.BoundingSpec(l0=64, linf=64, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=-100,
+                          max_value=100, middle=0.0)
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 5)
+    cnt = np.bincount(pk, minlength=P)
+    np.testing.assert_array_equal(got["count"], cnt)
+    pairs = np.unique(pid * P + pk)
+    np.testing.assert_array_equal(got["privacy_id_count"], np.bincount(pairs % P, minlength=P))
+    ref = np.zeros(P)
+    np.add.at(ref, pk, val)
+    assert np.allclose(got["sum"], ref, rtol=1e-12, atol=1e-9)
+
+
+def test_public_filter(device):
+    from pipelinedp_amd import executor as X
+    U, P, n = 200, 40, 5000
+    pid, pk, val = _gen(7, n, U, P, O.VALUE_F64)
+    allowed = np.zeros(P, dtype=bool)
+    allowed[::3] = True
+    spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0, max_value=10)
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed)
+    want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0, 10, 0))
+    assert np.all(got["count"][~allowed] == 0)
+
+
+def test_out_of_range_keys_raise(device):
+    import torch
+    from pipelinedp_amd import executor as X
+    pid = torch.tensor([0, 1, 5], dtype=torch.int64, device=device)
+    pk = torch.tensor([0, 1, 1], dtype=torch.int64, device=device)
+    spec = X.BoundingSpec(l0=1, linf=1, value_kind=O.VALUE_NONE, flags=0)
+    with pytest.raises(ValueError):
+        X.bound_and_reduce(pid, pk, None, n_privacy_ids=3, n_partitions=2, bounding=spec, seed=1)
+
+
+def test_empty_input(device):
+    import torch
+    from pipelinedp_amd import executor as X
+    e = torch.zeros(0, dtype=torch.int64, device=device)
+    spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0, max_value=1)
+    acc = X.bound_and_reduce(e, e, torch.zeros(0, dtype=torch.float64, device=device), n_privacy_ids=4,
+                             n_partitions=3, bounding=spec, seed=1)
+    assert int(acc["count"].sum()) == 0
+
+
+@pytest.mark.parametrize("strategy", [O.SELECT_TRUNCATED_GEOMETRIC, O.SELECT_LAPLACE,
+                                      O.SELECT_GAUSSIAN, O.SELECT_ALL_NONEMPTY, O.SELECT_PUBLIC])
+@pytest.mark.parametrize("pre_threshold", [0, 3])
+def test_select_and_noise_matches_oracle(device, strategy, pre_threshold):
+    import torch
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(strategy * 10 + pre_threshold)
+    P = 5000
+    rc = rng.integers(0, 40, P).astype(np.int64)
+    rc[rng.random(P) < 0.2] = 0
+    acc_np = {
+        "privacy_id_count": rc,
+        "count": rc * 2,
+        "sum": rng.normal(0, 10, P),
+        "normalized_sum": rng.normal(0, 10, P),
+        "normalized_sum_sq": np.abs(rng.normal(0, 10, P)),
+    }
+    acc = {k: torch.as_tensor(v).to(device) for k, v in acc_np.items()}
+    table = np.minimum(1.0, 1e-3 * (np.exp(0.3 * np.arange(40)) - 1))
+    table[0] = 0.0
+    pub = (rng.random(P) < 0.5).astype(np.uint8)
+    sel = X.SelectionSpec(strategy=strategy, max_rows_per_privacy_id=1, pre_threshold=pre_threshold,
+                          keep_prob=table, noise_scale=2.5, threshold=12.0,
+                          want_noised_count=True)
+    ops = [
+        X.MetricOpSpec(kind=O.OP_COUNT, noise_kind=O.NOISE_LAPLACE, out_col=(0,), scale=(1.5,)),
+        X.MetricOpSpec(kind=O.OP_SUM, noise_kind=O.NOISE_GAUSSIAN, out_col=(1,), scale=(3.0,)),
+        X.MetricOpSpec(kind=O.OP_MEAN, noise_kind=O.NOISE_LAPLACE, out_col=(2, 3, 4), scale=(1.0, 2.0),
+                       middle=5.0),
+        X.MetricOpSpec(kind=O.OP_VARIANCE, noise_kind=O.NOISE_GAUSSIAN, out_col=(5, 6, 7, 8),
+                       scale=(1.0, 2.0, 3.0), middle=5.0),
+        X.MetricOpSpec(kind=O.OP_PRIVACY_ID_COUNT, noise_kind=O.NOISE_GAUSSIAN, out_col=(9,), scale=(0.7,)),
+    ]
+    if strategy in (O.SELECT_LAPLACE, O.SELECT_GAUSSIAN):
+        ops.append(X.MetricOpSpec(kind=O.OP_THRESHOLDED_PID, out_col=(10,)))
+    n_cols = 1 + max(c for o in ops for c in o.out_col)
+    index, out, n_kept = X.select_and_noise(acc, selection=sel, ops=ops, n_cols=n_cols, seed_select=42,
+                                            seed_noise=4242, partition_offset=1000,
+                                            public_mask=torch.as_tensor(pub).to(device))
+    keep, noised = O.select(rc, strategy, max_rows_per_privacy_id=1, pre_threshold=pre_threshold,
+                            keep_prob=table, noise_scale=2.5, threshold=12.0, public_mask=pub, seed=42,
+                            partition_offset=1000)
+    want_index = np.flatnonzero(keep)
+    np.testing.assert_array_equal(index.cpu().numpy(), want_index)
+    want = O.noise_metrics([o.as_dict() for o in ops], want_index, acc_np, False, noised, 4242,
+                           partition_offset=1000, n_cols=n_cols)
+    got = out.cpu().numpy()[:, :n_kept]
+    # transcendental noise: device libm vs numpy differ by a few ulp
+    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-9)
+
+
+def test_single_hip_runtime_loaded(device):
+    """The library must bind to torch's libamdhip64 (one HIP runtime per process)."""
+    from pipelinedp_amd import _native
+    _native.lib()
+    with open("/proc/self/maps") as f:
+        paths = {line.split()[-1] for line in f if "libamdhip64" in line}
+    assert len(paths) == 1, paths
