@@ -63,10 +63,30 @@ typedef struct pdp_bound_config {
   double max_sum;
   int64_t row_offset;    /* global index of this shard's row 0 (row priorities) */
   uint64_t seed;         /* sampling seed */
+  int32_t algorithm;     /* PDP_ALGO_*; every algorithm keeps the same samples */
+  int32_t reserved;
 } pdp_bound_config;
 
 #define PDP_MAX_L0 256
 #define PDP_MAX_LINF 256
+
+/* bounding algorithms (identical results, different data movement) */
+#define PDP_ALGO_AUTO 0
+#define PDP_ALGO_GLOBAL_SKETCH 1 /* per-pid / per-pair sketches in HBM, device atomics */
+#define PDP_ALGO_BUCKETED 2      /* rows partitioned by pid bucket, sketches in LDS */
+
+typedef struct pdp_bound_plan_info {
+  int32_t algorithm;   /* resolved PDP_ALGO_* */
+  int32_t bucket_bits; /* privacy ids per bucket = 2^bucket_bits */
+  int32_t rand_shift;  /* pair sampling key: random bits [rand_shift, 64) */
+  int32_t pk_bits;     /* partition bits [0, pk_bits) */
+  int64_t n_buckets;
+  int64_t n_tiles;
+  int64_t lds_bytes;   /* per bucket workgroup */
+} pdp_bound_plan_info;
+
+/* Resolves the execution plan for `cfg` (no device work). */
+int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info);
 
 /* Per-partition accumulators, dense arrays of length n_partitions.  They are
  * the columnar form of CompoundCombiner's accumulator (combiners.py:749-764):
@@ -100,21 +120,11 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
                             const uint8_t* pk_allowed, void* workspace,
                             uint64_t workspace_bytes, void* stream);
 
-/* The two phases of pdp_bound_contributions, exposed so that each kernel can
- * be timed on its own: pdp_bound_sketch (re)initialises the workspace and
- * builds the per-privacy-id bottom-l0 sketch ("Sample per privacy_id");
- * pdp_bound_rows counts the rows of every kept pair and keeps its bottom-linf
- * rows ("Sample per (privacy_id, partition_key)").  Same arguments as above. */
-int pdp_bound_sketch(const pdp_bound_config* cfg, const int64_t* privacy_id,
-                     const int64_t* partition_key, const uint8_t* pk_allowed, void* workspace,
-                     uint64_t workspace_bytes, void* stream);
-int pdp_bound_rows(const pdp_bound_config* cfg, const int64_t* privacy_id,
-                   const int64_t* partition_key, const void* value, const uint8_t* pk_allowed,
-                   void* workspace, uint64_t workspace_bytes, void* stream);
-
 /* Per-pair accumulators (CompoundCombiner.create_accumulator on the sampled
  * values, combiners.py:749-753) merged per partition key
  * (LocalBackend.combine_accumulators_per_key, pipeline_backend.py:555-565).
+ * Must follow pdp_bound_contributions on the same workspace and stream
+ * (BUCKETED: the per-bucket sampling itself runs here, in LDS).
  * `acc` arrays are ADDED to (zero them first, or chain shards). */
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value,
                           const void* workspace, uint64_t workspace_bytes,

@@ -50,16 +50,23 @@ def pk_bits(n_partitions):
     return b
 
 
-def pair_priority(seed, pid, pk, pk_mask):
+def pair_hash(seed, pid, pk):
     pid = np.asarray(pid).astype(np.uint64)
     pk = np.asarray(pk).astype(np.uint64)
-    mask = _U64(pk_mask)
     with np.errstate(over="ignore"):
         h = mix64(_U64(seed) ^ (pid * _U64(0x9E3779B97F4A7C15)))
-        h = mix64(h + pk * _U64(0xC2B2AE3D27D4EB4F) + _U64(0x165667B19E3779F9))
-    bad = (h | mask) == EMPTY
-    h = np.where(bad, h ^ (mask + _U64(1)), h)
-    return (h & ~mask) | pk
+        return mix64(h + pk * _U64(0xC2B2AE3D27D4EB4F) + _U64(0x165667B19E3779F9))
+
+
+def pair_priority(seed, pid, pk, rand_shift):
+    """Sampling key of (pid, pk): random bits [rand_shift, 64), then pk (the
+    kernels may also place the bucket-local pid in between; that does not change
+    the order among one pid's pairs)."""
+    h = pair_hash(seed, pid, pk)
+    low = _U64((1 << rand_shift) - 1)
+    x = (h & ~low) | np.asarray(pk).astype(np.uint64)
+    bad = (x | low) == EMPTY
+    return np.where(bad, x & ~_U64(1 << rand_shift), x)
 
 
 def derive_row_seed(seed):
@@ -135,7 +142,7 @@ def _ranks_within(groups_sorted):
 def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, value_kind,
                      flags, min_value=0.0, max_value=0.0, middle=0.0, min_sum=0.0,
                      max_sum=0.0, seed=0, row_offset=0, allowed=None, priorities="hash",
-                     rng=None):
+                     rng=None, rand_shift=None):
     """Returns dense per-partition accumulators (dict of numpy arrays, length P)."""
     pid = np.asarray(pid, dtype=np.int64)
     pk = np.asarray(pk, dtype=np.int64)
@@ -155,7 +162,8 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
     pid, pk, local = pid[valid], pk[valid], local[valid]
     if len(pid) == 0:
         return out
-    mask = (1 << pk_bits(P)) - 1
+    if rand_shift is None:
+        rand_shift = pk_bits(P)
     # distinct pairs
     order = np.lexsort((pk, pid))
     ps, ks, ls = pid[order], pk[order], local[order]
@@ -164,7 +172,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
     row_pair = np.cumsum(first) - 1
     pair_pid, pair_pk = ps[first], ks[first]
     if priorities == "hash":
-        pprio = pair_priority(seed, pair_pid, pair_pk, mask)
+        pprio = pair_priority(seed, pair_pid, pair_pk, rand_shift)
     else:
         rand = rng.integers(0, 1 << (64 - pk_bits(P)), size=len(pair_pid), dtype=np.uint64)
         pprio = (rand << _U64(pk_bits(P))) | pair_pk.astype(np.uint64)

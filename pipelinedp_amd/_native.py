@@ -27,6 +27,7 @@ SELECT_GAUSSIAN_THRESHOLDING = 3
 SELECT_PUBLIC = 4
 OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID = 1, 2, 3, 4, 5, 6
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
+ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED = 0, 1, 2
 MAX_L0 = 256
 MAX_LINF = 256
 MAX_OPS = 8
@@ -35,9 +36,8 @@ EXPORTED_SYMBOLS = (
     "pdp_abi_version",
     "pdp_last_error",
     "pdp_bound_workspace_bytes",
+    "pdp_bound_plan",
     "pdp_bound_contributions",
-    "pdp_bound_sketch",
-    "pdp_bound_rows",
     "pdp_reduce_partitions",
     "pdp_select_partitions",
     "pdp_compact_workspace_bytes",
@@ -67,6 +67,20 @@ class BoundConfig(ctypes.Structure):
         ("max_sum", ctypes.c_double),
         ("row_offset", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
+        ("algorithm", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class BoundPlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("algorithm", ctypes.c_int32),
+        ("bucket_bits", ctypes.c_int32),
+        ("rand_shift", ctypes.c_int32),
+        ("pk_bits", ctypes.c_int32),
+        ("n_buckets", ctypes.c_int64),
+        ("n_tiles", ctypes.c_int64),
+        ("lds_bytes", ctypes.c_int64),
     ]
 
 
@@ -122,8 +136,7 @@ def _declare(lib):
         "pdp_last_error": (ctypes.c_char_p, []),
         "pdp_bound_workspace_bytes": (ctypes.c_int, [P(BoundConfig), P(u64)]),
         "pdp_bound_contributions": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, vp, u64, vp]),
-        "pdp_bound_sketch": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, u64, vp]),
-        "pdp_bound_rows": (ctypes.c_int, [P(BoundConfig), vp, vp, vp, vp, vp, u64, vp]),
+        "pdp_bound_plan": (ctypes.c_int, [P(BoundConfig), P(BoundPlanInfo)]),
         "pdp_reduce_partitions": (ctypes.c_int, [P(BoundConfig), vp, vp, u64, P(PartitionAccumulators), vp]),
         "pdp_select_partitions": (ctypes.c_int, [P(SelectConfig), vp, vp, vp, vp]),
         "pdp_compact_workspace_bytes": (ctypes.c_int, [i64, P(u64)]),

@@ -1,0 +1,619 @@
+"""ColumnarBackend — the MI355X drop-in for LocalBackend on DPEngine.aggregate.
+
+DPEngine builds the aggregation as a chain of backend calls with stable
+stage names (reference dp_engine.py:109-187, contribution_bounders.py:72-111).
+Every call here records a lazy plan node; nothing runs until the result is
+iterated (after BudgetAccountant.compute_budgets(), when eps/delta exist).
+Iteration recognises the chain, resolves the input columns, and runs the
+whole aggregation through the HIP kernels:
+
+    extract -> [public filter] -> bound (L0/Linf sampling) -> reduce per
+    partition -> [public padding] -> [private selection] -> noisy metrics
+    -> [post-aggregation threshold drop]
+
+The recognised chain carries everything the kernels need: the combiner
+(bound method ``create_accumulator`` / ``compute_metrics``), the selection
+``functools.partial`` (budget, max_partitions, max_rows_per_privacy_id,
+strategy, pre_threshold) and the AggregateParams passed to ``annotate``.
+Both the reference's own DPEngine (pipeline_dp) and pipelinedp_amd.DPEngine
+produce this chain.
+
+Unsupported chains raise NotImplementedError (there is no row-wise CPU
+fallback); so does a missing GPU or HIP library.
+"""
+import collections
+import functools
+import os
+from typing import Any, List, Optional
+
+import numpy as np
+
+from pipelinedp_amd import _native as N
+from pipelinedp_amd import columnar as C
+from pipelinedp_amd import combiners as pdc
+from pipelinedp_amd import dp_computations as dpc
+from pipelinedp_amd import partition_selection as ps
+from pipelinedp_amd import pipeline_backend
+
+# stage names DPEngine / the bounders use (reference file:line)
+ST_EXTRACT = "Extract (privacy_id, partition_key, value))"          # dp_engine.py:415
+ST_KEY_BY_PREFIX = "Key by partition"                                # pipeline_functions.py:25-27
+ST_FILTER_KEYS = "Filtering out partitions"                          # dp_engine.py:294-295
+ST_DROP_KEY = "Drop key"                                             # dp_engine.py:296
+ST_DROP_PID = "Drop privacy id"                                      # dp_engine.py:140-141
+ST_COMBINE = "Reduce accumulators per partition key"                 # dp_engine.py:158-159
+ST_SELECT = "Filter private partitions"                              # dp_engine.py:371
+ST_METRICS = "Compute DP metrics"                                    # dp_engine.py:181-182
+ST_THRESHOLD_DROP = "Drop partitions under threshold"                # dp_engine.py:547-549
+ST_PUBLIC_JOIN = "Join public partitions with partitions from data"  # dp_engine.py:311-313
+ST_PUBLIC_TO_COL = "Public partitions to collection"                 # dp_engine.py:305-306
+ST_EMPTY_ACCS = "Build empty accumulators"                           # dp_engine.py:307-309
+
+# bounder stage sets (contribution_bounders.py)
+CROSS_AND_PER = {"Rekey to ( (privacy_id, partition_key), value))",
+                 "Sample per (privacy_id, partition_key)",
+                 "Apply aggregate_fn after per partition bounding",
+                 "Rekey to (privacy_id, (partition_key, accumulator))",
+                 "Sample per privacy_id", "Rekey by privacy_id and unnest"}          # :72-111
+CROSS_ONLY = {"Rekey to ((privacy_id), (partition_key, value))", "Group by privacy_id",
+              "Collect values per privacy_id and partition_key", "Sample",
+              "Unnest per privacy_id",
+              "Apply aggregate_fn after cross-partition contribution bounding"}     # :168-201
+PER_PRIVACY_ID = {"Rekey to ((privacy_id), (partition_key, value))", "Sample per privacy_id",
+                  "Collect values per privacy_id and partition_key", "Unnest",
+                  "Apply aggregate_fn after per privacy_id contribution bounding"}  # :122-156
+LINF_ONLY = {"Rekey to ((privacy_id, partition_key), value)",
+             "Sample per (privacy_id, partition_key)",
+             "Apply aggregate_fn after cross-partition contribution bounding"}      # :212-230
+NOOP = {"Rekey to ((privacy_id, partition_key), value)", "Group by (privacy_id, partition_key)",
+        "Apply aggregate_fn"}                                                       # :236-246
+ALREADY_ENFORCED = {"Remove privacy_id", "Wrap values into accumulators"}          # dp_engine.py:144-150
+
+
+class _Node:
+    """A lazy collection: one recorded backend call."""
+
+    def __init__(self, backend, op, parents, stage, fn=None, arg=None, kwargs=None):
+        self.backend = backend
+        self.op = op
+        self.parents = parents
+        self.stage = stage or ""
+        self.fn = fn
+        self.arg = arg
+        self.kwargs = kwargs or {}
+        self._result = None
+
+    def __iter__(self):
+        if self._result is None:
+            self._result = self.backend._execute(self)
+        return iter(self._result)
+
+    def __bool__(self):
+        return True
+
+    def __repr__(self):
+        return f"<columnar {self.op} {self.stage!r}>"
+
+
+def _enum_value(e):
+    return getattr(e, "value", e)
+
+
+class AggregatePlan:
+    """What the recognised DPEngine.aggregate chain asks for."""
+
+    def __init__(self):
+        self.source = None
+        self.extract_fn = None
+        self.public_keys = None          # public partitions (filter) or None
+        self.public_padding = None       # public partitions (padding) or None
+        self.bounder = None              # "cross_and_per" | "cross" | ...
+        self.linf_from_graph = None
+        self.l0_from_graph = None
+        self.combiner = None
+        self.selection = None            # functools.partial of filter_fn
+        self.compute_metrics = False
+        self.threshold_drop = False
+        self.params = None
+        self.budget = None
+
+
+def _chain(sink):
+    nodes = []
+    node = sink
+    while isinstance(node, _Node):
+        nodes.append(node)
+        node = node.parents[0] if node.parents else None
+    nodes.reverse()
+    return nodes, node
+
+
+def recognise(sink) -> AggregatePlan:
+    """Maps a recorded chain to an AggregatePlan; NotImplementedError otherwise."""
+    nodes, source = _chain(sink)
+    plan = AggregatePlan()
+    plan.source = source
+    stages = set()
+    for node in nodes:
+        st = node.stage
+        if node.op == "map" and st == ST_EXTRACT:
+            plan.extract_fn = node.fn
+        elif node.op == "map" and st.startswith(ST_KEY_BY_PREFIX):
+            pass
+        elif node.op == "filter_by_key" and st == ST_FILTER_KEYS:
+            plan.public_keys = node.arg
+        elif node.op == "values" and st == ST_DROP_KEY:
+            pass
+        elif node.op == "map_tuple" and st == ST_DROP_PID:
+            pass
+        elif node.op == "flatten" and st == ST_PUBLIC_JOIN:
+            plan.public_padding = _public_from_padding(node.parents[1])
+        elif node.op == "combine_accumulators_per_key" and st == ST_COMBINE:
+            plan.combiner = node.arg
+        elif node.op == "filter" and st == ST_SELECT:
+            plan.selection = node.fn
+        elif node.op == "map_values" and st == ST_METRICS:
+            plan.compute_metrics = True
+        elif node.op == "filter" and st == ST_THRESHOLD_DROP:
+            plan.threshold_drop = True
+        elif node.op == "annotate":
+            plan.params = node.kwargs.get("params")
+            plan.budget = node.kwargs.get("budget")
+        elif node.op == "sample_fixed_per_key" and st == "Sample per (privacy_id, partition_key)":
+            plan.linf_from_graph = node.arg
+            stages.add(st)
+        elif node.op == "sample_fixed_per_key" and st == "Sample per privacy_id":
+            plan.l0_from_graph = node.arg
+            stages.add(st)
+        else:
+            stages.add(st)
+    if plan.extract_fn is None:
+        raise NotImplementedError("ColumnarBackend executes DPEngine.aggregate graphs only "
+                                  f"(no '{ST_EXTRACT}' stage in {[n.stage for n in nodes]})")
+    if stages == CROSS_AND_PER:
+        plan.bounder = "cross_and_per"
+    elif stages == CROSS_ONLY:
+        plan.bounder = "cross"
+    elif stages == PER_PRIVACY_ID:
+        raise NotImplementedError("max_contributions (SamplingPerPrivacyIdContributionBounder) is "
+                                  "not on the pipelinedp_amd hot path yet")
+    elif stages == LINF_ONLY or stages == NOOP:
+        raise NotImplementedError("perform_cross_partition_contribution_bounding=False is not "
+                                  "supported by ColumnarBackend yet")
+    elif stages == ALREADY_ENFORCED:
+        raise NotImplementedError("contribution_bounds_already_enforced is not supported by "
+                                  "ColumnarBackend yet")
+    else:
+        raise NotImplementedError(f"unrecognised stages for ColumnarBackend: {sorted(stages)}")
+    if plan.combiner is None or not plan.compute_metrics:
+        raise NotImplementedError("incomplete DPEngine.aggregate graph")
+    if plan.params is None:
+        raise NotImplementedError("DPEngine.aggregate graph without annotate(params=...)")
+    return plan
+
+
+def _public_from_padding(branch):
+    nodes, source = _chain(branch)
+    for node in nodes:
+        if node.op == "to_collection" and node.stage == ST_PUBLIC_TO_COL:
+            return node.arg
+    if nodes and nodes[0].op == "map" and nodes[0].stage == ST_EMPTY_ACCS:
+        return source
+    raise NotImplementedError("unrecognised public-partition padding branch")
+
+
+# ------------------------------------------------------------ combiners --
+class MetricsProgram:
+    """Kernel metric ops + output field order for a CompoundCombiner."""
+
+    def __init__(self):
+        self.ops = []            # executor.MetricOpSpec
+        self.fields = []         # output names, MetricsTuple order
+        self.flags = 0
+        self.min_value = self.max_value = self.middle = 0.0
+        self.min_sum = self.max_sum = 0.0
+        self.int_bounds = True
+        self.needs_values = False
+        self.threshold_combiner = None
+
+
+def _noise_kind_code(kind) -> int:
+    return N.NOISE_GAUSSIAN if _enum_value(kind) == "gaussian" else N.NOISE_LAPLACE
+
+
+def _additive(spec, sens):
+    mech = dpc.create_additive_mechanism(spec, sens)
+    return (N.NOISE_GAUSSIAN if isinstance(mech, dpc.GaussianMechanism) else N.NOISE_LAPLACE,
+            float(mech.noise_parameter))
+
+
+def build_metrics_program(compound, params) -> MetricsProgram:
+    from pipelinedp_amd.executor import MetricOpSpec
+    prog = MetricsProgram()
+    col = {}
+
+    def out(name):
+        if name not in col:
+            col[name] = len(prog.fields)
+            prog.fields.append(name)
+        return col[name]
+
+    def set_bounds(lo, hi):
+        prog.min_value, prog.max_value = float(lo), float(hi)
+        prog.middle = dpc.compute_middle(lo, hi)
+        prog.int_bounds = prog.int_bounds and _is_int(lo) and _is_int(hi)
+
+    for c in compound._combiners:
+        name = type(c).__name__
+        if name == "CountCombiner":
+            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
+            prog.ops.append(MetricOpSpec(kind=N.OP_COUNT, noise_kind=nk, out_col=(out("count"),), scale=(sc,)))
+        elif name == "SumCombiner":
+            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
+            prog.needs_values = True
+            if c._bounding_per_partition:
+                prog.flags |= N.SUM_PER_PARTITION
+                prog.min_sum, prog.max_sum = float(c._min_bound), float(c._max_bound)
+                prog.int_bounds = prog.int_bounds and _is_int(c._min_bound) and _is_int(c._max_bound)
+            else:
+                prog.flags |= N.ACC_SUM
+                set_bounds(c._min_bound, c._max_bound)
+            prog.ops.append(MetricOpSpec(kind=N.OP_SUM, noise_kind=nk, out_col=(out("sum"),), scale=(sc,)))
+        elif name == "PrivacyIdCountCombiner":
+            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
+            prog.ops.append(MetricOpSpec(kind=N.OP_PRIVACY_ID_COUNT, noise_kind=nk,
+                                         out_col=(out("privacy_id_count"),), scale=(sc,)))
+        elif name == "PostAggregationThresholdingCombiner":
+            prog.threshold_combiner = c
+            prog.ops.append(MetricOpSpec(kind=N.OP_THRESHOLDED_PID, out_col=(out("privacy_id_count"),)))
+        elif name == "MeanCombiner":
+            prog.needs_values = True
+            prog.flags |= N.ACC_NSUM
+            set_bounds(c._min_value, c._max_value)
+            ck, cs = _additive(c._count_spec, c._count_sensitivities)
+            _, ss = _additive(c._sum_spec, c._sum_sensitivities)
+            names = c._metrics_to_compute
+            cols = (out("mean"), out("count") if "count" in names else -1,
+                    out("sum") if "sum" in names else -1)
+            prog.ops.append(MetricOpSpec(kind=N.OP_MEAN, noise_kind=ck, out_col=cols, scale=(cs, ss),
+                                         middle=prog.middle))
+        elif name == "VarianceCombiner":
+            prog.needs_values = True
+            prog.flags |= N.ACC_NSUM | N.ACC_NSUM2
+            p = c._params.aggregate_params
+            set_bounds(p.min_value, p.max_value)
+            noise_params = dpc.ScalarNoiseParams(
+                c._params.eps, c._params.delta, p.min_value, p.max_value, p.min_sum_per_partition,
+                p.max_sum_per_partition, p.max_partitions_contributed,
+                p.max_contributions_per_partition, _to_local_noise_kind(p.noise_kind))
+            scales = pdc.variance_noise_scales(noise_params)
+            names = c._metrics_to_compute
+            cols = (out("variance"), out("count") if "count" in names else -1,
+                    out("sum") if "sum" in names else -1, out("mean") if "mean" in names else -1)
+            lo, hi = p.min_value, p.max_value
+            prog.ops.append(MetricOpSpec(kind=N.OP_VARIANCE, noise_kind=_noise_kind_code(p.noise_kind),
+                                         out_col=cols, scale=scales, middle=prog.middle,
+                                         min_value=float(lo),
+                                         sq_min_value=float(dpc.compute_squares_interval(lo, hi)[0]),
+                                         degenerate=int(lo == hi)))
+        else:
+            raise NotImplementedError(f"{name} is not supported by ColumnarBackend "
+                                      "(hot path: Count/Sum/Mean/Variance/PrivacyIdCount)")
+    return prog
+
+
+def _to_local_noise_kind(kind):
+    from pipelinedp_amd import aggregate_params as agg
+    return agg.NoiseKind(_enum_value(kind))
+
+
+def _is_int(x) -> bool:
+    return isinstance(x, (int, np.integer)) and not isinstance(x, bool)
+
+
+# -------------------------------------------------------------- backend --
+class ColumnarBackend(pipeline_backend.PipelineBackend):
+    """Columnar, lazily executed PipelineBackend running on one MI355X GPU
+    (or one GPU per rank with torch.distributed; see parallel.py).
+
+    Args:
+      device: torch device (default cuda:current).
+      seed: fixes the sampling / selection / noise streams (testing only —
+        a DP release must use fresh randomness, the default).
+    """
+
+    def __init__(self, device=None, seed: Optional[int] = None):
+        self._device = device
+        self._seed = seed
+        self.last_plan_info = None
+
+    # ---------------------------------------------------- recorded ops --
+    def _node(self, op, col, stage, **kw):
+        return _Node(self, op, (col,), stage, **kw)
+
+    def map(self, col, fn, stage_name: str = None):
+        return self._node("map", col, stage_name, fn=fn)
+
+    def map_with_side_inputs(self, col, fn, side_input_cols, stage_name: str = None):
+        return self._node("map_with_side_inputs", col, stage_name, fn=fn, arg=side_input_cols)
+
+    def flat_map(self, col, fn, stage_name: str = None):
+        return self._node("flat_map", col, stage_name, fn=fn)
+
+    def map_tuple(self, col, fn, stage_name: str = None):
+        return self._node("map_tuple", col, stage_name, fn=fn)
+
+    def map_values(self, col, fn, stage_name: str = None):
+        return self._node("map_values", col, stage_name, fn=fn)
+
+    def group_by_key(self, col, stage_name: str = None):
+        return self._node("group_by_key", col, stage_name)
+
+    def filter(self, col, fn, stage_name: str = None):
+        return self._node("filter", col, stage_name, fn=fn)
+
+    def filter_by_key(self, col, keys_to_keep, stage_name: str = None):
+        return self._node("filter_by_key", col, stage_name, arg=keys_to_keep)
+
+    def keys(self, col, stage_name: str = None):
+        return self._node("keys", col, stage_name)
+
+    def values(self, col, stage_name: str = None):
+        return self._node("values", col, stage_name)
+
+    def sample_fixed_per_key(self, col, n: int, stage_name: str = None):
+        return self._node("sample_fixed_per_key", col, stage_name, arg=n)
+
+    def count_per_element(self, col, stage_name: str = None):
+        return self._node("count_per_element", col, stage_name)
+
+    def sum_per_key(self, col, stage_name: str = None):
+        return self._node("sum_per_key", col, stage_name)
+
+    def combine_accumulators_per_key(self, col, combiner, stage_name: str = None):
+        return self._node("combine_accumulators_per_key", col, stage_name, arg=combiner)
+
+    def reduce_per_key(self, col, fn, stage_name: str = None):
+        return self._node("reduce_per_key", col, stage_name, fn=fn)
+
+    def flatten(self, cols, stage_name: str = None):
+        cols = tuple(cols)
+        return _Node(self, "flatten", cols, stage_name)
+
+    def distinct(self, col, stage_name: str = None):
+        return self._node("distinct", col, stage_name)
+
+    def to_list(self, col, stage_name: str = None):
+        return self._node("to_list", col, stage_name)
+
+    def to_collection(self, collection_or_iterable, col, stage_name: str = None):
+        return _Node(self, "to_collection", (), stage_name, arg=collection_or_iterable)
+
+    def to_multi_transformable_collection(self, col):
+        return col
+
+    def annotate(self, col, stage_name: str = None, **kwargs):
+        return _Node(self, "annotate", (col,), stage_name, kwargs=kwargs)
+
+    # ------------------------------------------------------- execution --
+    def _torch_device(self):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("ColumnarBackend needs a ROCm GPU; there is no CPU fallback")
+        return torch.device(self._device) if self._device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+
+    def _seeds(self):
+        if self._seed is None:
+            raw = os.urandom(24)
+            return tuple(int.from_bytes(raw[i:i + 8], "little") for i in (0, 8, 16))
+        s = int(self._seed)
+        return tuple((s * 0x9E3779B97F4A7C15 + k * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+                     for k in (1, 2, 3))
+
+    def _execute(self, sink) -> List:
+        plan = recognise(sink)
+        return AggregateRun(self, plan).run()
+
+    def accumulators(self, col):
+        """Testing aid: executes the bounding + reduction of an aggregate
+        graph and returns {partition_key: reference-style pre-noise
+        accumulator (row_count, (child accumulators...))}."""
+        plan = recognise(col)
+        return AggregateRun(self, plan).raw_accumulators()
+
+
+class AggregateRun:
+    """One execution of a recognised aggregate plan on the GPU."""
+
+    def __init__(self, backend: ColumnarBackend, plan: AggregatePlan):
+        self.backend = backend
+        self.plan = plan
+        self.params = plan.params
+        self.prog = build_metrics_program(plan.combiner, plan.params)
+
+    # ---------------------------------------------------------- ingest --
+    def _columns(self):
+        import torch
+        device = self.backend._torch_device()
+        src = self.plan.source
+        specs = C.probe_columns(self.plan.extract_fn, src) if isinstance(src, C.ColumnTable) else None
+        if specs is not None:
+            pid_raw = src.column(specs[0].name) if specs[0] is not None else None
+            pk_raw = src.column(specs[1].name)
+            v = specs[2]
+            val_raw = src.column(v.name) if isinstance(v, C.ColumnRef) else None
+            n_pid, n_pk = src.n_privacy_ids, src.n_partitions
+            pk_decode = src.partition_keys
+        else:
+            rows = [self.plan.extract_fn(r) for r in src]
+            pid_raw = [r[0] for r in rows]
+            pk_raw = [r[1] for r in rows]
+            val_raw = [r[2] for r in rows] if self.prog.needs_values else None
+            n_pid = n_pk = None
+            pk_decode = None
+        if pid_raw is None:
+            raise NotImplementedError("privacy_id_extractor=None needs contribution_bounds_already_enforced")
+        pid_enc = C.encode_keys(_host_or_device(pid_raw), n_pid)
+        pk_enc = C.encode_keys(_host_or_device(pk_raw), n_pk)
+        if pk_decode is not None and pk_enc.decode is None:
+            pk_enc.decode = np.asarray(pk_decode, dtype=object)
+        public = self.plan.public_padding if self.plan.public_padding is not None else self.plan.public_keys
+        public_codes = None
+        if public is not None:
+            pk_enc, public_codes = C.extend_with_keys(pk_enc, public)
+        pid_t = torch.as_tensor(pid_enc.codes).to(device=device, dtype=torch.int64).contiguous()
+        pk_t = torch.as_tensor(pk_enc.codes).to(device=device, dtype=torch.int64).contiguous()
+        val_t = None
+        value_kind = N.VALUE_NONE
+        if self.prog.needs_values:
+            if val_raw is None:
+                raise ValueError("the value extractor must return a value column for SUM/MEAN/VARIANCE")
+            val_t = _value_tensor(val_raw, device)
+            value_kind = N.VALUE_I64 if val_t.dtype == torch.int64 else N.VALUE_F64
+        return pid_t, pk_t, val_t, value_kind, pid_enc, pk_enc, public_codes
+
+    def _bounding_spec(self, value_kind):
+        from pipelinedp_amd.executor import BoundingSpec
+        p = self.params
+        flags = self.prog.flags
+        if (flags & (N.ACC_SUM | N.SUM_PER_PARTITION)) and value_kind == N.VALUE_I64 and self.prog.int_bounds:
+            flags |= N.SUM_INT
+        l0 = int(p.max_partitions_contributed)
+        linf = int(p.max_contributions_per_partition) if self.plan.bounder == "cross_and_per" else 0
+        if self.plan.l0_from_graph is not None and self.plan.l0_from_graph != l0:
+            raise ValueError("inconsistent max_partitions_contributed in the graph")
+        return BoundingSpec(l0=l0, linf=linf, value_kind=value_kind, flags=flags,
+                            min_value=self.prog.min_value, max_value=self.prog.max_value,
+                            middle=self.prog.middle, min_sum=self.prog.min_sum, max_sum=self.prog.max_sum)
+
+    def _bound(self):
+        from pipelinedp_amd import executor as X
+        import torch
+        pid_t, pk_t, val_t, vk, pid_enc, pk_enc, public_codes = self._columns()
+        spec = self._bounding_spec(vk)
+        P = pk_enc.n
+        allowed = None
+        if public_codes is not None:
+            mask = np.zeros(P, dtype=np.uint8)
+            mask[public_codes] = 1
+            allowed = torch.as_tensor(mask).to(pid_t.device)
+        seed_bound, _, _ = self._seeds
+        if pid_t.numel() == 0:
+            acc = X.new_accumulators(P, spec, pid_t.device)
+        else:
+            acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=pid_enc.n, n_partitions=P,
+                                     bounding=spec, seed=seed_bound, allowed=allowed)
+            self.backend.last_plan_info = X.bound_plan(pid_t.numel(), pid_enc.n, P, spec)
+        return acc, spec, pk_enc, allowed
+
+    def _selection(self):
+        from pipelinedp_amd.executor import SelectionSpec
+        tc = self.prog.threshold_combiner
+        if tc is not None:
+            mech = tc.create_mechanism() if type(tc).__module__.startswith("pipelinedp_amd") else None
+            spec = tc._mechanism_spec
+            strategy = ps.create_partition_selection_strategy(
+                _local_strategy(spec.mechanism_type.to_partition_selection_strategy()), spec.eps,
+                spec.delta, tc._sensitivities.l0, tc._pre_threshold)
+            return strategy.device_spec(1)
+        if self.plan.public_keys is not None or self.plan.public_padding is not None:
+            return SelectionSpec(strategy=N.SELECT_PUBLIC)
+        if self.plan.selection is None:
+            return SelectionSpec(strategy=N.SELECT_ALL_NONEMPTY)
+        part = self.plan.selection
+        if not isinstance(part, functools.partial) or len(part.args) != 5:
+            raise NotImplementedError("unrecognised private partition selection function")
+        budget, max_partitions, max_rows, strategy, pre_threshold = part.args
+        strat = ps.create_partition_selection_strategy(_local_strategy(strategy), budget.eps, budget.delta,
+                                                       max_partitions, pre_threshold)
+        return strat.device_spec(int(max_rows))
+
+    def run(self) -> List:
+        import torch
+        from pipelinedp_amd import executor as X
+        acc, spec, pk_enc, allowed = self._bound()
+        sel = self._selection()
+        public_mask = allowed if (self.plan.public_keys is not None or self.plan.public_padding is not None) else None
+        _, seed_select, seed_noise = self._seeds
+        index, out, n_kept = X.select_and_noise(acc, selection=sel, ops=self.prog.ops,
+                                                n_cols=len(self.prog.fields), seed_select=seed_select,
+                                                seed_noise=seed_noise, public_mask=public_mask)
+        idx = index.cpu().numpy()
+        vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((len(self.prog.fields), 0))
+        nt = pdc._get_or_create_named_tuple("MetricsTuple", tuple(self.prog.fields))
+        result = []
+        drop_nan_pid = self.prog.threshold_combiner is not None
+        pid_col = self.prog.fields.index("privacy_id_count") if drop_nan_pid else -1
+        columns = [vals[c].tolist() for c in range(len(self.prog.fields))]
+        for j, p in enumerate(idx.tolist()):
+            row = tuple(col[j] for col in columns)
+            if drop_nan_pid and row[pid_col] != row[pid_col]:
+                continue
+            result.append((pk_enc.key_of(p), nt(*row)))
+        return result
+
+    def raw_accumulators(self):
+        acc, spec, pk_enc, allowed = self._bound()
+        host = {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+        public = allowed.cpu().numpy().astype(bool) if allowed is not None else None
+        out = {}
+        for p in range(pk_enc.n):
+            rc = int(host["privacy_id_count"][p])
+            if public is None and rc == 0:
+                continue
+            if public is not None and not public[p]:
+                continue
+            children = []
+            for c in self.plan.combiner._combiners:
+                name = type(c).__name__
+                if name == "CountCombiner":
+                    children.append(int(host["count"][p]))
+                elif name == "SumCombiner":
+                    s = host["sum"][p]
+                    children.append(int(s) if host["sum"].dtype == np.int64 else float(s))
+                elif name in ("PrivacyIdCountCombiner", "PostAggregationThresholdingCombiner"):
+                    children.append(rc)
+                elif name == "MeanCombiner":
+                    children.append((int(host["count"][p]), float(host["normalized_sum"][p])))
+                elif name == "VarianceCombiner":
+                    children.append((int(host["count"][p]), float(host["normalized_sum"][p]),
+                                     float(host["normalized_sum_sq"][p])))
+            row_count = rc + (1 if public is not None else 0)  # empty public accumulator
+            out[pk_enc.key_of(p)] = (row_count, tuple(children))
+        return out
+
+    @property
+    def _seeds(self):
+        if not hasattr(self, "_seed_cache"):
+            self._seed_cache = self.backend._seeds()
+        return self._seed_cache
+
+
+def _local_strategy(strategy):
+    from pipelinedp_amd import aggregate_params as agg
+    return agg.PartitionSelectionStrategy(_enum_value(strategy))
+
+
+def _host_or_device(col):
+    if C._is_torch(col):
+        return col
+    return np.asarray(col) if not isinstance(col, np.ndarray) else col
+
+
+def _value_tensor(col, device):
+    import torch
+    if C._is_torch(col):
+        t = col.to(device)
+        if t.dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool):
+            return t.to(torch.int64).contiguous()
+        return t.to(torch.float64).contiguous()
+    arr = np.asarray(col)
+    if arr.dtype.kind in "iub":
+        return torch.as_tensor(arr.astype(np.int64)).to(device)
+    if arr.dtype.kind == "f":
+        return torch.as_tensor(arr.astype(np.float64)).to(device)
+    vals = [float(v) for v in col]
+    if all(float(v).is_integer() and isinstance(v, (int, np.integer)) for v in col):
+        return torch.as_tensor(np.asarray(col, dtype=np.int64)).to(device)
+    return torch.as_tensor(np.asarray(vals, dtype=np.float64)).to(device)

@@ -1,0 +1,523 @@
+"""Combiners of the aggregate path (mirror of pipeline_dp/combiners.py).
+
+Each combiner keeps the reference's accumulator definition
+(create_accumulator / merge_accumulators / compute_metrics, combiners.py:241-587,
+698-797) so that a CompoundCombiner behaves identically row-wise.  On the
+ColumnarBackend these methods are never called per row: the backend reads
+the combiner's configuration (bounds, mechanism specs, metric names) and runs
+the same arithmetic in the HIP kernels (csrc/pdp_bound.hip, pdp_select.hip).
+Quantile, vector-sum and custom combiners are outside the hot path.
+"""
+import abc
+import collections
+import copy
+from typing import Iterable, List, Sized, Tuple
+
+import numpy as np
+
+from pipelinedp_amd import aggregate_params as agg
+from pipelinedp_amd import budget_accounting
+from pipelinedp_amd import dp_computations as dpc
+from pipelinedp_amd import partition_selection
+
+
+class Combiner(abc.ABC):
+    """create_accumulator(values of one privacy id) -> merge -> compute_metrics."""
+
+    @abc.abstractmethod
+    def create_accumulator(self, values):
+        pass
+
+    @abc.abstractmethod
+    def merge_accumulators(self, accumulator1, accumulator2):
+        pass
+
+    @abc.abstractmethod
+    def compute_metrics(self, accumulator):
+        pass
+
+    @abc.abstractmethod
+    def metrics_names(self) -> List[str]:
+        pass
+
+    @abc.abstractmethod
+    def explain_computation(self):
+        pass
+
+    def expects_per_partition_sampling(self) -> bool:
+        return True
+
+
+class CustomCombiner(Combiner, abc.ABC):
+    """Experimental user combiners (reference :88-139): not supported on the GPU."""
+
+    @abc.abstractmethod
+    def request_budget(self, budget_accountant):
+        pass
+
+    def set_aggregate_params(self, aggregate_params):
+        self._aggregate_params = aggregate_params
+
+    def metrics_names(self) -> List[str]:
+        return self.__class__.__name__
+
+
+class CombinerParams:
+    """Mechanism spec + a copy of the aggregate params (reference :142-186)."""
+
+    def __init__(self, spec: budget_accounting.MechanismSpec, aggregate_params: agg.AggregateParams):
+        self.mechanism_spec = spec
+        self.aggregate_params = copy.copy(aggregate_params)
+
+    @property
+    def eps(self):
+        return self.mechanism_spec.eps
+
+    @property
+    def delta(self):
+        return self.mechanism_spec.delta
+
+    @property
+    def scalar_noise_params(self) -> dpc.ScalarNoiseParams:
+        p = self.aggregate_params
+        return dpc.ScalarNoiseParams(self.eps, self.delta, p.min_value, p.max_value,
+                                     p.min_sum_per_partition, p.max_sum_per_partition,
+                                     p.max_partitions_contributed, p.max_contributions_per_partition,
+                                     p.noise_kind)
+
+
+class MechanismContainerMixin(abc.ABC):
+    """Lazily creates the mechanism once budgets are known (reference :189-217)."""
+
+    @abc.abstractmethod
+    def create_mechanism(self):
+        pass
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state.pop("_mechanism", None)
+        return state
+
+    def get_mechanism(self):
+        if not hasattr(self, "_mechanism"):
+            self._mechanism = self.create_mechanism()
+        return self._mechanism
+
+
+class AdditiveMechanismMixin(MechanismContainerMixin):
+
+    def create_mechanism(self) -> dpc.AdditiveMechanism:
+        return dpc.create_additive_mechanism(self.mechanism_spec(), self.sensitivities())
+
+    @abc.abstractmethod
+    def sensitivities(self) -> dpc.Sensitivities:
+        pass
+
+    @abc.abstractmethod
+    def mechanism_spec(self) -> budget_accounting.MechanismSpec:
+        pass
+
+
+class _SimpleAdditive(Combiner, AdditiveMechanismMixin):
+    """Count-like combiner: int accumulator merged by +, noised once."""
+    METRIC = ""
+
+    def merge_accumulators(self, a, b):
+        return a + b
+
+    def compute_metrics(self, acc) -> dict:
+        return {self.METRIC: self.get_mechanism().add_noise(acc)}
+
+    def metrics_names(self) -> List[str]:
+        return [self.METRIC]
+
+    def explain_computation(self):
+        return lambda: (f"Computed DP {self.METRIC} with\n"
+                        f"     {self.get_mechanism().describe()}")
+
+    def mechanism_spec(self):
+        return self._mechanism_spec
+
+    def sensitivities(self):
+        return self._sensitivities
+
+
+class CountCombiner(_SimpleAdditive):
+    """Accumulator: number of values (reference :241-280)."""
+    METRIC = "count"
+
+    def __init__(self, mechanism_spec, aggregate_params):
+        self._mechanism_spec = mechanism_spec
+        self._sensitivities = dpc.compute_sensitivities_for_count(aggregate_params)
+
+    def create_accumulator(self, values: Sized) -> int:
+        return len(values)
+
+
+class PrivacyIdCountCombiner(_SimpleAdditive):
+    """Accumulator: 1 if the privacy id contributed (reference :283-325)."""
+    METRIC = "privacy_id_count"
+
+    def __init__(self, mechanism_spec, aggregate_params):
+        self._mechanism_spec = mechanism_spec
+        self._sensitivities = dpc.compute_sensitivities_for_privacy_id_count(aggregate_params)
+
+    def create_accumulator(self, values: Sized) -> int:
+        return 1 if values else 0
+
+    def expects_per_partition_sampling(self) -> bool:
+        return False
+
+
+class ThresholdingMechanism:
+    """Noised privacy-unit count compared to a threshold (reference
+    dp_computations.py:774-838)."""
+
+    def __init__(self, epsilon, delta, strategy, l0_sensitivity, pre_threshold):
+        self._strategy_type = strategy
+        self._pre_threshold = pre_threshold
+        self._strategy = partition_selection.create_partition_selection_strategy(
+            strategy, epsilon, delta, l0_sensitivity, pre_threshold)
+
+    @property
+    def strategy(self):
+        return self._strategy
+
+    def noised_value_if_should_keep(self, num_privacy_units: int):
+        return self._strategy.noised_value_if_should_keep(num_privacy_units)
+
+    def threshold(self) -> float:
+        return self._strategy.threshold
+
+    def describe(self) -> str:
+        s = self._strategy
+        text = (f"{self._strategy_type.value} with threshold={s.threshold:.1f} eps={s.epsilon} "
+                f"delta={s.delta}")
+        if self._pre_threshold is not None:
+            text += f" and pre_threshold={self._pre_threshold}"
+        return text
+
+
+class PostAggregationThresholdingCombiner(Combiner, MechanismContainerMixin):
+    """privacy_id_count noised by a thresholding strategy; partitions under the
+    threshold get None and are dropped (reference :328-382)."""
+
+    def __init__(self, budget_accountant, aggregate_params):
+        self._mechanism_spec = budget_accountant.request_budget(
+            agg.noise_to_thresholding(aggregate_params.noise_kind),
+            weight=aggregate_params.budget_weight)
+        self._sensitivities = dpc.compute_sensitivities_for_privacy_id_count(aggregate_params)
+        self._pre_threshold = aggregate_params.pre_threshold
+
+    def create_accumulator(self, values: Sized) -> int:
+        return 1 if values else 0
+
+    def merge_accumulators(self, a, b):
+        return a + b
+
+    def compute_metrics(self, count) -> dict:
+        return {"privacy_id_count": self.get_mechanism().noised_value_if_should_keep(count)}
+
+    def metrics_names(self) -> List[str]:
+        return ["privacy_id_count"]
+
+    def explain_computation(self):
+        return lambda: (f"Computed DP privacy_id_count with\n"
+                        f"     {self.get_mechanism().describe()}")
+
+    def mechanism_spec(self):
+        return self._mechanism_spec
+
+    def sensitivities(self):
+        return self._sensitivities
+
+    def expects_per_partition_sampling(self) -> bool:
+        return False
+
+    def create_mechanism(self) -> ThresholdingMechanism:
+        spec = self._mechanism_spec
+        return ThresholdingMechanism(spec.eps, spec.delta,
+                                     spec.mechanism_type.to_partition_selection_strategy(),
+                                     self._sensitivities.l0, self._pre_threshold)
+
+
+class SumCombiner(_SimpleAdditive):
+    """Per-value clip then sum, or sum then per-partition clip (reference :385-437)."""
+    METRIC = "sum"
+
+    def __init__(self, mechanism_spec, aggregate_params):
+        self._mechanism_spec = mechanism_spec
+        self._sensitivities = dpc.compute_sensitivities_for_sum(aggregate_params)
+        self._bounding_per_partition = aggregate_params.bounds_per_partition_are_set
+        if self._bounding_per_partition:
+            self._min_bound = aggregate_params.min_sum_per_partition
+            self._max_bound = aggregate_params.max_sum_per_partition
+        else:
+            self._min_bound = aggregate_params.min_value
+            self._max_bound = aggregate_params.max_value
+
+    def create_accumulator(self, values: Iterable[float]):
+        if self._bounding_per_partition:
+            return np.clip(sum(values), self._min_bound, self._max_bound)
+        return np.clip(values, self._min_bound, self._max_bound).sum()
+
+    def expects_per_partition_sampling(self) -> bool:
+        return not self._bounding_per_partition
+
+
+class MeanCombiner(Combiner, MechanismContainerMixin):
+    """Accumulator (count, sum(clip(v) - middle)) (reference :440-519)."""
+
+    def __init__(self, count_spec, sum_spec, params, metrics_to_compute):
+        if len(metrics_to_compute) != len(set(metrics_to_compute)):
+            raise ValueError(f"{metrics_to_compute} cannot contain duplicates")
+        for metric in metrics_to_compute:
+            if metric not in ("count", "sum", "mean"):
+                raise ValueError(f"{metric} should be one of ['count', 'sum', 'mean']")
+        if "mean" not in metrics_to_compute:
+            raise ValueError(f"one of the {metrics_to_compute} should be 'mean'")
+        self._count_spec = count_spec
+        self._sum_spec = sum_spec
+        self._metrics_to_compute = metrics_to_compute
+        self._min_value = params.min_value
+        self._max_value = params.max_value
+        self._count_sensitivities = dpc.compute_sensitivities_for_count(params)
+        self._sum_sensitivities = dpc.compute_sensitivities_for_normalized_sum(params)
+
+    def create_accumulator(self, values) -> Tuple[int, float]:
+        middle = dpc.compute_middle(self._min_value, self._max_value)
+        normalized = np.clip(values, self._min_value, self._max_value) - middle
+        return len(values), normalized.sum()
+
+    def merge_accumulators(self, a, b):
+        return a[0] + b[0], a[1] + b[1]
+
+    def compute_metrics(self, acc) -> dict:
+        count, nsum = acc
+        dp_count, dp_sum, dp_mean = self.get_mechanism().compute_mean(count, nsum)
+        out = {"mean": dp_mean}
+        if "count" in self._metrics_to_compute:
+            out["count"] = dp_count
+        if "sum" in self._metrics_to_compute:
+            out["sum"] = dp_sum
+        return out
+
+    def metrics_names(self) -> List[str]:
+        return self._metrics_to_compute
+
+    def explain_computation(self):
+        return lambda: "DP mean computation:\n" + self.get_mechanism().describe()
+
+    def create_mechanism(self) -> dpc.MeanMechanism:
+        return dpc.create_mean_mechanism(dpc.compute_middle(self._min_value, self._max_value),
+                                         self._count_spec, self._count_sensitivities,
+                                         self._sum_spec, self._sum_sensitivities)
+
+    def mechanism_spec(self):
+        return self._count_spec, self._sum_spec
+
+
+class VarianceCombiner(Combiner):
+    """Accumulator (count, sum(c), sum(c^2)) with c = clip(v) - middle
+    (reference :522-587); noise by compute_dp_var."""
+
+    def __init__(self, params: CombinerParams, metrics_to_compute):
+        self._params = params
+        if len(metrics_to_compute) != len(set(metrics_to_compute)):
+            raise ValueError(f"{metrics_to_compute} cannot contain duplicates")
+        for metric in metrics_to_compute:
+            if metric not in ("count", "sum", "mean", "variance"):
+                raise ValueError(f"{metric} should be one of ['count', 'sum', 'mean', 'variance']")
+        if "variance" not in metrics_to_compute:
+            raise ValueError(f"one of the {metrics_to_compute} should be 'variance'")
+        self._metrics_to_compute = metrics_to_compute
+
+    def create_accumulator(self, values):
+        p = self._params.aggregate_params
+        middle = dpc.compute_middle(p.min_value, p.max_value)
+        normalized = np.clip(values, p.min_value, p.max_value) - middle
+        return len(values), normalized.sum(), (normalized**2).sum()
+
+    def merge_accumulators(self, a, b):
+        return a[0] + b[0], a[1] + b[1], a[2] + b[2]
+
+    def compute_metrics(self, acc) -> dict:
+        count, nsum, nsum2 = acc
+        dp_count, dp_sum, dp_mean, dp_var = compute_dp_var(count, nsum, nsum2,
+                                                           self._params.scalar_noise_params)
+        out = {"variance": dp_var}
+        if "count" in self._metrics_to_compute:
+            out["count"] = dp_count
+        if "sum" in self._metrics_to_compute:
+            out["sum"] = dp_sum
+        if "mean" in self._metrics_to_compute:
+            out["mean"] = dp_mean
+        return out
+
+    def metrics_names(self) -> List[str]:
+        return self._metrics_to_compute
+
+    def explain_computation(self):
+        return lambda: f"Computed variance with (eps={self._params.eps} delta={self._params.delta})"
+
+    def mechanism_spec(self):
+        return self._params.mechanism_spec
+
+
+def variance_noise_scales(dp_params: dpc.ScalarNoiseParams):
+    """Noise scales of compute_dp_var's three mechanisms (reference
+    dp_computations.py:306-365): count, normalised sum, normalised sum of
+    squares, over an equal three-way budget split."""
+    (ce, cd), (se, sd), (qe, qd) = dpc.equally_split_budget(dp_params.eps, dp_params.delta, 3)
+    l0 = dp_params.l0_sensitivity()
+    linf = dp_params.max_contributions_per_partition
+    kind = dp_params.noise_kind
+    lo, hi = dp_params.min_value, dp_params.max_value
+    mid = dpc.compute_middle(lo, hi)
+    sq_lo, sq_hi = dpc.compute_squares_interval(lo, hi)
+    sq_mid = dpc.compute_middle(sq_lo, sq_hi)
+    count_scale = dpc.noise_scale(kind, ce, cd, l0, linf)
+    if lo == hi:
+        return count_scale, 0.0, 0.0
+    return (count_scale, dpc.noise_scale(kind, se, sd, l0, linf * abs(mid - lo)),
+            dpc.noise_scale(kind, qe, qd, l0, linf * abs(sq_mid - sq_lo)))
+
+
+def compute_dp_var(count, normalized_sum, normalized_sum_squares, dp_params):
+    """Host restatement of dp_computations.compute_dp_var (single partition)."""
+    cs, ss, qs = variance_noise_scales(dp_params)
+    rng = np.random.default_rng()
+
+    def noise(scale):
+        if dp_params.noise_kind == agg.NoiseKind.LAPLACE:
+            return rng.laplace(0.0, scale)
+        return rng.normal(0.0, scale)
+
+    lo, hi = dp_params.min_value, dp_params.max_value
+    dp_count = count + noise(cs)
+    if lo == hi:
+        dp_mean, dp_mean_sq = lo, dpc.compute_squares_interval(lo, hi)[0]
+    else:
+        denom = max(1.0, dp_count)
+        dp_mean = (normalized_sum + noise(ss)) / denom
+        dp_mean_sq = (normalized_sum_squares + noise(qs)) / denom
+    dp_var = dp_mean_sq - dp_mean**2
+    if lo != hi:
+        dp_mean += dpc.compute_middle(lo, hi)
+    return dp_count, dp_mean * dp_count, dp_mean, dp_var
+
+
+_named_tuple_cache = {}
+
+
+def _get_or_create_named_tuple(type_name: str, field_names: tuple):
+    key = (type_name, field_names)
+    nt = _named_tuple_cache.get(key)
+    if nt is None:
+        nt = collections.namedtuple(type_name, field_names)
+        nt.__reduce__ = lambda self: (_create_named_tuple_instance, (type_name, field_names, tuple(self)))
+        _named_tuple_cache[key] = nt
+    return nt
+
+
+def _create_named_tuple_instance(type_name: str, field_names: tuple, values):
+    return _get_or_create_named_tuple(type_name, field_names)(*values)
+
+
+class CompoundCombiner(Combiner):
+    """Accumulator (row_count, (child accumulators...)); outputs a MetricsTuple
+    with the children's metric dicts concatenated (reference :698-797)."""
+
+    def __init__(self, combiners: Iterable[Combiner], return_named_tuple: bool):
+        self._combiners = list(combiners)
+        self._metrics_to_compute = []
+        self._return_named_tuple = return_named_tuple
+        if not return_named_tuple:
+            return
+        for c in self._combiners:
+            self._metrics_to_compute.extend(c.metrics_names())
+        if len(self._metrics_to_compute) != len(set(self._metrics_to_compute)):
+            raise ValueError(f"two combiners in {combiners} cannot compute the same metrics")
+        self._metrics_to_compute = tuple(self._metrics_to_compute)
+
+    @property
+    def combiners(self):
+        return self._combiners
+
+    def create_accumulator(self, values):
+        return 1, tuple(c.create_accumulator(values) for c in self._combiners)
+
+    def merge_accumulators(self, acc1, acc2):
+        merged = tuple(c.merge_accumulators(a, b) for c, a, b in zip(self._combiners, acc1[1], acc2[1]))
+        return acc1[0] + acc2[0], merged
+
+    def compute_metrics(self, compound_accumulator):
+        _, accs = compound_accumulator
+        if not self._return_named_tuple:
+            return tuple(c.compute_metrics(a) for c, a in zip(self._combiners, accs))
+        combined = {}
+        for c, a in zip(self._combiners, accs):
+            metrics = c.compute_metrics(a)
+            for name in metrics:
+                if name in combined:
+                    raise Exception(f"{name} computed by {c} was already computed by another combiner")
+            combined.update(metrics)
+        return _create_named_tuple_instance("MetricsTuple", tuple(combined), tuple(combined.values()))
+
+    def metrics_names(self) -> List[str]:
+        return self._metrics_to_compute
+
+    def explain_computation(self):
+        return [c.explain_computation() for c in self._combiners]
+
+    def expects_per_partition_sampling(self) -> bool:
+        return any(c.expects_per_partition_sampling() for c in self._combiners)
+
+
+def create_compound_combiner(aggregate_params: agg.AggregateParams,
+                             budget_accountant) -> CompoundCombiner:
+    """Combiner set and budget-request order of the reference (:849-922):
+    VARIANCE > MEAN > {COUNT, SUM}, then PRIVACY_ID_COUNT."""
+    metrics = aggregate_params.metrics
+    mechanism_type = aggregate_params.noise_kind.convert_to_mechanism_type()
+    weight = aggregate_params.budget_weight
+    combiners = []
+    if agg.Metrics.VARIANCE in metrics:
+        budget = budget_accountant.request_budget(mechanism_type, weight=weight)
+        names = ["variance"] + [n for m, n in ((agg.Metrics.MEAN, "mean"), (agg.Metrics.COUNT, "count"),
+                                               (agg.Metrics.SUM, "sum")) if m in metrics]
+        combiners.append(VarianceCombiner(CombinerParams(budget, aggregate_params), names))
+    elif agg.Metrics.MEAN in metrics:
+        count_budget = budget_accountant.request_budget(mechanism_type, weight=weight)
+        sum_budget = budget_accountant.request_budget(mechanism_type, weight=weight)
+        names = ["mean"] + [n for m, n in ((agg.Metrics.COUNT, "count"), (agg.Metrics.SUM, "sum"))
+                            if m in metrics]
+        combiners.append(MeanCombiner(count_budget, sum_budget, aggregate_params, names))
+    else:
+        if agg.Metrics.COUNT in metrics:
+            combiners.append(CountCombiner(budget_accountant.request_budget(mechanism_type, weight=weight),
+                                           aggregate_params))
+        if agg.Metrics.SUM in metrics:
+            combiners.append(SumCombiner(budget_accountant.request_budget(mechanism_type, weight=weight),
+                                         aggregate_params))
+    if agg.Metrics.PRIVACY_ID_COUNT in metrics:
+        if aggregate_params.post_aggregation_thresholding:
+            combiners.append(PostAggregationThresholdingCombiner(budget_accountant, aggregate_params))
+        else:
+            combiners.append(PrivacyIdCountCombiner(
+                budget_accountant.request_budget(mechanism_type, weight=weight), aggregate_params))
+    if agg.Metrics.VECTOR_SUM in metrics:
+        raise NotImplementedError("VECTOR_SUM is not on the pipelinedp_amd hot path")
+    if any(m.is_percentile for m in metrics):
+        raise NotImplementedError("PERCENTILE (PyDP quantile trees) is not on the pipelinedp_amd hot path")
+    return CompoundCombiner(combiners, return_named_tuple=True)
+
+
+def create_compound_combiner_with_custom_combiners(aggregate_params, budget_accountant,
+                                                   custom_combiners):
+    for combiner in custom_combiners:
+        p = copy.copy(aggregate_params)
+        p.custom_combiners = None
+        combiner.set_aggregate_params(p)
+        combiner.request_budget(budget_accountant)
+    return CompoundCombiner(custom_combiners, return_named_tuple=False)

@@ -1,0 +1,705 @@
+// pdp_bound.hip — contribution bounding + per-partition reduction (gfx950).
+//
+// Replaces, for one shard of dense columns (privacy_id, partition_key, value):
+//   SamplingCrossAndPerPartitionContributionBounder.bound_contributions
+//     (contribution_bounders.py:72-111): "Sample per (privacy_id, partition_key)"
+//     (<= linf rows) and "Sample per privacy_id" (<= l0 distinct partitions);
+//   SamplingCrossPartitionContributionBounder (:168-201) when linf == 0;
+//   CompoundCombiner.create_accumulator / merge_accumulators (combiners.py:749-764)
+//     and LocalBackend.combine_accumulators_per_key (pipeline_backend.py:555-565).
+//
+// Sampling = bottom-k on counter-based keys (pdp_internal.h: pair_key, row_key),
+// so the kept sets depend only on (seed, data), not on scheduling or path.
+//
+// Two execution paths, same results:
+//
+//  BUCKETED (default when the per-privacy-id state fits LDS)
+//    k_part_hist     tile histogram of bucket = pid >> bucket_bits      (8 B/row)
+//    k_scan_*        exclusive scan of the bucket-major tile counts
+//    k_part_scatter  rows -> bucket order as (pair key u64, row u32)  (16 B in, 12 B out)
+//    k_bucket_bound  one workgroup per bucket, all sampling state in LDS:
+//                    B1 bottom-l0 pair sketch per pid, B2 per-pair row count
+//                    + bottom-linf row sketch, B3 gather the sampled values
+//                    and merge each kept pair into the partition accumulators
+//  GLOBAL (fallback for large l0 * linf)
+//    k_pair_sketch / k_pair_rows / k_reduce_pairs: the same sketches in HBM,
+//    updated with device-scope atomics.
+#include "pdp_internal.h"
+
+namespace pdp {
+namespace {
+
+constexpr int kPartThreads = 512;
+constexpr int64_t kTileRows = 65536;
+constexpr int kBucketThreads = 1024;
+constexpr int64_t kLdsBudget = 128 * 1024;
+constexpr int kMinRandomBits = 24;
+constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
+constexpr int kScanItems = 16;
+constexpr int kScanChunk = kBlock * kScanItems;
+
+struct Plan {
+  int algorithm;   // PDP_ALGO_*
+  int pk_bits;
+  int bucket_bits;
+  int rand_shift;
+  int64_t n_buckets;
+  int64_t n_tiles;
+  int64_t lds_bytes;
+};
+
+int64_t per_pid_lds(const pdp_bound_config* c) {
+  const int64_t l0 = c->l0;
+  const int64_t pair = 4 + (c->linf > 0 ? 8 * (int64_t)c->linf : 24);
+  return l0 * 8 + l0 * pair;
+}
+
+Plan make_plan(const pdp_bound_config* c) {
+  Plan p{};
+  p.pk_bits = bits_for(c->n_partitions);
+  const int64_t per_pid = per_pid_lds(c);
+  const int64_t max_pids = kLdsBudget / per_pid;
+  int s = -1;
+  if (max_pids >= 16) {
+    s = 0;
+    while (((int64_t)2 << s) <= max_pids) ++s;          // largest 2^s <= max_pids
+    const int u_bits = bits_for(c->n_privacy_ids);
+    if (s > u_bits) s = u_bits;                          // one bucket covers all pids
+    if (64 - p.pk_bits - s < kMinRandomBits) s = -1;
+    // one partitioning pass: the per-tile bucket histogram must fit LDS
+    if (s >= 0 && ((c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s) > kMaxBuckets) s = -1;
+  }
+  const int auto_algo = s >= 0 ? PDP_ALGO_BUCKETED : PDP_ALGO_GLOBAL_SKETCH;
+  p.algorithm = c->algorithm == PDP_ALGO_AUTO ? auto_algo : c->algorithm;
+  if (p.algorithm == PDP_ALGO_BUCKETED && s < 0) p.algorithm = -1;  // infeasible
+  p.bucket_bits = s < 0 ? 0 : s;
+  p.rand_shift = p.pk_bits + p.bucket_bits;
+  p.n_buckets = (c->n_privacy_ids + ((int64_t)1 << p.bucket_bits) - 1) >> p.bucket_bits;
+  p.n_tiles = (c->n_rows + kTileRows - 1) / kTileRows;
+  if (p.n_tiles < 1) p.n_tiles = 1;
+  p.lds_bytes = ((int64_t)1 << p.bucket_bits) * per_pid;
+  return p;
+}
+
+struct Ws {
+  // common
+  uint64_t err;
+  // global path
+  uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
+  // bucketed path
+  uint64_t counts, chunk_sums, keys, rowidx;
+  uint64_t total;
+};
+
+Ws layout(const pdp_bound_config* c, const Plan& p) {
+  Ws w{};
+  uint64_t off = 0;
+  w.err = off;
+  off = align256(off + 16);
+  if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH) {
+    const uint64_t slots = (uint64_t)c->n_privacy_ids * (uint64_t)c->l0;
+    w.sketch = off; off = align256(off + slots * 8);
+    w.cnt = off; off = align256(off + slots * 4);
+    if (c->linf > 0) {
+      w.rows = off; off = align256(off + slots * (uint64_t)c->linf * 8);
+    } else {
+      w.fsum = off; off = align256(off + slots * 8);  // double or int64
+      w.nsum = off; off = align256(off + slots * 8);
+      w.nsum2 = off; off = align256(off + slots * 8);
+    }
+  } else {
+    const uint64_t n_counts = (uint64_t)p.n_buckets * (uint64_t)p.n_tiles + 1;
+    const uint64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
+    w.counts = off; off = align256(off + n_counts * 4);
+    w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
+    w.keys = off; off = align256(off + (uint64_t)c->n_rows * 8);
+    w.rowidx = off; off = align256(off + (uint64_t)c->n_rows * 4);
+  }
+  w.total = off;
+  return w;
+}
+
+int validate(const pdp_bound_config* c) {
+  if (c == nullptr) return set_error(PDP_E_INVALID, "config is NULL");
+  if (c->n_rows < 0 || c->n_rows >= ((int64_t)1 << 32))
+    return set_error(PDP_E_INVALID, "n_rows must be in [0, 2^32)");
+  if (c->n_privacy_ids < 1 || c->n_privacy_ids >= ((int64_t)1 << 40))
+    return set_error(PDP_E_INVALID, "n_privacy_ids must be in [1, 2^40)");
+  if (c->n_partitions < 1 || c->n_partitions >= ((int64_t)1 << 32))
+    return set_error(PDP_E_INVALID, "n_partitions must be in [1, 2^32)");
+  if (c->l0 < 1 || c->l0 > PDP_MAX_L0)
+    return set_error(PDP_E_UNSUPPORTED, "l0 out of supported range [1, 256]");
+  if (c->linf < 0 || c->linf > PDP_MAX_LINF)
+    return set_error(PDP_E_UNSUPPORTED, "linf out of supported range [0, 256]");
+  if (c->value_kind < PDP_VALUE_NONE || c->value_kind > PDP_VALUE_I64)
+    return set_error(PDP_E_INVALID, "bad value_kind");
+  if (c->value_kind != PDP_VALUE_I64 && (c->flags & PDP_SUM_INT))
+    return set_error(PDP_E_INVALID, "PDP_SUM_INT requires int64 values");
+  if (c->algorithm < PDP_ALGO_AUTO || c->algorithm > PDP_ALGO_BUCKETED)
+    return set_error(PDP_E_INVALID, "bad algorithm");
+  if (make_plan(c).algorithm < 0)
+    return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm infeasible for this l0/linf/P");
+  return PDP_OK;
+}
+
+struct KP {  // kernel parameters
+  int64_t n, U, P;
+  int l0, linf;
+  int pk_bits, bucket_bits, rand_shift;
+  int64_t n_buckets, n_tiles;
+  uint64_t pk_mask, seed, row_seed;
+  int64_t row_offset;
+  ClipParams clip;
+};
+
+KP make_kp(const pdp_bound_config* c, const Plan& p) {
+  KP k;
+  k.n = c->n_rows;
+  k.U = c->n_privacy_ids;
+  k.P = c->n_partitions;
+  k.l0 = c->l0;
+  k.linf = c->linf;
+  k.pk_bits = p.pk_bits;
+  k.bucket_bits = p.bucket_bits;
+  k.rand_shift = p.rand_shift;
+  k.n_buckets = p.n_buckets;
+  k.n_tiles = p.n_tiles;
+  k.pk_mask = (1ULL << p.pk_bits) - 1;
+  k.seed = c->seed;
+  k.row_seed = derive_row_seed(c->seed);
+  k.row_offset = c->row_offset;
+  k.clip = ClipParams{c->min_value, c->max_value, c->middle, c->min_sum, c->max_sum, c->flags};
+  return k;
+}
+
+// ============================================================ GLOBAL path ==
+__global__ void __launch_bounds__(kBlock) k_pair_sketch(KP kp, const int64_t* __restrict__ pid,
+                                                        const int64_t* __restrict__ pk,
+                                                        const uint8_t* __restrict__ allowed,
+                                                        unsigned long long* sketch, unsigned int* err) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += stride) {
+    const int64_t u = pid[i];
+    const int64_t k = pk[i];
+    if (u < 0 || u >= kp.U || k < 0 || k >= kp.P) {
+      atomicOr(err, 1u);
+      continue;
+    }
+    if (allowed != nullptr && allowed[k] == 0) continue;
+    const uint64_t x = pair_key(kp.seed, u, k, 0, kp.rand_shift);
+    unsigned long long* s = sketch + u * kp.l0;
+    if (x >= s[kp.l0 - 1]) continue;  // values only decrease: a stale read is safe
+    sketch_insert(s, kp.l0, x);
+  }
+}
+
+template <int VALUE_KIND, bool KEEP_ALL_ROWS>
+__global__ void __launch_bounds__(kBlock) k_pair_rows(KP kp, const int64_t* __restrict__ pid,
+                                                      const int64_t* __restrict__ pk,
+                                                      const void* __restrict__ value,
+                                                      const uint8_t* __restrict__ allowed,
+                                                      const unsigned long long* __restrict__ sketch,
+                                                      unsigned int* pair_cnt, unsigned long long* pair_rows,
+                                                      double* pair_fsum, double* pair_nsum,
+                                                      double* pair_nsum2) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int flags = kp.clip.flags;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += stride) {
+    const int64_t u = pid[i];
+    const int64_t k = pk[i];
+    if (u < 0 || u >= kp.U || k < 0 || k >= kp.P) continue;
+    if (allowed != nullptr && allowed[k] == 0) continue;
+    const uint64_t x = pair_key(kp.seed, u, k, 0, kp.rand_shift);
+    const unsigned long long* s = sketch + u * kp.l0;
+    if (x > s[kp.l0 - 1]) continue;
+    const int j = sketch_find(s, kp.l0, x);
+    if (j < 0) continue;
+    const int64_t slot = u * kp.l0 + j;
+    atomicAdd(pair_cnt + slot, 1u);
+    if (!KEEP_ALL_ROWS) {
+      const uint64_t y = row_key(kp.row_seed, kp.row_offset + i, (uint32_t)i);
+      unsigned long long* r = pair_rows + slot * kp.linf;
+      if (y < r[kp.linf - 1]) sketch_insert(r, kp.linf, y);
+    } else if (VALUE_KIND != PDP_VALUE_NONE) {
+      double v;
+      long long iv;
+      load_value<VALUE_KIND>(value, (uint32_t)i, &v, &iv);
+      if (flags & PDP_SUM_PER_PARTITION) {
+        if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(pair_fsum + slot), (unsigned long long)iv);
+        else unsafeAtomicAdd(pair_fsum + slot, v);
+      } else if (flags & PDP_ACC_SUM) {
+        if (flags & PDP_SUM_INT)
+          atomicAdd((unsigned long long*)(pair_fsum + slot),
+                    (unsigned long long)clamp_ll(iv, (long long)kp.clip.lo, (long long)kp.clip.hi));
+        else unsafeAtomicAdd(pair_fsum + slot, fmin(fmax(v, kp.clip.lo), kp.clip.hi));
+      }
+      if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
+        const double c = fmin(fmax(v, kp.clip.lo), kp.clip.hi) - kp.clip.mid;
+        if (flags & PDP_ACC_NSUM) unsafeAtomicAdd(pair_nsum + slot, c);
+        if (flags & PDP_ACC_NSUM2) unsafeAtomicAdd(pair_nsum2 + slot, c * c);
+      }
+    }
+  }
+}
+
+// pair accumulator of a KEEP_ALL_ROWS pair from its summed slots
+__device__ __forceinline__ PairSums pair_sums_from_totals(long long cnt, double fsum_or_bits, double nsum,
+                                                          double nsum2, const ClipParams& cp) {
+  PairSums s{cnt, 0, 0.0, nsum, nsum2};
+  long long ibits = __double_as_longlong(fsum_or_bits);
+  if (cp.flags & PDP_SUM_PER_PARTITION) {
+    if (cp.flags & PDP_SUM_INT) s.isum = clamp_ll(ibits, (long long)cp.min_sum, (long long)cp.max_sum);
+    else s.fsum = fmin(fmax(fsum_or_bits, cp.min_sum), cp.max_sum);
+  } else if (cp.flags & PDP_SUM_INT) {
+    s.isum = ibits;
+  } else {
+    s.fsum = fsum_or_bits;
+  }
+  return s;
+}
+
+template <int VALUE_KIND, bool KEEP_ALL_ROWS>
+__global__ void __launch_bounds__(kBlock) k_reduce_pairs(KP kp, const void* __restrict__ value,
+                                                         const unsigned long long* __restrict__ sketch,
+                                                         const unsigned int* __restrict__ pair_cnt,
+                                                         const unsigned long long* __restrict__ pair_rows,
+                                                         const double* __restrict__ pair_fsum,
+                                                         const double* __restrict__ pair_nsum,
+                                                         const double* __restrict__ pair_nsum2,
+                                                         pdp_partition_accumulators acc) {
+  const int64_t n_slots = kp.U * kp.l0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_slots; s += stride) {
+    const uint64_t x = sketch[s];
+    if (x == kEmpty) continue;
+    const int64_t p = (int64_t)(x & kp.pk_mask);
+    const unsigned int c = pair_cnt[s];
+    if (c == 0) continue;
+    PairSums ps;
+    if (!KEEP_ALL_ROWS) {
+      const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
+      ps = pair_sums_from_rows<VALUE_KIND>(pair_rows + s * kp.linf, m, value, kp.clip);
+    } else if (VALUE_KIND != PDP_VALUE_NONE) {
+      ps = pair_sums_from_totals((long long)c, pair_fsum[s], pair_nsum[s], pair_nsum2[s], kp.clip);
+    } else {
+      ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
+    }
+    add_pair_to_partition(acc, p, ps, kp.clip.flags);
+  }
+}
+
+// ========================================================== BUCKETED path ==
+__global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t* __restrict__ pid,
+                                                            unsigned* __restrict__ counts, unsigned* err) {
+  extern __shared__ unsigned hist[];
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * kTileRows;
+  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    const int64_t u = pid[i];
+    if (u < 0 || u >= kp.U) {
+      atomicOr(err, 1u);
+      continue;
+    }
+    atomicAdd(hist + (u >> kp.bucket_bits), 1u);
+  }
+  __syncthreads();
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x)
+    counts[b * kp.n_tiles + blockIdx.x] = hist[b];
+}
+
+// exclusive scan of u32 counts[0..n) in place, total -> counts[n]
+__global__ void __launch_bounds__(kBlock) k_scan_chunks(const unsigned* __restrict__ v, int64_t n,
+                                                        unsigned* __restrict__ chunk_sums) {
+  __shared__ unsigned red[kBlock / 64];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+  unsigned s = 0;
+#pragma unroll
+  for (int t = 0; t < kScanItems; ++t)
+    if (base + t < n) s += v[base + t];
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t = 0;
+    for (int w = 0; w < kBlock / 64; ++w) t += red[w];
+    chunk_sums[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_top(unsigned* chunk_sums, int64_t n_chunks) {
+  __shared__ unsigned part[kBlock];
+  __shared__ unsigned carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n_chunks; base += kBlock) {
+    const int64_t i = base + threadIdx.x;
+    const unsigned x = i < n_chunks ? chunk_sums[i] : 0;
+    part[threadIdx.x] = x;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {
+      const unsigned t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < n_chunks) chunk_sums[i] = carry + part[threadIdx.x] - x;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry += part[kBlock - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) chunk_sums[n_chunks] = carry;
+}
+
+__global__ void __launch_bounds__(kBlock) k_scan_apply(unsigned* v, int64_t n,
+                                                       const unsigned* __restrict__ chunk_sums,
+                                                       int64_t n_chunks) {
+  __shared__ unsigned part[kBlock];
+  const int64_t base = (int64_t)blockIdx.x * kScanChunk + (int64_t)threadIdx.x * kScanItems;
+  unsigned loc[kScanItems];
+  unsigned s = 0;
+#pragma unroll
+  for (int t = 0; t < kScanItems; ++t) {
+    loc[t] = base + t < n ? v[base + t] : 0;
+    s += loc[t];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < kBlock; off <<= 1) {
+    const unsigned t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  unsigned run = chunk_sums[blockIdx.x] + part[threadIdx.x] - s;
+#pragma unroll
+  for (int t = 0; t < kScanItems; ++t) {
+    if (base + t < n) v[base + t] = run;
+    run += loc[t];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) v[n] = chunk_sums[n_chunks];
+}
+
+__global__ void __launch_bounds__(kPartThreads) k_part_scatter(KP kp, const int64_t* __restrict__ pid,
+                                                               const int64_t* __restrict__ pk,
+                                                               const uint8_t* __restrict__ allowed,
+                                                               const unsigned* __restrict__ offsets,
+                                                               unsigned long long* __restrict__ keys,
+                                                               unsigned* __restrict__ rowidx, unsigned* err) {
+  extern __shared__ unsigned cursor[];
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x)
+    cursor[b] = offsets[b * kp.n_tiles + blockIdx.x];
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * kTileRows;
+  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  const uint64_t bmask = (1ULL << kp.bucket_bits) - 1;
+  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    const int64_t u = pid[i];
+    if (u < 0 || u >= kp.U) continue;  // flagged by k_part_hist, not counted
+    const int64_t k = pk[i];
+    const unsigned pos = atomicAdd(cursor + (u >> kp.bucket_bits), 1u);
+    uint64_t x;
+    if (k < 0 || k >= kp.P) {
+      atomicOr(err, 1u);
+      x = kEmpty;
+    } else if (allowed != nullptr && allowed[k] == 0) {
+      x = kEmpty;
+    } else {
+      x = pair_key(kp.seed, u, k, ((uint64_t)u & bmask) << kp.pk_bits, kp.rand_shift);
+    }
+    keys[pos] = x;
+    rowidx[pos] = (unsigned)i;
+  }
+}
+
+template <int VALUE_KIND, bool KEEP_ALL_ROWS>
+__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const unsigned long long* __restrict__ keys,
+                                                                 const unsigned* __restrict__ rowidx,
+                                                                 const unsigned* __restrict__ offsets,
+                                                                 const void* __restrict__ value,
+                                                                 pdp_partition_accumulators acc) {
+  extern __shared__ unsigned long long smem[];
+  const int64_t S = (int64_t)1 << kp.bucket_bits;
+  const int l0 = kp.l0;
+  const int64_t n_slots = S * l0;
+  unsigned long long* sk = smem;                      // [S*l0] pair sketch per pid
+  unsigned long long* rsk = sk + n_slots;             // bounded: [S*l0*linf] row sketches
+  double* tot = (double*)(sk + n_slots);              // keep-all: [3][S*l0] pair sums
+  unsigned* cnt = KEEP_ALL_ROWS ? (unsigned*)(tot + 3 * n_slots) : (unsigned*)(rsk + n_slots * kp.linf);
+  for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
+    sk[t] = kEmpty;
+    cnt[t] = 0;
+  }
+  if (!KEEP_ALL_ROWS) {
+    for (int64_t t = threadIdx.x; t < n_slots * kp.linf; t += blockDim.x) rsk[t] = kEmpty;
+  } else {
+    for (int64_t t = threadIdx.x; t < 3 * n_slots; t += blockDim.x) tot[t] = 0.0;
+  }
+  __syncthreads();
+  const int64_t b = blockIdx.x;
+  const int64_t begin = offsets[b * kp.n_tiles];
+  const int64_t end = offsets[(b + 1) * kp.n_tiles];  // counts has n_buckets*n_tiles+1 entries
+  const uint64_t bmask = (uint64_t)S - 1;
+  // B1: bottom-l0 distinct pair keys per privacy id
+  for (int64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+    const uint64_t x = keys[i];
+    if (x == kEmpty) continue;
+    unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
+    if (x >= s[l0 - 1]) continue;
+    sketch_insert(s, l0, x);
+  }
+  __syncthreads();
+  // B2: rows of kept pairs
+  const int flags = kp.clip.flags;
+  for (int64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
+    const uint64_t x = keys[i];
+    if (x == kEmpty) continue;
+    const int64_t pl = (x >> kp.pk_bits) & bmask;
+    const unsigned long long* s = sk + pl * l0;
+    if (x > s[l0 - 1]) continue;
+    const int j = sketch_find(s, l0, x);
+    if (j < 0) continue;
+    const int64_t slot = pl * l0 + j;
+    atomicAdd(cnt + slot, 1u);
+    const uint32_t r = rowidx[i];
+    if (!KEEP_ALL_ROWS) {
+      const uint64_t y = row_key(kp.row_seed, kp.row_offset + r, r);
+      unsigned long long* rs = rsk + slot * kp.linf;
+      if (y < rs[kp.linf - 1]) sketch_insert(rs, kp.linf, y);
+    } else if (VALUE_KIND != PDP_VALUE_NONE) {
+      double v;
+      long long iv;
+      load_value<VALUE_KIND>(value, r, &v, &iv);
+      if (flags & PDP_SUM_PER_PARTITION) {
+        if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(tot + slot), (unsigned long long)iv);
+        else atomicAdd(tot + slot, v);
+      } else if (flags & PDP_ACC_SUM) {
+        if (flags & PDP_SUM_INT)
+          atomicAdd((unsigned long long*)(tot + slot),
+                    (unsigned long long)clamp_ll(iv, (long long)kp.clip.lo, (long long)kp.clip.hi));
+        else atomicAdd(tot + slot, fmin(fmax(v, kp.clip.lo), kp.clip.hi));
+      }
+      if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
+        const double c = fmin(fmax(v, kp.clip.lo), kp.clip.hi) - kp.clip.mid;
+        if (flags & PDP_ACC_NSUM) atomicAdd(tot + n_slots + slot, c);
+        if (flags & PDP_ACC_NSUM2) atomicAdd(tot + 2 * n_slots + slot, c * c);
+      }
+    }
+  }
+  __syncthreads();
+  // B3: merge every kept pair into its partition
+  for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
+    const uint64_t x = sk[slot];
+    if (x == kEmpty) continue;
+    const int64_t p = (int64_t)(x & kp.pk_mask);
+    const unsigned c = cnt[slot];
+    if (c == 0) continue;
+    PairSums ps;
+    if (!KEEP_ALL_ROWS) {
+      const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
+      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot * kp.linf, m, value, kp.clip);
+    } else if (VALUE_KIND != PDP_VALUE_NONE) {
+      ps = pair_sums_from_totals((long long)c, tot[slot], tot[n_slots + slot], tot[2 * n_slots + slot], kp.clip);
+    } else {
+      ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
+    }
+    add_pair_to_partition(acc, p, ps, flags);
+  }
+}
+
+// ---------------------------------------------------------- launchers --
+template <int VK, bool KA>
+int launch_global_rows(const KP& kp, hipStream_t st, const int64_t* pid, const int64_t* pk, const void* value,
+                       const uint8_t* allowed, char* ws, const Ws& w) {
+  hipLaunchKernelGGL((k_pair_rows<VK, KA>), dim3(grid_for(kp.n)), dim3(kBlock), 0, st, kp, pid, pk, value,
+                     allowed, (const unsigned long long*)(ws + w.sketch), (unsigned*)(ws + w.cnt),
+                     KA ? nullptr : (unsigned long long*)(ws + w.rows), KA ? (double*)(ws + w.fsum) : nullptr,
+                     KA ? (double*)(ws + w.nsum) : nullptr, KA ? (double*)(ws + w.nsum2) : nullptr);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+template <int VK, bool KA>
+int launch_global_reduce(const KP& kp, hipStream_t st, const void* value, const char* ws, const Ws& w,
+                         const pdp_partition_accumulators& acc) {
+  hipLaunchKernelGGL((k_reduce_pairs<VK, KA>), dim3(grid_for(kp.U * kp.l0)), dim3(kBlock), 0, st, kp, value,
+                     (const unsigned long long*)(ws + w.sketch), (const unsigned*)(ws + w.cnt),
+                     KA ? nullptr : (const unsigned long long*)(ws + w.rows),
+                     KA ? (const double*)(ws + w.fsum) : nullptr, KA ? (const double*)(ws + w.nsum) : nullptr,
+                     KA ? (const double*)(ws + w.nsum2) : nullptr, acc);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+template <int VK, bool KA>
+int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, const char* ws, const Ws& w, const void* value,
+                  const pdp_partition_accumulators& acc) {
+  auto kern = k_bucket_bound<VK, KA>;
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)p.lds_bytes));
+  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), (unsigned)p.lds_bytes, st, kp,
+                     (const unsigned long long*)(ws + w.keys), (const unsigned*)(ws + w.rowidx),
+                     (const unsigned*)(ws + w.counts), value, acc);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+template <template <int, bool> class F, typename... A>
+int dispatch(int value_kind, bool keep_all, A&&... args) {
+  switch (value_kind) {
+    case PDP_VALUE_NONE:
+      return keep_all ? F<PDP_VALUE_NONE, true>::run(args...) : F<PDP_VALUE_NONE, false>::run(args...);
+    case PDP_VALUE_F64:
+      return keep_all ? F<PDP_VALUE_F64, true>::run(args...) : F<PDP_VALUE_F64, false>::run(args...);
+    default:
+      return keep_all ? F<PDP_VALUE_I64, true>::run(args...) : F<PDP_VALUE_I64, false>::run(args...);
+  }
+}
+
+template <int VK, bool KA>
+struct GlobalRows {
+  template <typename... A>
+  static int run(A&&... a) { return launch_global_rows<VK, KA>(a...); }
+};
+template <int VK, bool KA>
+struct GlobalReduce {
+  template <typename... A>
+  static int run(A&&... a) { return launch_global_reduce<VK, KA>(a...); }
+};
+template <int VK, bool KA>
+struct Bucket {
+  template <typename... A>
+  static int run(A&&... a) { return launch_bucket<VK, KA>(a...); }
+};
+
+int check_ws(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes, Plan* p, Ws* w) {
+  const int rc = validate(cfg);
+  if (rc != PDP_OK) return rc;
+  *p = make_plan(cfg);
+  *w = layout(cfg, *p);
+  if (workspace == nullptr || workspace_bytes < w->total)
+    return set_error(PDP_E_WORKSPACE, "workspace too small (see pdp_bound_workspace_bytes)");
+  return PDP_OK;
+}
+
+}  // namespace
+}  // namespace pdp
+
+using namespace pdp;
+
+extern "C" {
+
+int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
+  const int rc = validate(cfg);
+  if (rc != PDP_OK) return rc;
+  if (info == nullptr) return set_error(PDP_E_INVALID, "info is NULL");
+  const Plan p = make_plan(cfg);
+  info->algorithm = p.algorithm;
+  info->bucket_bits = p.bucket_bits;
+  info->rand_shift = p.rand_shift;
+  info->pk_bits = p.pk_bits;
+  info->n_buckets = p.algorithm == PDP_ALGO_BUCKETED ? p.n_buckets : 0;
+  info->n_tiles = p.n_tiles;
+  info->lds_bytes = p.algorithm == PDP_ALGO_BUCKETED ? p.lds_bytes : 0;
+  return PDP_OK;
+}
+
+int pdp_bound_workspace_bytes(const pdp_bound_config* cfg, uint64_t* bytes) {
+  const int rc = validate(cfg);
+  if (rc != PDP_OK) return rc;
+  if (bytes == nullptr) return set_error(PDP_E_INVALID, "bytes is NULL");
+  *bytes = layout(cfg, make_plan(cfg)).total;
+  return PDP_OK;
+}
+
+int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_id, const int64_t* partition_key,
+                            const void* value, const uint8_t* pk_allowed, void* workspace,
+                            uint64_t workspace_bytes, void* stream) {
+  Plan p;
+  Ws w;
+  int rc = check_ws(cfg, workspace, workspace_bytes, &p, &w);
+  if (rc != PDP_OK) return rc;
+  if (cfg->n_rows > 0 && (privacy_id == nullptr || partition_key == nullptr))
+    return set_error(PDP_E_INVALID, "key columns are NULL");
+  if (cfg->value_kind != PDP_VALUE_NONE && cfg->n_rows > 0 && value == nullptr)
+    return set_error(PDP_E_INVALID, "value column is NULL");
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const KP kp = make_kp(cfg, p);
+  unsigned* err = (unsigned*)(ws + w.err);
+  PDP_HIP_CHECK(hipMemsetAsync(err, 0, 16, st));
+  if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH) {
+    const uint64_t slots = (uint64_t)cfg->n_privacy_ids * (uint64_t)cfg->l0;
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.sketch, 0xFF, slots * 8, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.cnt, 0, slots * 4, st));
+    if (cfg->linf > 0) PDP_HIP_CHECK(hipMemsetAsync(ws + w.rows, 0xFF, slots * (uint64_t)cfg->linf * 8, st));
+    else PDP_HIP_CHECK(hipMemsetAsync(ws + w.fsum, 0, w.total - w.fsum, st));
+    if (cfg->n_rows == 0) return PDP_OK;
+    hipLaunchKernelGGL(k_pair_sketch, dim3(grid_for(cfg->n_rows)), dim3(kBlock), 0, st, kp, privacy_id,
+                       partition_key, pk_allowed, (unsigned long long*)(ws + w.sketch), err);
+    PDP_HIP_CHECK(hipGetLastError());
+    return dispatch<GlobalRows>(cfg->value_kind, cfg->linf == 0, kp, st, privacy_id, partition_key, value,
+                                pk_allowed, ws, w);
+  }
+  // bucketed: histogram -> scan -> scatter
+  const int64_t n_counts = p.n_buckets * p.n_tiles;
+  const int64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
+  unsigned* counts = (unsigned*)(ws + w.counts);
+  unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);
+  const size_t hist_lds = (size_t)p.n_buckets * 4;
+  if (hist_lds > 160 * 1024) return set_error(PDP_E_UNSUPPORTED, "too many privacy-id buckets for one pass");
+  if (cfg->n_rows == 0) {
+    PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (n_counts + 1) * 4, st));
+    return PDP_OK;
+  }
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)hist_lds));
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)hist_lds));
+  hipLaunchKernelGGL(k_part_hist, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
+                     counts, err);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, st, chunk_sums, n_chunks);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums,
+                     n_chunks);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
+                     partition_key, pk_allowed, counts, (unsigned long long*)(ws + w.keys),
+                     (unsigned*)(ws + w.rowidx), err);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, const void* workspace,
+                          uint64_t workspace_bytes, const pdp_partition_accumulators* acc, void* stream) {
+  Plan p;
+  Ws w;
+  int rc = check_ws(cfg, workspace, workspace_bytes, &p, &w);
+  if (rc != PDP_OK) return rc;
+  if (acc == nullptr || acc->privacy_id_count == nullptr)
+    return set_error(PDP_E_INVALID, "accumulators.privacy_id_count is required");
+  if ((cfg->flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION)) && acc->sum == nullptr)
+    return set_error(PDP_E_INVALID, "accumulators.sum is required by flags");
+  if ((cfg->flags & PDP_ACC_NSUM) && acc->normalized_sum == nullptr)
+    return set_error(PDP_E_INVALID, "accumulators.normalized_sum is required by flags");
+  if ((cfg->flags & PDP_ACC_NSUM2) && acc->normalized_sum_sq == nullptr)
+    return set_error(PDP_E_INVALID, "accumulators.normalized_sum_sq is required by flags");
+  if (cfg->value_kind == PDP_VALUE_NONE &&
+      (cfg->flags & (PDP_ACC_SUM | PDP_ACC_NSUM | PDP_ACC_NSUM2 | PDP_SUM_PER_PARTITION)))
+    return set_error(PDP_E_INVALID, "value sums requested without a value column");
+  if (cfg->value_kind != PDP_VALUE_NONE && cfg->n_rows > 0 && value == nullptr)
+    return set_error(PDP_E_INVALID, "value column is NULL");
+  hipStream_t st = (hipStream_t)stream;
+  const KP kp = make_kp(cfg, p);
+  const char* ws = (const char*)workspace;
+  if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH)
+    return dispatch<GlobalReduce>(cfg->value_kind, cfg->linf == 0, kp, st, value, ws, w, *acc);
+  if (cfg->n_rows == 0) return PDP_OK;
+  return dispatch<Bucket>(cfg->value_kind, cfg->linf == 0, kp, p, st, ws, w, value, *acc);
+}
+
+}  // extern "C"

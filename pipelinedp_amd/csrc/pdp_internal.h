@@ -1,0 +1,230 @@
+// pdp_internal.h — device helpers shared by the gfx950 kernels of the
+// DPEngine.aggregate hot path (hashing, Philox, noise, sorted sketches).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdio>
+#include <string>
+
+#include "../../include/pipelinedp_amd.h"
+
+namespace pdp {
+
+// ------------------------------------------------------------ errors (host) --
+int set_error(int code, const char* msg);
+
+#define PDP_HIP_CHECK(expr)                                                        \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      char buf_[256];                                                              \
+      snprintf(buf_, sizeof(buf_), "%s failed: %s", #expr, hipGetErrorString(e_)); \
+      return ::pdp::set_error(PDP_E_HIP, buf_);                                    \
+    }                                                                              \
+  } while (0)
+
+constexpr uint64_t kEmpty = ~0ULL;
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(int64_t n, int64_t cap = 1 << 16) {
+  int64_t g = (n + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+inline uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
+
+inline int bits_for(int64_t n) {  // smallest b >= 1 with 2^b >= n
+  int b = 1;
+  while (b < 63 && ((int64_t)1 << b) < n) ++b;
+  return b;
+}
+
+// ---------------------------------------------------------------- hashing --
+// SplitMix64 finaliser: a bijective 64-bit mixer; keyed by the seed it is a
+// counter-based generator for sampling priorities.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+__host__ __device__ __forceinline__ uint64_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {
+  uint64_t h = mix64(seed ^ ((uint64_t)pid * 0x9E3779B97F4A7C15ULL));
+  return mix64(h + (uint64_t)pk * 0xC2B2AE3D27D4EB4FULL + 0x165667B19E3779F9ULL);
+}
+
+// Sampling key of the pair (pid, pk): bits [rand_shift, 64) are random, bits
+// [pk_bits, rand_shift) carry `mid` (the bucket-local pid, or 0) and bits
+// [0, pk_bits) the partition.  Within one privacy id keys order by (random
+// part, partition) whatever `mid` is, so every execution path samples the
+// same pairs.  Never equal to kEmpty.
+__host__ __device__ __forceinline__ uint64_t pair_key(uint64_t seed, int64_t pid, int64_t pk,
+                                                      uint64_t mid_bits, int rand_shift) {
+  const uint64_t h = pair_hash(seed, pid, pk);
+  const uint64_t low = (1ULL << rand_shift) - 1;
+  uint64_t x = (h & ~low) | mid_bits | (uint64_t)pk;
+  if ((x | low) == kEmpty) x &= ~(1ULL << rand_shift);
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t derive_row_seed(uint64_t seed) {
+  return mix64(seed ^ 0x5851F42D4C957F2DULL);
+}
+
+// Sampling key of row `local_row` (global index global_row): 32 random bits,
+// then the local row index (unique, < 2^32, never kEmpty).
+__device__ __forceinline__ uint64_t row_key(uint64_t row_seed, int64_t global_row, uint32_t local_row) {
+  const uint64_t h = mix64(row_seed ^ ((uint64_t)global_row * 0xD6E8FEB86659FD93ULL));
+  return (h & 0xFFFFFFFF00000000ULL) | (uint64_t)local_row;
+}
+
+// ---------------------------------------------------------------- philox --
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x;
+    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// uniform double in (0, 1): 53-bit grid, open interval
+__device__ __forceinline__ double u01(uint32_t hi, uint32_t lo) {
+  const uint64_t x = (((uint64_t)hi << 32) | lo) >> 11;
+  return ((double)x + 0.5) * (1.0 / 9007199254740992.0);
+}
+
+// counter = (global partition index, mechanism slot, "PDP!")
+__device__ __forceinline__ U4 philox_for(uint64_t seed, int64_t gidx, uint32_t slot) {
+  U4 c{(uint32_t)((uint64_t)gidx), (uint32_t)((uint64_t)gidx >> 32), slot, 0x50445021u};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+__device__ __forceinline__ double laplace_noise(double b, U4 r) {
+  const double u = u01(r.x, r.y) - 0.5;  // (-0.5, 0.5)
+  const double mag = -b * log1p(-2.0 * fabs(u));
+  return u < 0.0 ? -mag : mag;
+}
+
+__device__ __forceinline__ double gaussian_noise(double sigma, U4 r) {
+  const double u1 = u01(r.x, r.y);
+  const double u2 = u01(r.z, r.w);
+  return sigma * sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+}
+
+__device__ __forceinline__ double draw_noise(int kind, double scale, U4 r) {
+  return kind == PDP_NOISE_GAUSSIAN ? gaussian_noise(scale, r) : laplace_noise(scale, r);
+}
+
+// ------------------------------------------------- sorted-sketch insertion --
+// Keep in the ascending array s[0..k) the k smallest DISTINCT keys ever
+// inserted (kEmpty = free).  Lock-free: each atomicMin keeps the array
+// sorted and hands the displaced key to the next slot; meeting an equal key
+// means it is already present.  Works on LDS and global pointers.
+__device__ __forceinline__ void sketch_insert(unsigned long long* s, int k, uint64_t x) {
+  for (int j = 0; j < k; ++j) {
+    const uint64_t old = atomicMin(s + j, (unsigned long long)x);
+    if (old == x) return;
+    if (old > x) {
+      if (old == kEmpty) return;
+      x = old;
+    }
+  }
+}
+
+__device__ __forceinline__ int sketch_find(const unsigned long long* s, int k, uint64_t x) {
+  int lo = 0, hi = k;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return (lo < k && s[lo] == x) ? lo : -1;
+}
+
+// ------------------------------------------------ per-pair accumulation --
+struct PairSums {
+  long long count;
+  long long isum;
+  double fsum, nsum, nsum2;
+};
+
+template <int VALUE_KIND>
+__device__ __forceinline__ void load_value(const void* value, uint32_t row, double* v, long long* iv) {
+  if (VALUE_KIND == PDP_VALUE_I64) {
+    *iv = ((const long long*)value)[row];
+    *v = (double)*iv;
+  } else {
+    *iv = 0;
+    *v = ((const double*)value)[row];
+  }
+}
+
+__device__ __forceinline__ long long clamp_ll(long long v, long long lo, long long hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+struct ClipParams {
+  double lo, hi, mid, min_sum, max_sum;
+  int flags;
+};
+
+// CompoundCombiner.create_accumulator on the sampled rows of one pair
+// (combiners.py:749-753 with the Count/Sum/Mean/Variance children).
+template <int VALUE_KIND>
+__device__ __forceinline__ PairSums pair_sums_from_rows(const unsigned long long* rows, long long m,
+                                                        const void* value, const ClipParams& cp) {
+  PairSums s{m, 0, 0.0, 0.0, 0.0};
+  if (VALUE_KIND == PDP_VALUE_NONE) return s;
+  double raw = 0.0;
+  long long iraw = 0;
+  for (long long t = 0; t < m; ++t) {
+    double v;
+    long long iv;
+    load_value<VALUE_KIND>(value, (uint32_t)rows[t], &v, &iv);
+    const double cv = fmin(fmax(v, cp.lo), cp.hi);
+    if (cp.flags & PDP_SUM_PER_PARTITION) {
+      raw += v;
+      iraw += iv;
+    } else if (cp.flags & PDP_SUM_INT) {
+      s.isum += clamp_ll(iv, (long long)cp.lo, (long long)cp.hi);
+    } else {
+      s.fsum += cv;
+    }
+    const double nc = cv - cp.mid;
+    s.nsum += nc;
+    s.nsum2 += nc * nc;
+  }
+  if (cp.flags & PDP_SUM_PER_PARTITION) {
+    if (cp.flags & PDP_SUM_INT) s.isum = clamp_ll(iraw, (long long)cp.min_sum, (long long)cp.max_sum);
+    else s.fsum = fmin(fmax(raw, cp.min_sum), cp.max_sum);
+  }
+  return s;
+}
+
+// merge one pair's accumulator into the partition accumulators
+__device__ __forceinline__ void add_pair_to_partition(const pdp_partition_accumulators& acc, int64_t p,
+                                                      const PairSums& s, int flags) {
+  atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ULL);
+  if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)s.count);
+  if (acc.sum && (flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION))) {
+    if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)s.isum);
+    else unsafeAtomicAdd((double*)acc.sum + p, s.fsum);
+  }
+  if (acc.normalized_sum && (flags & PDP_ACC_NSUM)) unsafeAtomicAdd(acc.normalized_sum + p, s.nsum);
+  if (acc.normalized_sum_sq && (flags & PDP_ACC_NSUM2)) unsafeAtomicAdd(acc.normalized_sum_sq + p, s.nsum2);
+}
+
+}  // namespace pdp

@@ -1,0 +1,320 @@
+// pdp_select.hip — partition selection, compaction and noisy metrics.
+//
+//   k_select          private partition selection (dp_engine.py:315-371 ->
+//                     PyDP create_partition_strategy(...).should_keep,
+//                     partition_selection.py:29-44); thresholding strategies
+//                     also emit the noised privacy-unit count
+//                     (PostAggregationThresholdingCombiner, combiners.py:328-382)
+//   k_compact_*       ascending stream compaction of the kept partitions
+//   k_noise_metrics   CompoundCombiner.compute_metrics (combiners.py:766-788)
+//                     for Count/Sum/PrivacyIdCount/Mean/Variance children
+#include <cstring>
+
+#include "pdp_internal.h"
+
+namespace pdp {
+namespace {
+
+__global__ void __launch_bounds__(kBlock) k_select(pdp_select_config cfg, const int64_t* __restrict__ row_count,
+                                                   uint8_t* __restrict__ keep, double* __restrict__ noised) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < cfg.n_partitions; p += stride) {
+    const int64_t rc = row_count[p];
+    uint8_t kp = 0;
+    double nz = __builtin_nan("");
+    if (cfg.strategy == PDP_SELECT_PUBLIC) {
+      kp = cfg.public_mask[p] != 0;
+    } else if (cfg.strategy == PDP_SELECT_ALL_NONEMPTY) {
+      kp = rc > 0;
+    } else if (rc > 0) {
+      const int64_t mr = cfg.max_rows_per_privacy_id > 0 ? cfg.max_rows_per_privacy_id : 1;
+      int64_t n = (rc + mr - 1) / mr;
+      bool pre_ok = true;
+      int64_t shift = 0;
+      if (cfg.pre_threshold > 0) {
+        if (n < cfg.pre_threshold) pre_ok = false;
+        shift = cfg.pre_threshold - 1;
+        n -= shift;
+      }
+      if (pre_ok) {
+        const U4 r = philox_for(cfg.seed, cfg.partition_offset + p, 0x53454C00u);
+        if (cfg.strategy == PDP_SELECT_TRUNCATED_GEOMETRIC) {
+          const int64_t t = n < cfg.keep_table_len ? n : (int64_t)cfg.keep_table_len - 1;
+          kp = u01(r.x, r.y) < cfg.keep_prob[t];
+        } else {
+          const double v = (double)n + (cfg.strategy == PDP_SELECT_GAUSSIAN_THRESHOLDING
+                                            ? gaussian_noise(cfg.noise_scale, r)
+                                            : laplace_noise(cfg.noise_scale, r));
+          kp = v > cfg.threshold;
+          if (kp) nz = v + (double)shift;
+        }
+      }
+    }
+    keep[p] = kp;
+    if (noised) noised[p] = nz;
+  }
+}
+
+constexpr int kCompactItems = 16;
+constexpr int kCompactChunk = kBlock * kCompactItems;
+
+__global__ void __launch_bounds__(kBlock) k_compact_count(const uint8_t* __restrict__ keep, int64_t n,
+                                                          int64_t* __restrict__ block_counts) {
+  __shared__ int64_t red[kBlock / 64];
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk + (int64_t)threadIdx.x * kCompactItems;
+  int c = 0;
+#pragma unroll
+  for (int t = 0; t < kCompactItems; ++t) {
+    const int64_t i = base + t;
+    c += (i < n && keep[i]) ? 1 : 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t s = 0;
+    for (int w = 0; w < kBlock / 64; ++w) s += red[w];
+    block_counts[blockIdx.x] = s;
+  }
+}
+
+// exclusive scan of block_counts in place (single workgroup), total -> *out_count
+__global__ void __launch_bounds__(kBlock) k_compact_scan(int64_t* block_counts, int64_t nb,
+                                                         int64_t* out_count) {
+  __shared__ int64_t part[kBlock];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nb; base += kBlock) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < nb ? block_counts[i] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {
+      const int64_t t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < nb) block_counts[i] = carry + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == kBlock - 1) carry += part[kBlock - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out_count = carry;
+}
+
+__global__ void __launch_bounds__(kBlock) k_compact_write(const uint8_t* __restrict__ keep, int64_t n,
+                                                          const int64_t* __restrict__ block_offsets,
+                                                          int64_t* __restrict__ out_index) {
+  __shared__ int part[kBlock];
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk + (int64_t)threadIdx.x * kCompactItems;
+  int c = 0;
+#pragma unroll
+  for (int t = 0; t < kCompactItems; ++t) {
+    const int64_t i = base + t;
+    c += (i < n && keep[i]) ? 1 : 0;
+  }
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (int off = 1; off < kBlock; off <<= 1) {
+    const int t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += t;
+    __syncthreads();
+  }
+  int64_t pos = block_offsets[blockIdx.x] + part[threadIdx.x] - c;
+  for (int t = 0; t < kCompactItems; ++t) {
+    const int64_t i = base + t;
+    if (i < n && keep[i]) out_index[pos++] = i;
+  }
+}
+
+struct OpsPack {
+  pdp_metric_op op[PDP_MAX_OPS];
+};
+
+__device__ __forceinline__ void put(double* out, int64_t stride, int col, int64_t i, double v) {
+  if (col >= 0) out[(int64_t)col * stride + i] = v;
+}
+
+__global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops,
+                                                          const int64_t* __restrict__ index,
+                                                          int64_t n_kept, const int64_t* __restrict__ n_kept_dev,
+                                                          int64_t partition_offset,
+                                                          pdp_partition_accumulators acc, int sum_is_int,
+                                                          const double* __restrict__ noised_count,
+                                                          double* __restrict__ out, int64_t out_stride,
+                                                          uint64_t seed) {
+  int64_t n = n_kept;
+  if (n_kept_dev != nullptr) {
+    const int64_t d = *n_kept_dev;
+    n = d < n ? d : n;
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t p = index[i];
+    const int64_t g = partition_offset + p;
+    for (int o = 0; o < n_ops; ++o) {
+      const pdp_metric_op& op = ops.op[o];
+      const uint32_t slot = (uint32_t)o << 4;
+      switch (op.kind) {
+        case PDP_OP_COUNT: {
+          const double v = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          put(out, out_stride, op.out_col[0], i, v);
+          break;
+        }
+        case PDP_OP_SUM: {
+          const double s = sum_is_int ? (double)((const long long*)acc.sum)[p] : ((const double*)acc.sum)[p];
+          put(out, out_stride, op.out_col[0], i, s + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot)));
+          break;
+        }
+        case PDP_OP_PRIVACY_ID_COUNT: {
+          const double v = (double)acc.privacy_id_count[p] +
+                           draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          put(out, out_stride, op.out_col[0], i, v);
+          break;
+        }
+        case PDP_OP_MEAN: {
+          const double dp_count = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          const double denom = fmax(1.0, dp_count);
+          const double dp_nsum = acc.normalized_sum[p] + draw_noise(op.noise_kind, op.scale[1], philox_for(seed, g, slot + 1));
+          const double mean = op.middle + dp_nsum / denom;
+          put(out, out_stride, op.out_col[0], i, mean);
+          put(out, out_stride, op.out_col[1], i, dp_count);
+          put(out, out_stride, op.out_col[2], i, mean * dp_count);
+          break;
+        }
+        case PDP_OP_VARIANCE: {
+          const double dp_count = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          double dp_mean, dp_mean_sq;
+          if (op.degenerate) {
+            dp_mean = op.min_value;
+            dp_mean_sq = op.sq_min_value;
+          } else {
+            const double denom = fmax(1.0, dp_count);
+            dp_mean = (acc.normalized_sum[p] + draw_noise(op.noise_kind, op.scale[1], philox_for(seed, g, slot + 1))) / denom;
+            dp_mean_sq = (acc.normalized_sum_sq[p] + draw_noise(op.noise_kind, op.scale[2], philox_for(seed, g, slot + 2))) / denom;
+          }
+          const double dp_var = dp_mean_sq - dp_mean * dp_mean;
+          if (!op.degenerate) dp_mean += op.middle;
+          put(out, out_stride, op.out_col[0], i, dp_var);
+          put(out, out_stride, op.out_col[1], i, dp_count);
+          put(out, out_stride, op.out_col[2], i, dp_mean * dp_count);
+          put(out, out_stride, op.out_col[3], i, dp_mean);
+          break;
+        }
+        case PDP_OP_THRESHOLDED_PID: {
+          put(out, out_stride, op.out_col[0], i, noised_count[p]);
+          break;
+        }
+        default:
+          break;
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace pdp
+
+using namespace pdp;
+
+extern "C" {
+
+int pdp_select_partitions(const pdp_select_config* cfg, const int64_t* row_count, uint8_t* keep,
+                          double* noised_count, void* stream) {
+  if (cfg == nullptr || keep == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (cfg->n_partitions < 0) return pdp::set_error(PDP_E_INVALID, "n_partitions < 0");
+  if (cfg->strategy < PDP_SELECT_ALL_NONEMPTY || cfg->strategy > PDP_SELECT_PUBLIC)
+    return pdp::set_error(PDP_E_INVALID, "bad strategy");
+  if (cfg->strategy == PDP_SELECT_PUBLIC && cfg->public_mask == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "public_mask is required");
+  if (cfg->strategy == PDP_SELECT_TRUNCATED_GEOMETRIC && (cfg->keep_prob == nullptr || cfg->keep_table_len < 1))
+    return pdp::set_error(PDP_E_INVALID, "keep_prob table is required");
+  if (cfg->strategy != PDP_SELECT_PUBLIC && row_count == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "row_count is required");
+  if (cfg->n_partitions == 0) return PDP_OK;
+  hipLaunchKernelGGL(k_select, dim3(grid_for(cfg->n_partitions)), dim3(kBlock), 0, (hipStream_t)stream,
+                     *cfg, row_count, keep, noised_count);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+int pdp_compact_workspace_bytes(int64_t n, uint64_t* bytes) {
+  if (bytes == nullptr || n < 0) return pdp::set_error(PDP_E_INVALID, "bad argument");
+  const int64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
+  *bytes = align256((uint64_t)(nb > 0 ? nb : 1) * 8);
+  return PDP_OK;
+}
+
+int pdp_compact(const uint8_t* keep, int64_t n, int64_t* out_index, int64_t* out_count, void* workspace,
+                uint64_t workspace_bytes, void* stream) {
+  if (n < 0 || out_count == nullptr) return pdp::set_error(PDP_E_INVALID, "bad argument");
+  uint64_t need = 0;
+  pdp_compact_workspace_bytes(n, &need);
+  if (workspace == nullptr || workspace_bytes < need) return pdp::set_error(PDP_E_WORKSPACE, "workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    PDP_HIP_CHECK(hipMemsetAsync(out_count, 0, 8, st));
+    return PDP_OK;
+  }
+  if (keep == nullptr || out_index == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  const int64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
+  int64_t* bc = (int64_t*)workspace;
+  hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(kBlock), 0, st, keep, n, bc);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kBlock), 0, st, bc, nb, out_count);
+  PDP_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_compact_write, dim3((unsigned)nb), dim3(kBlock), 0, st, keep, n, bc, out_index);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* index, int64_t n_kept,
+                      const int64_t* n_kept_dev, int64_t partition_offset,
+                      const pdp_partition_accumulators* acc, int32_t sum_is_int,
+                      const double* noised_count, double* out, int64_t out_stride, uint64_t seed,
+                      void* stream) {
+  if (ops == nullptr || n_ops < 0 || n_ops > PDP_MAX_OPS || acc == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "bad ops");
+  if (n_kept < 0 || out_stride < n_kept) return pdp::set_error(PDP_E_INVALID, "bad n_kept / out_stride");
+  if (n_kept == 0 || n_ops == 0) return PDP_OK;
+  if (index == nullptr || out == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  OpsPack pack;
+  memset(&pack, 0, sizeof(pack));
+  for (int i = 0; i < n_ops; ++i) {
+    const pdp_metric_op& o = ops[i];
+    switch (o.kind) {
+      case PDP_OP_COUNT:
+        if (!acc->count) return pdp::set_error(PDP_E_INVALID, "COUNT needs accumulators.count");
+        break;
+      case PDP_OP_SUM:
+        if (!acc->sum) return pdp::set_error(PDP_E_INVALID, "SUM needs accumulators.sum");
+        break;
+      case PDP_OP_PRIVACY_ID_COUNT:
+        if (!acc->privacy_id_count) return pdp::set_error(PDP_E_INVALID, "needs privacy_id_count");
+        break;
+      case PDP_OP_MEAN:
+        if (!acc->count || !acc->normalized_sum) return pdp::set_error(PDP_E_INVALID, "MEAN needs count, normalized_sum");
+        break;
+      case PDP_OP_VARIANCE:
+        if (!acc->count || !acc->normalized_sum || !acc->normalized_sum_sq)
+          return pdp::set_error(PDP_E_INVALID, "VARIANCE needs count, normalized sums");
+        break;
+      case PDP_OP_THRESHOLDED_PID:
+        if (!noised_count) return pdp::set_error(PDP_E_INVALID, "THRESHOLDED_PID needs noised_count");
+        break;
+      default:
+        return pdp::set_error(PDP_E_INVALID, "unknown op kind");
+    }
+    pack.op[i] = o;
+  }
+  hipLaunchKernelGGL(k_noise_metrics, dim3(grid_for(n_kept)), dim3(kBlock), 0, (hipStream_t)stream, pack,
+                     n_ops, index, n_kept, n_kept_dev, partition_offset, *acc, sum_is_int, noised_count,
+                     out, out_stride, seed);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+}  // extern "C"

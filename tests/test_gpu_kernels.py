@@ -31,7 +31,12 @@ def _gen(seed, n, U, P, value_kind, skew=False):
     return pid, pk, val
 
 
-def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+def _rand_shift(n, U, P, spec, algorithm=0):
+    from pipelinedp_amd import executor as X
+    return X.bound_plan(n, U, P, spec, algorithm).rand_shift
+
+
+def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0):
     import torch
     from pipelinedp_amd import executor as X
     tp = torch.as_tensor(pid).to(device)
@@ -39,17 +44,18 @@ def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0)
     tv = None if val is None else torch.as_tensor(val).to(device)
     ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
     acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
-                             allowed=ta, row_offset=row_offset)
+                             allowed=ta, row_offset=row_offset, algorithm=algorithm)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
 
-def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0):
     return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0,
                               linf=spec.linf, value_kind=spec.value_kind, flags=spec.flags,
                               min_value=spec.min_value, max_value=spec.max_value,
                               middle=spec.middle, min_sum=spec.min_sum, max_sum=spec.max_sum,
-                              seed=seed, row_offset=row_offset, allowed=allowed)
+                              seed=seed, row_offset=row_offset, allowed=allowed,
+                              rand_shift=_rand_shift(len(pid), U, P, spec, algorithm))
 
 
 def _abs_scale(pid, pk, val, P, lo, hi, mid):
@@ -88,9 +94,14 @@ CASES = [
 ]
 
 
+ALGOS = {"global": 1, "bucketed": 2}
+
+
 @pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
 @pytest.mark.parametrize("skew", [False, True])
-def test_bound_and_reduce_matches_oracle(device, case, skew):
+@pytest.mark.parametrize("algo", list(ALGOS))
+def test_bound_and_reduce_matches_oracle(device, case, skew, algo):
+    from pipelinedp_amd import _native as N
     from pipelinedp_amd import executor as X
     l0, linf, vk, flags, lo, hi, pp = case
     U, P, n = 700, 257, 40000
@@ -99,8 +110,12 @@ def test_bound_and_reduce_matches_oracle(device, case, skew):
     spec = X.BoundingSpec(l0=l0, linf=linf, value_kind=vk, flags=flags, min_value=lo, max_value=hi,
                           middle=mid, min_sum=pp[0] if pp else 0.0, max_sum=pp[1] if pp else 0.0)
     seed = 0x1234_5678_9ABC_DEF0 + l0
-    got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77)
-    want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77)
+    try:
+        X.bound_plan(n, U, P, spec, ALGOS[algo])
+    except N.NativeLibraryError:
+        pytest.skip(f"{algo} infeasible for l0={l0}, linf={linf}")
+    got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo])
+    want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo])
     _compare(got, want, _abs_scale(pid, pk, val, P, lo, hi, mid))
 
 
@@ -125,27 +140,55 @@ def test_no_sampling_keeps_everything(device):
     assert np.allclose(got["sum"], ref, rtol=1e-12, atol=1e-9)
 
 
-def test_public_filter(device):
+@pytest.mark.parametrize("algo", list(ALGOS))
+def test_public_filter(device, algo):
     from pipelinedp_amd import executor as X
     U, P, n = 200, 40, 5000
     pid, pk, val = _gen(7, n, U, P, O.VALUE_F64)
     allowed = np.zeros(P, dtype=bool)
     allowed[::3] = True
     spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0, max_value=10)
-    got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed)
-    want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed)
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo])
+    want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo])
     _compare(got, want, _abs_scale(pid, pk, val, P, 0, 10, 0))
     assert np.all(got["count"][~allowed] == 0)
 
 
-def test_out_of_range_keys_raise(device):
+@pytest.mark.parametrize("algo", list(ALGOS))
+@pytest.mark.parametrize("bad", ["pid", "pk"])
+def test_out_of_range_keys_raise(device, algo, bad):
     import torch
     from pipelinedp_amd import executor as X
-    pid = torch.tensor([0, 1, 5], dtype=torch.int64, device=device)
-    pk = torch.tensor([0, 1, 1], dtype=torch.int64, device=device)
+    pid = torch.tensor([0, 1, 5 if bad == "pid" else 2], dtype=torch.int64, device=device)
+    pk = torch.tensor([0, 1, 7 if bad == "pk" else 1], dtype=torch.int64, device=device)
     spec = X.BoundingSpec(l0=1, linf=1, value_kind=O.VALUE_NONE, flags=0)
     with pytest.raises(ValueError):
-        X.bound_and_reduce(pid, pk, None, n_privacy_ids=3, n_partitions=2, bounding=spec, seed=1)
+        X.bound_and_reduce(pid, pk, None, n_privacy_ids=3, n_partitions=2, bounding=spec, seed=1,
+                           algorithm=ALGOS[algo])
+
+
+@pytest.mark.parametrize("heavy", [False, True])
+def test_algorithms_agree_at_scale(device, heavy):
+    """Bucketed and global paths keep the same samples on a larger skewed input
+    (one privacy id with 200k rows when heavy)."""
+    import torch
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(8)
+    n, U, P = 2_000_000, 50_000, 30_000
+    pid = rng.integers(0, U, n)
+    if heavy:
+        pid[:200_000] = 17
+    pk = np.minimum(rng.zipf(1.2, n) - 1, P - 1)
+    val = rng.normal(5, 3, n)
+    spec = X.BoundingSpec(l0=4, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM,
+                          min_value=0.0, max_value=10.0, middle=5.0)
+    a = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=1)
+    b = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=2)
+    np.testing.assert_array_equal(a["privacy_id_count"], b["privacy_id_count"])
+    np.testing.assert_array_equal(a["count"], b["count"])
+    sc = _abs_scale(pid, pk, val, P, 0.0, 10.0, 5.0)
+    assert np.all(np.abs(a["sum"] - b["sum"]) <= FLOAT_RTOL * sc)
+    assert np.all(np.abs(a["normalized_sum"] - b["normalized_sum"]) <= FLOAT_RTOL * sc)
 
 
 def test_empty_input(device):
