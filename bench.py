@@ -34,6 +34,11 @@ if HERE not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
+# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 wide-load
+# correction + WRITE_SIZE, MI355X_MICROARCH.md "HBM"), profiles/r01/pmc_*.txt;
+# None where not measured for the current kernel set.
+TRAFFIC_BYTES = {}
+
 # workload constants (C2)
 ROWS_PER_GPU = 100_000_000
 PRIVACY_IDS_PER_GPU = 1_000_000
@@ -98,6 +103,7 @@ def main():
     args = parse()
     import torch
     import torch.distributed as dist
+    from pipelinedp_amd import _native as N
     from pipelinedp_amd import executor as X
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,19 +130,18 @@ def main():
     P_pad = ((P + world - 1) // world) * world
     slice_len = P_pad // world
     ws = X.BoundWorkspace()
+    plan = X.bound_plan(n, U, P_pad, bounding)
     acc = X.new_accumulators(P_pad, bounding, device)
     seed_base = int.from_bytes(os.urandom(8), "little")
 
-    def step(i, timer=None):
+    def step(i):
         for t in acc.values():
             if t is not None:
                 t.zero_()
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
-                           check_keys=False, timer=timer)
+                           check_keys=False)
         if world > 1:
-            if timer is not None:
-                timer.mark("exchange")
             part = {}
             for k, t in acc.items():
                 if t is None:
@@ -145,14 +150,12 @@ def main():
                 dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM)
                 part[k] = out
             mine = {k: part.get(k) for k in acc}
-            if timer is not None:
-                timer.mark("end_exchange")
         else:
             mine = acc
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
                                           seed_noise=seed_base ^ (i * 104729 + 2),
-                                          partition_offset=rank * slice_len, timer=timer)
+                                          partition_offset=rank * slice_len)
         return n_kept
 
     for i in range(args.warmup):
@@ -161,31 +164,29 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timer = X.StageTimer()
+    N.profiler_enable(True)  # HIP events around every library kernel, on its launch stream
     t0 = time.perf_counter()
     kept = 0
     for i in range(args.steps):
-        kept = step(args.warmup + i, timer)
+        kept = step(args.warmup + i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kernels = N.profiler_report()
+    N.profiler_enable(False)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stages = {k: v / args.steps for k, v in timer.durations().items()}  # ms per step
-    # algorithmic bytes per launch of each stage (DESIGN.md "Kernels")
-    slots = U * L0
-    alg_bytes = {
-        "sketch": 16.0 * n,                       # pid + pk
-        "rows": 16.0 * n,                         # pid + pk
-        "reduce": slots * 12.0 + slots * LINF * 8.0 * 0.5 + P * 8.0 * 3,  # sketch+cnt, gathers, accs
-        "select": P * (8.0 + 1.0 + 8.0),
-    }
-    dom = max((k for k in stages if k in alg_bytes), key=lambda k: stages[k])
-    achieved = alg_bytes[dom] / (stages[dom] * 1e-3) / 1e9
+    kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}  # average ms per launch
+    launches_per_step = {k: v[1] / args.steps for k, v in kernels.items()}
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches_per_step[k])
+    # algorithmic bytes of the path: 24 B per input row (pid, pk,
+    # value), attributed to the dominant kernel's launch
+    alg_bytes = 24.0 * n
+    achieved = alg_bytes / (kernel_ms[dom] * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     total_rows = n * world * args.steps
     value_rows_s = total_rows / elapsed
@@ -211,13 +212,14 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": {"sketch": "k_pair_sketch", "rows": "k_pair_rows", "reduce": "k_reduce_pairs",
-                       "select": "k_select+compact+noise", "exchange": "rccl"}.get(dom, dom),
+            "kernel": dom,
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": TRAFFIC_BYTES.get(dom),
+            "bytes_per_launch": alg_bytes,
+            "avg_ms": kernel_ms[dom],
         },
         "path_roofline": {
             "achieved": path_bytes / (ms_per_step * 1e-3) / 1e9,
@@ -225,7 +227,9 @@ def main():
             "frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "bytes_per_step": path_bytes,
         },
-        "stage_ms": stages,
+        "kernel_ms": kernel_ms,
+        "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
+                       "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes},
         "partitions_kept": kept,
         "cpu_baseline": None,
     }

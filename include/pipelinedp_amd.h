@@ -212,6 +212,16 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
  * (synchronises `stream`). */
 int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
 
+/* Kernel profiler: when enabled, every kernel launch of this library is
+ * bracketed by HIP events recorded on its launch stream.  enable(1) clears
+ * previous records; report() synchronises on them and returns, per kernel
+ * name (first-launch order), the summed milliseconds and the launch count.
+ * `names` is max_entries * PDP_PROF_NAME_LEN bytes. */
+#define PDP_PROF_NAME_LEN 64
+int pdp_profiler_enable(int enable);
+int pdp_profiler_report(int32_t max_entries, char* names, double* total_ms, int64_t* calls,
+                        int32_t* n_entries);
+
 #ifdef __cplusplus
 }
 #endif

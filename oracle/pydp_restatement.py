@@ -34,7 +34,10 @@ def _phi(x):
 def _gauss_delta(sigma, eps, l2):
     a = l2 / (2.0 * sigma)
     b = eps * sigma / l2
-    return _phi(a - b) - math.exp(eps) * _phi(-a - b)
+    if eps < 700.0:
+        return _phi(a - b) - math.exp(eps) * _phi(-a - b)
+    with np.errstate(over="ignore", invalid="ignore"):  # C++ double: inf * 0 = NaN
+        return float(np.float64(_phi(a - b)) - np.exp(np.float64(eps)) * np.float64(_phi(-a - b)))
 
 
 def calibrate_gaussian_sigma(eps, delta, l2):
@@ -92,7 +95,7 @@ def truncated_geometric_table(eps, delta, l0):
         e, d = eps / l0, adjusted_delta(delta, l0)
         p, table = 0.0, [0.0]
         while p < 1.0 and len(table) < (1 << 22) and d > 0:
-            p = min(math.exp(e) * p + d, 1.0 - math.exp(-e) * (1.0 - p - d), 1.0)
+            p = min(math.exp(min(e, 700.0)) * p + d, 1.0 - math.exp(-e) * (1.0 - p - d), 1.0)
             table.append(p)
         _tg_cache[key] = table
     return _tg_cache[key]

@@ -44,7 +44,10 @@ EXPORTED_SYMBOLS = (
     "pdp_compact",
     "pdp_noise_metrics",
     "pdp_bound_error_flags",
+    "pdp_profiler_enable",
+    "pdp_profiler_report",
 )
+PROF_NAME_LEN = 64
 
 
 class NativeLibraryError(RuntimeError):
@@ -144,6 +147,8 @@ def _declare(lib):
         "pdp_noise_metrics": (ctypes.c_int, [P(MetricOp), i32, vp, i64, vp, i64,
                                              P(PartitionAccumulators), i32, vp, vp, i64, u64, vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
+        "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
+        "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -184,3 +189,23 @@ def check(rc: int, what: str):
         msg = lib().pdp_last_error()
         msg = msg.decode() if msg else ""
         raise NativeLibraryError(f"{what} failed with code {rc}: {msg}")
+
+
+def profiler_enable(on: bool = True):
+    """Starts (clears) or stops per-kernel HIP-event timing in the library."""
+    check(lib().pdp_profiler_enable(1 if on else 0), "pdp_profiler_enable")
+
+
+def profiler_report(max_entries: int = 64):
+    """{kernel name: (total ms, launches)} since profiler_enable (synchronises)."""
+    names = ctypes.create_string_buffer(max_entries * PROF_NAME_LEN)
+    total = (ctypes.c_double * max_entries)()
+    calls = (ctypes.c_int64 * max_entries)()
+    n = ctypes.c_int32(0)
+    check(lib().pdp_profiler_report(max_entries, names, total, calls, ctypes.byref(n)),
+          "pdp_profiler_report")
+    out = {}
+    for k in range(n.value):
+        raw = names.raw[k * PROF_NAME_LEN:(k + 1) * PROF_NAME_LEN]
+        out[raw.split(b"\0", 1)[0].decode()] = (total[k], calls[k])
+    return out

@@ -14,13 +14,18 @@
 // Two execution paths, same results:
 //
 //  BUCKETED (default when the per-privacy-id state fits LDS)
-//    k_part_hist     tile histogram of bucket = pid >> bucket_bits      (8 B/row)
-//    k_scan_*        exclusive scan of the bucket-major tile counts
-//    k_part_scatter  rows -> bucket order as (pair key u64, row u32)  (16 B in, 12 B out)
-//    k_bucket_bound  one workgroup per bucket, all sampling state in LDS:
-//                    B1 bottom-l0 pair sketch per pid, B2 per-pair row count
-//                    + bottom-linf row sketch, B3 gather the sampled values
-//                    and merge each kept pair into the partition accumulators
+//    Privacy ids are grouped in buckets of 2^bucket_bits ids (one LDS-sized
+//    workgroup each) and buckets in super-buckets of 2^super_bits buckets, so
+//    that every partitioning pass writes to <= 64 destinations per workgroup
+//    (long coalesced runs; ~2000 direct destinations thrash L2 5x).
+//    k_part_hist       per-tile histogram of bucket = pid >> bucket_bits  (8 B/row)
+//    k_transpose_counts, k_scan_*   bucket-major exclusive offsets
+//    k_scatter_l1      rows -> super-bucket order (pair key u64, row u32)  (16 B in, 12 B out)
+//    k_scatter_l2      super-bucket chunks -> bucket order                 (12 B in, 12 B out)
+//    k_bucket_bound    one workgroup per bucket, all sampling state in LDS:
+//                      B1 bottom-l0 pair sketch per pid, B2 per-pair row count
+//                      + bottom-linf row sketch, B3 gather the sampled values
+//                      and merge each kept pair into the partition accumulators
 //  GLOBAL (fallback for large l0 * linf)
 //    k_pair_sketch / k_pair_rows / k_reduce_pairs: the same sketches in HBM,
 //    updated with device-scope atomics.
@@ -31,10 +36,14 @@ namespace {
 
 constexpr int kPartThreads = 512;
 constexpr int64_t kTileRows = 65536;
+constexpr int kUnroll = 8;
 constexpr int kBucketThreads = 1024;
 constexpr int64_t kLdsBudget = 128 * 1024;
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
+constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
+constexpr int kL2Items = 16;
+constexpr int64_t kL2Chunk = (int64_t)kPartThreads * kL2Items;
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
@@ -42,8 +51,10 @@ struct Plan {
   int algorithm;   // PDP_ALGO_*
   int pk_bits;
   int bucket_bits;
+  int super_bits;
   int rand_shift;
   int64_t n_buckets;
+  int64_t n_supers;
   int64_t n_tiles;
   int64_t lds_bytes;
 };
@@ -59,22 +70,24 @@ Plan make_plan(const pdp_bound_config* c) {
   p.pk_bits = bits_for(c->n_partitions);
   const int64_t per_pid = per_pid_lds(c);
   const int64_t max_pids = kLdsBudget / per_pid;
-  int s = -1;
+  int s = -1, s2 = 0;
   if (max_pids >= 16) {
     s = 0;
     while (((int64_t)2 << s) <= max_pids) ++s;          // largest 2^s <= max_pids
     const int u_bits = bits_for(c->n_privacy_ids);
     if (s > u_bits) s = u_bits;                          // one bucket covers all pids
-    if (64 - p.pk_bits - s < kMinRandomBits) s = -1;
-    // one partitioning pass: the per-tile bucket histogram must fit LDS
-    if (s >= 0 && ((c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s) > kMaxBuckets) s = -1;
+    const int64_t nb = (c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s;
+    while (((nb + ((int64_t)1 << s2) - 1) >> s2) > kMaxSupers) ++s2;
+    if (nb > kMaxBuckets || 64 - p.pk_bits - s - s2 < kMinRandomBits) s = -1;
   }
   const int auto_algo = s >= 0 ? PDP_ALGO_BUCKETED : PDP_ALGO_GLOBAL_SKETCH;
   p.algorithm = c->algorithm == PDP_ALGO_AUTO ? auto_algo : c->algorithm;
   if (p.algorithm == PDP_ALGO_BUCKETED && s < 0) p.algorithm = -1;  // infeasible
   p.bucket_bits = s < 0 ? 0 : s;
-  p.rand_shift = p.pk_bits + p.bucket_bits;
+  p.super_bits = s < 0 ? 0 : s2;
+  p.rand_shift = p.pk_bits + p.bucket_bits + p.super_bits;
   p.n_buckets = (c->n_privacy_ids + ((int64_t)1 << p.bucket_bits) - 1) >> p.bucket_bits;
+  p.n_supers = (p.n_buckets + ((int64_t)1 << p.super_bits) - 1) >> p.super_bits;
   p.n_tiles = (c->n_rows + kTileRows - 1) / kTileRows;
   if (p.n_tiles < 1) p.n_tiles = 1;
   p.lds_bytes = ((int64_t)1 << p.bucket_bits) * per_pid;
@@ -87,7 +100,7 @@ struct Ws {
   // global path
   uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
   // bucketed path
-  uint64_t counts, chunk_sums, keys, rowidx;
+  uint64_t counts_tm, counts, chunk_sums, cursor, super_base, keys1, rows1, keys2, rows2;
   uint64_t total;
 };
 
@@ -108,12 +121,23 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.nsum2 = off; off = align256(off + slots * 8);
     }
   } else {
-    const uint64_t n_counts = (uint64_t)p.n_buckets * (uint64_t)p.n_tiles + 1;
+    const uint64_t n_counts = (uint64_t)p.n_buckets * (uint64_t)p.n_tiles;
     const uint64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
-    w.counts = off; off = align256(off + n_counts * 4);
+    const uint64_t n = (uint64_t)c->n_rows;
+    w.counts_tm = off; off = align256(off + n_counts * 4);
+    w.counts = off; off = align256(off + (n_counts + 1) * 4);
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
-    w.keys = off; off = align256(off + (uint64_t)c->n_rows * 8);
-    w.rowidx = off; off = align256(off + (uint64_t)c->n_rows * 4);
+    w.cursor = off; off = align256(off + (uint64_t)p.n_buckets * 4);
+    w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
+    w.keys1 = off; off = align256(off + n * 8);
+    w.rows1 = off; off = align256(off + n * 4);
+    if (p.super_bits > 0) {
+      w.keys2 = off; off = align256(off + n * 8);
+      w.rows2 = off; off = align256(off + n * 4);
+    } else {
+      w.keys2 = w.keys1;
+      w.rows2 = w.rows1;
+    }
   }
   w.total = off;
   return w;
@@ -142,11 +166,12 @@ int validate(const pdp_bound_config* c) {
   return PDP_OK;
 }
 
+
 struct KP {  // kernel parameters
   int64_t n, U, P;
   int l0, linf;
-  int pk_bits, bucket_bits, rand_shift;
-  int64_t n_buckets, n_tiles;
+  int pk_bits, bucket_bits, super_bits, rand_shift;
+  int64_t n_buckets, n_supers, n_tiles;
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
   ClipParams clip;
@@ -161,8 +186,10 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.linf = c->linf;
   k.pk_bits = p.pk_bits;
   k.bucket_bits = p.bucket_bits;
+  k.super_bits = p.super_bits;
   k.rand_shift = p.rand_shift;
   k.n_buckets = p.n_buckets;
+  k.n_supers = p.n_supers;
   k.n_tiles = p.n_tiles;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
@@ -289,24 +316,302 @@ __global__ void __launch_bounds__(kBlock) k_reduce_pairs(KP kp, const void* __re
 }
 
 // ========================================================== BUCKETED path ==
+// A key whose random part is all ones is "dead" (non-public or invalid
+// partition): it keeps its pid bits so it stays in its bucket, and is skipped.
+__device__ __forceinline__ bool dead_key(uint64_t x, int rand_shift) {
+  return (x | ((1ULL << rand_shift) - 1)) == kEmpty;
+}
+
 __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t* __restrict__ pid,
-                                                            unsigned* __restrict__ counts, unsigned* err) {
+                                                            unsigned* __restrict__ counts_tm, unsigned* err) {
   extern __shared__ unsigned hist[];
   for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) hist[b] = 0;
   __syncthreads();
   const int64_t t0 = (int64_t)blockIdx.x * kTileRows;
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
-  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-    const int64_t u = pid[i];
-    if (u < 0 || u >= kp.U) {
-      atomicOr(err, 1u);
-      continue;
+  for (int64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += (int64_t)blockDim.x * kUnroll) {
+    int64_t u[kUnroll];
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) {
+      const int64_t i = i0 + (int64_t)k * blockDim.x;
+      u[k] = i < t1 ? pid[i] : INT64_MIN;
     }
-    atomicAdd(hist + (u >> kp.bucket_bits), 1u);
+#pragma unroll
+    for (int k = 0; k < kUnroll; ++k) {
+      if (u[k] == INT64_MIN) continue;
+      if (u[k] < 0 || u[k] >= kp.U) {
+        atomicOr(err, 1u);
+        continue;
+      }
+      atomicAdd(hist + (u[k] >> kp.bucket_bits), 1u);
+    }
   }
   __syncthreads();
-  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x)
-    counts[b * kp.n_tiles + blockIdx.x] = hist[b];
+  unsigned* row = counts_tm + (int64_t)blockIdx.x * kp.n_buckets;  // tile-major: coalesced
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) row[b] = hist[b];
+}
+
+// [n_tiles][n_buckets] -> [n_buckets][n_tiles]
+__global__ void __launch_bounds__(kBlock) k_transpose_counts(const unsigned* __restrict__ in, int64_t rows,
+                                                             int64_t cols, unsigned* __restrict__ out) {
+  __shared__ unsigned tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  for (int k = ty; k < 64; k += 4) {
+    const int64_t r = r0 + k, c = c0 + tx;
+    tile[k][tx] = (r < rows && c < cols) ? in[r * cols + c] : 0;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {
+    const int64_t c = c0 + k, r = r0 + tx;
+    if (c < cols && r < rows) out[c * rows + r] = tile[tx][k];
+  }
+}
+
+// cursor[b] = start of bucket b; super_base[B] = start of super-bucket B
+__global__ void __launch_bounds__(kBlock) k_init_cursors(KP kp, const unsigned* __restrict__ counts,
+                                                         unsigned* __restrict__ cursor,
+                                                         unsigned* __restrict__ super_base) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < kp.n_buckets) cursor[i] = counts[i * kp.n_tiles];
+  if (i <= kp.n_supers) {
+    const int64_t b = i << kp.super_bits;
+    super_base[i] = counts[(b < kp.n_buckets ? b : kp.n_buckets) * kp.n_tiles];
+  }
+}
+
+// Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
+__global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
+                                                             const int64_t* __restrict__ pk,
+                                                             const uint8_t* __restrict__ allowed,
+                                                             const unsigned* __restrict__ counts,
+                                                             const unsigned* __restrict__ super_base,
+                                                             unsigned long long* __restrict__ keys1,
+                                                             unsigned* __restrict__ rows1, unsigned* err) {
+  __shared__ unsigned cur[kMaxSupers];
+  const int64_t t = blockIdx.x;
+  for (int B = threadIdx.x; B < kMaxSupers; B += blockDim.x) cur[B] = 0;
+  __syncthreads();
+  // rows of super-bucket B in tiles < t = sum over its buckets of (offset[b][t] - offset[b][0])
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) {
+    const unsigned v = counts[b * kp.n_tiles + t] - counts[b * kp.n_tiles];
+    if (v) atomicAdd(cur + (b >> kp.super_bits), v);
+  }
+  __syncthreads();
+  for (int B = threadIdx.x; B < kp.n_supers; B += blockDim.x) cur[B] += super_base[B];
+  __syncthreads();
+  const int64_t t0 = t * kTileRows;
+  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  const int mid_bits = kp.bucket_bits + kp.super_bits;
+  const uint64_t mid_mask = (1ULL << mid_bits) - 1;
+  const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
+  for (int64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += (int64_t)blockDim.x * kUnroll) {
+    int64_t u[kUnroll], k[kUnroll];
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      u[q] = i < t1 ? pid[i] : -1;
+      k[q] = i < t1 ? pk[i] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      if (u[q] < 0 || u[q] >= kp.U) continue;  // flagged by k_part_hist, not counted
+      const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
+      uint64_t x;
+      if (k[q] < 0 || k[q] >= kp.P) {
+        atomicOr(err, 1u);
+        x = dead | midv;
+      } else if (allowed != nullptr && allowed[k[q]] == 0) {
+        x = dead | midv;
+      } else {
+        x = pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift);
+      }
+      const unsigned pos = atomicAdd(cur + (u[q] >> mid_bits), 1u);
+      keys1[pos] = x;
+      rows1[pos] = (unsigned)(i0 + (int64_t)q * blockDim.x);
+    }
+  }
+}
+
+// Level 2: chunks of one super-bucket -> its 2^super_bits bucket regions.
+__global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
+                                                             unsigned* __restrict__ cursor,
+                                                             const unsigned long long* __restrict__ keys1,
+                                                             const unsigned* __restrict__ rows1,
+                                                             unsigned long long* __restrict__ keys2,
+                                                             unsigned* __restrict__ rows2) {
+  extern __shared__ unsigned lds[];
+  __shared__ int64_t s_first, s_r0, s_r1;
+  const int nsub = 1 << kp.super_bits;
+  unsigned* hist = lds;          // [nsub]
+  unsigned* cur = lds + nsub;    // [nsub]
+  if (threadIdx.x == 0) {
+    // locate this workgroup's (super-bucket, chunk)
+    int64_t g = blockIdx.x, B = 0, first = -1, r0 = 0, r1 = 0;
+    for (; B < kp.n_supers; ++B) {
+      const int64_t lo = super_base[B], hi = super_base[B + 1];
+      const int64_t nch = (hi - lo + kL2Chunk - 1) / kL2Chunk;
+      if (g < nch) {
+        first = B << kp.super_bits;
+        r0 = lo + g * kL2Chunk;
+        r1 = r0 + kL2Chunk < hi ? r0 + kL2Chunk : hi;
+        break;
+      }
+      g -= nch;
+    }
+    s_first = first;
+    s_r0 = r0;
+    s_r1 = r1;
+  }
+  for (int s = threadIdx.x; s < nsub; s += blockDim.x) hist[s] = 0;
+  __syncthreads();
+  if (s_first < 0) return;  // grid is an upper bound on the chunk count
+  const int64_t r0 = s_r0, r1 = s_r1;
+  const int sub_shift = kp.pk_bits + kp.bucket_bits;
+  const uint64_t sub_mask = (uint64_t)nsub - 1;
+  unsigned long long x[kL2Items];
+  unsigned r[kL2Items];
+#pragma unroll
+  for (int q = 0; q < kL2Items; ++q) {
+    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
+    x[q] = i < r1 ? keys1[i] : 0;
+    r[q] = i < r1 ? rows1[i] : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kL2Items; ++q) {
+    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
+    if (i < r1) atomicAdd(hist + ((x[q] >> sub_shift) & sub_mask), 1u);
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < nsub; s += blockDim.x) {
+    const int64_t b = s_first + s;
+    cur[s] = (hist[s] && b < kp.n_buckets) ? atomicAdd(cursor + b, hist[s]) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kL2Items; ++q) {
+    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
+    if (i >= r1) continue;
+    const unsigned pos = atomicAdd(cur + ((x[q] >> sub_shift) & sub_mask), 1u);
+    keys2[pos] = x[q];
+    rows2[pos] = r[q];
+  }
+}
+
+template <int VALUE_KIND, bool KEEP_ALL_ROWS>
+__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const unsigned long long* __restrict__ keys,
+                                                                 const unsigned* __restrict__ rowidx,
+                                                                 const unsigned* __restrict__ offsets,
+                                                                 const void* __restrict__ value,
+                                                                 pdp_partition_accumulators acc) {
+  extern __shared__ unsigned long long smem[];
+  const int64_t S = (int64_t)1 << kp.bucket_bits;
+  const int l0 = kp.l0;
+  const int64_t n_slots = S * l0;
+  unsigned long long* sk = smem;                      // [S*l0] pair sketch per pid
+  unsigned long long* rsk = sk + n_slots;             // bounded: [S*l0*linf] row sketches
+  double* tot = (double*)(sk + n_slots);              // keep-all: [3][S*l0] pair sums
+  unsigned* cnt = KEEP_ALL_ROWS ? (unsigned*)(tot + 3 * n_slots) : (unsigned*)(rsk + n_slots * kp.linf);
+  for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
+    sk[t] = kEmpty;
+    cnt[t] = 0;
+  }
+  if (!KEEP_ALL_ROWS) {
+    for (int64_t t = threadIdx.x; t < n_slots * kp.linf; t += blockDim.x) rsk[t] = kEmpty;
+  } else {
+    for (int64_t t = threadIdx.x; t < 3 * n_slots; t += blockDim.x) tot[t] = 0.0;
+  }
+  __syncthreads();
+  const int64_t b = blockIdx.x;
+  const int64_t begin = offsets[b * kp.n_tiles];
+  const int64_t end = offsets[(b + 1) * kp.n_tiles];  // offsets has n_buckets*n_tiles+1 entries
+  const uint64_t bmask = (uint64_t)S - 1;
+  const int64_t step = (int64_t)blockDim.x * kUnroll;
+  // B1: bottom-l0 distinct pair keys per privacy id
+  for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += step) {
+    uint64_t xs[kUnroll];
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      xs[q] = i < end ? keys[i] : kEmpty;
+    }
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const uint64_t x = xs[q];
+      if (dead_key(x, kp.rand_shift)) continue;
+      unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
+      if (x >= s[l0 - 1]) continue;
+      sketch_insert(s, l0, x);
+    }
+  }
+  __syncthreads();
+  // B2: rows of kept pairs
+  const int flags = kp.clip.flags;
+  for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += step) {
+    uint64_t xs[kUnroll];
+    uint32_t rs_[kUnroll];
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      xs[q] = i < end ? keys[i] : kEmpty;
+      rs_[q] = i < end ? rowidx[i] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < kUnroll; ++q) {
+      const uint64_t x = xs[q];
+      if (dead_key(x, kp.rand_shift)) continue;
+      const int64_t pl = (x >> kp.pk_bits) & bmask;
+      const unsigned long long* s = sk + pl * l0;
+      if (x > s[l0 - 1]) continue;
+      const int j = sketch_find(s, l0, x);
+      if (j < 0) continue;
+      const int64_t slot = pl * l0 + j;
+      atomicAdd(cnt + slot, 1u);
+      const uint32_t r = rs_[q];
+      if (!KEEP_ALL_ROWS) {
+        const uint64_t y = row_key(kp.row_seed, kp.row_offset + r, r);
+        unsigned long long* rs = rsk + slot * kp.linf;
+        if (y < rs[kp.linf - 1]) sketch_insert(rs, kp.linf, y);
+      } else if (VALUE_KIND != PDP_VALUE_NONE) {
+        double v;
+        long long iv;
+        load_value<VALUE_KIND>(value, r, &v, &iv);
+        if (flags & PDP_SUM_PER_PARTITION) {
+          if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(tot + slot), (unsigned long long)iv);
+          else atomicAdd(tot + slot, v);
+        } else if (flags & PDP_ACC_SUM) {
+          if (flags & PDP_SUM_INT)
+            atomicAdd((unsigned long long*)(tot + slot),
+                      (unsigned long long)clamp_ll(iv, (long long)kp.clip.lo, (long long)kp.clip.hi));
+          else atomicAdd(tot + slot, fmin(fmax(v, kp.clip.lo), kp.clip.hi));
+        }
+        if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
+          const double c = fmin(fmax(v, kp.clip.lo), kp.clip.hi) - kp.clip.mid;
+          if (flags & PDP_ACC_NSUM) atomicAdd(tot + n_slots + slot, c);
+          if (flags & PDP_ACC_NSUM2) atomicAdd(tot + 2 * n_slots + slot, c * c);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // B3: merge every kept pair into its partition
+  for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
+    const uint64_t x = sk[slot];
+    if (x == kEmpty) continue;
+    const int64_t p = (int64_t)(x & kp.pk_mask);
+    const unsigned c = cnt[slot];
+    if (c == 0) continue;
+    PairSums ps;
+    if (!KEEP_ALL_ROWS) {
+      const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
+      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot * kp.linf, m, value, kp.clip);
+    } else if (VALUE_KIND != PDP_VALUE_NONE) {
+      ps = pair_sums_from_totals((long long)c, tot[slot], tot[n_slots + slot], tot[2 * n_slots + slot], kp.clip);
+    } else {
+      ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
+    }
+    add_pair_to_partition(acc, p, ps, flags);
+  }
 }
 
 // exclusive scan of u32 counts[0..n) in place, total -> counts[n]
@@ -381,141 +686,17 @@ __global__ void __launch_bounds__(kBlock) k_scan_apply(unsigned* v, int64_t n,
   if (blockIdx.x == 0 && threadIdx.x == 0) v[n] = chunk_sums[n_chunks];
 }
 
-__global__ void __launch_bounds__(kPartThreads) k_part_scatter(KP kp, const int64_t* __restrict__ pid,
-                                                               const int64_t* __restrict__ pk,
-                                                               const uint8_t* __restrict__ allowed,
-                                                               const unsigned* __restrict__ offsets,
-                                                               unsigned long long* __restrict__ keys,
-                                                               unsigned* __restrict__ rowidx, unsigned* err) {
-  extern __shared__ unsigned cursor[];
-  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x)
-    cursor[b] = offsets[b * kp.n_tiles + blockIdx.x];
-  __syncthreads();
-  const int64_t t0 = (int64_t)blockIdx.x * kTileRows;
-  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
-  const uint64_t bmask = (1ULL << kp.bucket_bits) - 1;
-  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-    const int64_t u = pid[i];
-    if (u < 0 || u >= kp.U) continue;  // flagged by k_part_hist, not counted
-    const int64_t k = pk[i];
-    const unsigned pos = atomicAdd(cursor + (u >> kp.bucket_bits), 1u);
-    uint64_t x;
-    if (k < 0 || k >= kp.P) {
-      atomicOr(err, 1u);
-      x = kEmpty;
-    } else if (allowed != nullptr && allowed[k] == 0) {
-      x = kEmpty;
-    } else {
-      x = pair_key(kp.seed, u, k, ((uint64_t)u & bmask) << kp.pk_bits, kp.rand_shift);
-    }
-    keys[pos] = x;
-    rowidx[pos] = (unsigned)i;
-  }
-}
-
-template <int VALUE_KIND, bool KEEP_ALL_ROWS>
-__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const unsigned long long* __restrict__ keys,
-                                                                 const unsigned* __restrict__ rowidx,
-                                                                 const unsigned* __restrict__ offsets,
-                                                                 const void* __restrict__ value,
-                                                                 pdp_partition_accumulators acc) {
-  extern __shared__ unsigned long long smem[];
-  const int64_t S = (int64_t)1 << kp.bucket_bits;
-  const int l0 = kp.l0;
-  const int64_t n_slots = S * l0;
-  unsigned long long* sk = smem;                      // [S*l0] pair sketch per pid
-  unsigned long long* rsk = sk + n_slots;             // bounded: [S*l0*linf] row sketches
-  double* tot = (double*)(sk + n_slots);              // keep-all: [3][S*l0] pair sums
-  unsigned* cnt = KEEP_ALL_ROWS ? (unsigned*)(tot + 3 * n_slots) : (unsigned*)(rsk + n_slots * kp.linf);
-  for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
-    sk[t] = kEmpty;
-    cnt[t] = 0;
-  }
-  if (!KEEP_ALL_ROWS) {
-    for (int64_t t = threadIdx.x; t < n_slots * kp.linf; t += blockDim.x) rsk[t] = kEmpty;
-  } else {
-    for (int64_t t = threadIdx.x; t < 3 * n_slots; t += blockDim.x) tot[t] = 0.0;
-  }
-  __syncthreads();
-  const int64_t b = blockIdx.x;
-  const int64_t begin = offsets[b * kp.n_tiles];
-  const int64_t end = offsets[(b + 1) * kp.n_tiles];  // counts has n_buckets*n_tiles+1 entries
-  const uint64_t bmask = (uint64_t)S - 1;
-  // B1: bottom-l0 distinct pair keys per privacy id
-  for (int64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
-    const uint64_t x = keys[i];
-    if (x == kEmpty) continue;
-    unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
-    if (x >= s[l0 - 1]) continue;
-    sketch_insert(s, l0, x);
-  }
-  __syncthreads();
-  // B2: rows of kept pairs
-  const int flags = kp.clip.flags;
-  for (int64_t i = begin + threadIdx.x; i < end; i += blockDim.x) {
-    const uint64_t x = keys[i];
-    if (x == kEmpty) continue;
-    const int64_t pl = (x >> kp.pk_bits) & bmask;
-    const unsigned long long* s = sk + pl * l0;
-    if (x > s[l0 - 1]) continue;
-    const int j = sketch_find(s, l0, x);
-    if (j < 0) continue;
-    const int64_t slot = pl * l0 + j;
-    atomicAdd(cnt + slot, 1u);
-    const uint32_t r = rowidx[i];
-    if (!KEEP_ALL_ROWS) {
-      const uint64_t y = row_key(kp.row_seed, kp.row_offset + r, r);
-      unsigned long long* rs = rsk + slot * kp.linf;
-      if (y < rs[kp.linf - 1]) sketch_insert(rs, kp.linf, y);
-    } else if (VALUE_KIND != PDP_VALUE_NONE) {
-      double v;
-      long long iv;
-      load_value<VALUE_KIND>(value, r, &v, &iv);
-      if (flags & PDP_SUM_PER_PARTITION) {
-        if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(tot + slot), (unsigned long long)iv);
-        else atomicAdd(tot + slot, v);
-      } else if (flags & PDP_ACC_SUM) {
-        if (flags & PDP_SUM_INT)
-          atomicAdd((unsigned long long*)(tot + slot),
-                    (unsigned long long)clamp_ll(iv, (long long)kp.clip.lo, (long long)kp.clip.hi));
-        else atomicAdd(tot + slot, fmin(fmax(v, kp.clip.lo), kp.clip.hi));
-      }
-      if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
-        const double c = fmin(fmax(v, kp.clip.lo), kp.clip.hi) - kp.clip.mid;
-        if (flags & PDP_ACC_NSUM) atomicAdd(tot + n_slots + slot, c);
-        if (flags & PDP_ACC_NSUM2) atomicAdd(tot + 2 * n_slots + slot, c * c);
-      }
-    }
-  }
-  __syncthreads();
-  // B3: merge every kept pair into its partition
-  for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
-    const uint64_t x = sk[slot];
-    if (x == kEmpty) continue;
-    const int64_t p = (int64_t)(x & kp.pk_mask);
-    const unsigned c = cnt[slot];
-    if (c == 0) continue;
-    PairSums ps;
-    if (!KEEP_ALL_ROWS) {
-      const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
-      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot * kp.linf, m, value, kp.clip);
-    } else if (VALUE_KIND != PDP_VALUE_NONE) {
-      ps = pair_sums_from_totals((long long)c, tot[slot], tot[n_slots + slot], tot[2 * n_slots + slot], kp.clip);
-    } else {
-      ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
-    }
-    add_pair_to_partition(acc, p, ps, flags);
-  }
-}
 
 // ---------------------------------------------------------- launchers --
 template <int VK, bool KA>
 int launch_global_rows(const KP& kp, hipStream_t st, const int64_t* pid, const int64_t* pk, const void* value,
                        const uint8_t* allowed, char* ws, const Ws& w) {
+  PDP_PROF_BEGIN("k_pair_rows", st);
   hipLaunchKernelGGL((k_pair_rows<VK, KA>), dim3(grid_for(kp.n)), dim3(kBlock), 0, st, kp, pid, pk, value,
                      allowed, (const unsigned long long*)(ws + w.sketch), (unsigned*)(ws + w.cnt),
                      KA ? nullptr : (unsigned long long*)(ws + w.rows), KA ? (double*)(ws + w.fsum) : nullptr,
                      KA ? (double*)(ws + w.nsum) : nullptr, KA ? (double*)(ws + w.nsum2) : nullptr);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }
@@ -523,11 +704,13 @@ int launch_global_rows(const KP& kp, hipStream_t st, const int64_t* pid, const i
 template <int VK, bool KA>
 int launch_global_reduce(const KP& kp, hipStream_t st, const void* value, const char* ws, const Ws& w,
                          const pdp_partition_accumulators& acc) {
+  PDP_PROF_BEGIN("k_reduce_pairs", st);
   hipLaunchKernelGGL((k_reduce_pairs<VK, KA>), dim3(grid_for(kp.U * kp.l0)), dim3(kBlock), 0, st, kp, value,
                      (const unsigned long long*)(ws + w.sketch), (const unsigned*)(ws + w.cnt),
                      KA ? nullptr : (const unsigned long long*)(ws + w.rows),
                      KA ? (const double*)(ws + w.fsum) : nullptr, KA ? (const double*)(ws + w.nsum) : nullptr,
                      KA ? (const double*)(ws + w.nsum2) : nullptr, acc);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }
@@ -538,9 +721,11 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, const char* ws, c
   auto kern = k_bucket_bound<VK, KA>;
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)p.lds_bytes));
+  PDP_PROF_BEGIN("k_bucket_bound", st);
   hipLaunchKernelGGL(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), (unsigned)p.lds_bytes, st, kp,
-                     (const unsigned long long*)(ws + w.keys), (const unsigned*)(ws + w.rowidx),
+                     (const unsigned long long*)(ws + w.keys2), (const unsigned*)(ws + w.rows2),
                      (const unsigned*)(ws + w.counts), value, acc);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }
@@ -636,41 +821,73 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     if (cfg->linf > 0) PDP_HIP_CHECK(hipMemsetAsync(ws + w.rows, 0xFF, slots * (uint64_t)cfg->linf * 8, st));
     else PDP_HIP_CHECK(hipMemsetAsync(ws + w.fsum, 0, w.total - w.fsum, st));
     if (cfg->n_rows == 0) return PDP_OK;
+    PDP_PROF_BEGIN("k_pair_sketch", st);
     hipLaunchKernelGGL(k_pair_sketch, dim3(grid_for(cfg->n_rows)), dim3(kBlock), 0, st, kp, privacy_id,
                        partition_key, pk_allowed, (unsigned long long*)(ws + w.sketch), err);
+    PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     return dispatch<GlobalRows>(cfg->value_kind, cfg->linf == 0, kp, st, privacy_id, partition_key, value,
                                 pk_allowed, ws, w);
   }
-  // bucketed: histogram -> scan -> scatter
+  // bucketed: histogram -> transpose -> scan -> cursors -> scatter (1 or 2 levels)
   const int64_t n_counts = p.n_buckets * p.n_tiles;
   const int64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
   unsigned* counts = (unsigned*)(ws + w.counts);
-  unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);
-  const size_t hist_lds = (size_t)p.n_buckets * 4;
-  if (hist_lds > 160 * 1024) return set_error(PDP_E_UNSUPPORTED, "too many privacy-id buckets for one pass");
   if (cfg->n_rows == 0) {
     PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (n_counts + 1) * 4, st));
     return PDP_OK;
   }
+  unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
+  unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);
+  const size_t hist_lds = (size_t)p.n_buckets * 4;
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)hist_lds));
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)hist_lds));
+  PDP_PROF_BEGIN("k_part_hist", st);
   hipLaunchKernelGGL(k_part_hist, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
-                     counts, err);
+                     counts_tm, err);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_transpose_counts", st);
+  hipLaunchKernelGGL(k_transpose_counts, dim3((unsigned)((p.n_buckets + 63) / 64), (unsigned)((p.n_tiles + 63) / 64)),
+                     dim3(kBlock), 0, st, counts_tm, p.n_tiles, p.n_buckets, counts);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scan_chunks", st);
   hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scan_top", st);
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, st, chunk_sums, n_chunks);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scan_apply", st);
   hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums,
                      n_chunks);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
-                     partition_key, pk_allowed, counts, (unsigned long long*)(ws + w.keys),
-                     (unsigned*)(ws + w.rowidx), err);
+  unsigned* cursor = (unsigned*)(ws + w.cursor);
+  unsigned* super_base = (unsigned*)(ws + w.super_base);
+  const int64_t n_init = (p.n_buckets > p.n_supers + 1 ? p.n_buckets : p.n_supers + 1);
+  PDP_PROF_BEGIN("k_init_cursors", st);
+  hipLaunchKernelGGL(k_init_cursors, dim3(grid_for(n_init)), dim3(kBlock), 0, st, kp, counts, cursor, super_base);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scatter_l1", st);
+  hipLaunchKernelGGL(k_scatter_l1, dim3((unsigned)p.n_tiles), dim3(kPartThreads), 0, st, kp, privacy_id,
+                     partition_key, pk_allowed, counts, super_base, (unsigned long long*)(ws + w.keys1),
+                     (unsigned*)(ws + w.rows1), err);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  if (p.super_bits > 0) {
+    const int64_t n_l2 = (cfg->n_rows + kL2Chunk - 1) / kL2Chunk + p.n_supers;
+    const size_t l2_lds = (size_t)2 * ((size_t)1 << p.super_bits) * 4;
+    PDP_PROF_BEGIN("k_scatter_l2", st);
+    hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)n_l2), dim3(kPartThreads), l2_lds, st, kp, super_base, cursor,
+                       (const unsigned long long*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
+                       (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
   return PDP_OK;
 }
 

@@ -228,3 +228,17 @@ __device__ __forceinline__ void add_pair_to_partition(const pdp_partition_accumu
 }
 
 }  // namespace pdp
+
+// ------------------------------------------------------------ profiler --
+// Optional per-launch HIP-event timing (pdp_profiler_enable / _report):
+// PDP_PROF_BEGIN/END bracket a launch on its own stream; disabled = no-op.
+namespace pdp {
+bool profiler_enabled();
+void profiler_begin(const char* name, hipStream_t stream);
+void profiler_end(hipStream_t stream);
+}  // namespace pdp
+
+#define PDP_PROF_BEGIN(name, stream) \
+  do { if (::pdp::profiler_enabled()) ::pdp::profiler_begin(name, stream); } while (0)
+#define PDP_PROF_END(stream) \
+  do { if (::pdp::profiler_enabled()) ::pdp::profiler_end(stream); } while (0)

@@ -235,8 +235,10 @@ int pdp_select_partitions(const pdp_select_config* cfg, const int64_t* row_count
   if (cfg->strategy != PDP_SELECT_PUBLIC && row_count == nullptr)
     return pdp::set_error(PDP_E_INVALID, "row_count is required");
   if (cfg->n_partitions == 0) return PDP_OK;
+  PDP_PROF_BEGIN("k_select", (hipStream_t)stream);
   hipLaunchKernelGGL(k_select, dim3(grid_for(cfg->n_partitions)), dim3(kBlock), 0, (hipStream_t)stream,
                      *cfg, row_count, keep, noised_count);
+  PDP_PROF_END((hipStream_t)stream);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }
@@ -262,11 +264,17 @@ int pdp_compact(const uint8_t* keep, int64_t n, int64_t* out_index, int64_t* out
   if (keep == nullptr || out_index == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
   const int64_t nb = (n + kCompactChunk - 1) / kCompactChunk;
   int64_t* bc = (int64_t*)workspace;
+  PDP_PROF_BEGIN("k_compact_count", st);
   hipLaunchKernelGGL(k_compact_count, dim3((unsigned)nb), dim3(kBlock), 0, st, keep, n, bc);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_compact_scan", st);
   hipLaunchKernelGGL(k_compact_scan, dim3(1), dim3(kBlock), 0, st, bc, nb, out_count);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_compact_write", st);
   hipLaunchKernelGGL(k_compact_write, dim3((unsigned)nb), dim3(kBlock), 0, st, keep, n, bc, out_index);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }
@@ -310,9 +318,11 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
     }
     pack.op[i] = o;
   }
+  PDP_PROF_BEGIN("k_noise_metrics", (hipStream_t)stream);
   hipLaunchKernelGGL(k_noise_metrics, dim3(grid_for(n_kept)), dim3(kBlock), 0, (hipStream_t)stream, pack,
                      n_ops, index, n_kept, n_kept_dev, partition_offset, *acc, sum_is_int, noised_count,
                      out, out_stride, seed);
+  PDP_PROF_END((hipStream_t)stream);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }

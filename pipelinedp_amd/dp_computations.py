@@ -89,7 +89,14 @@ def gaussian_delta(sigma: float, eps: float, l2_sensitivity: float) -> float:
     Balle & Wang 2018): Phi(l2/(2s) - eps s/l2) - e^eps Phi(-l2/(2s) - eps s/l2)."""
     a = l2_sensitivity / (2.0 * sigma)
     b = eps * sigma / l2_sensitivity
-    return _std_normal_cdf(a - b) - math.exp(eps) * _std_normal_cdf(-a - b)
+    if eps < 700.0:
+        return _std_normal_cdf(a - b) - math.exp(eps) * _std_normal_cdf(-a - b)
+    # IEEE double semantics of the C++ restated here: e^eps overflows to inf,
+    # inf * 0 = NaN, and a NaN delta never exceeds the target, so huge budgets
+    # calibrate sigma down to 0 (the reference's "no noise" test budgets).
+    with np.errstate(over="ignore", invalid="ignore"):
+        return float(np.float64(_std_normal_cdf(a - b)) -
+                     np.exp(np.float64(eps)) * np.float64(_std_normal_cdf(-a - b)))
 
 
 def compute_sigma(eps: float, delta: float, l2_sensitivity: float) -> float:
@@ -411,7 +418,7 @@ def truncated_geometric_keep_table(eps: float, delta: float, max_partitions_cont
         raise ValueError(f"delta must be in [0, 1), but {delta} given")
     e = eps / max_partitions_contributed
     d = adjusted_delta(delta, max_partitions_contributed)
-    ee, eme = math.exp(e), math.exp(-e)
+    ee, eme = math.exp(min(e, 700.0)), math.exp(-e)  # e^700 already saturates pi
     table = [0.0]
     p = 0.0
     while len(table) < max_len:
