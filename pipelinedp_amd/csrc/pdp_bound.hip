@@ -42,8 +42,6 @@ constexpr int64_t kLdsBudget = 128 * 1024;
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
 constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
-constexpr int kL2Items = 16;
-constexpr int64_t kL2Chunk = (int64_t)kPartThreads * kL2Items;
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
@@ -380,6 +378,73 @@ __global__ void __launch_bounds__(kBlock) k_init_cursors(KP kp, const unsigned* 
   }
 }
 
+// LDS-staged multi-destination write: the rows of one sub-chunk (ITEMS per
+// thread) are counting-sorted by destination in LDS and each destination's
+// run is then written contiguously at gcur[dest] (coalesced, long runs).
+constexpr int kStageItems = 8;
+constexpr int kStageRows = kPartThreads * kStageItems;  // 4096
+constexpr int kMaxDest = 1024;
+
+struct StageLds {
+  unsigned hist[kMaxDest];
+  unsigned start[kMaxDest];
+  unsigned gcur[kMaxDest];
+  unsigned long long keys[kStageRows];
+  unsigned rows[kStageRows];
+  unsigned short dest[kStageRows];
+};
+
+// phase 1: histogram + local rank (dest < 0 = drop the row)
+__device__ __forceinline__ void stage_count(StageLds& s, int ndest, const int (&d)[kStageItems],
+                                            unsigned (&rank)[kStageItems]) {
+  for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kStageItems; ++q) rank[q] = d[q] >= 0 ? atomicAdd(s.hist + d[q], 1u) : 0;
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of hist by one wave
+    const int lane = threadIdx.x;
+    unsigned carry = 0;
+    for (int base = 0; base < ndest; base += 64) {
+      const unsigned v = base + lane < ndest ? s.hist[base + lane] : 0;
+      unsigned incl = v;
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned up = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += up;
+      }
+      if (base + lane < ndest) s.start[base + lane] = carry + incl - v;
+      carry += __shfl(incl, 63, 64);
+    }
+  }
+  __syncthreads();
+}
+
+// phase 2: place into the LDS stage, then write every run at gcur[dest]
+__device__ __forceinline__ void stage_write(StageLds& s, int ndest, const int (&d)[kStageItems],
+                                            const unsigned (&rank)[kStageItems],
+                                            const unsigned long long (&x)[kStageItems],
+                                            const unsigned (&r)[kStageItems],
+                                            unsigned long long* __restrict__ out_keys,
+                                            unsigned* __restrict__ out_rows) {
+#pragma unroll
+  for (int q = 0; q < kStageItems; ++q) {
+    if (d[q] < 0) continue;
+    const unsigned slot = s.start[d[q]] + rank[q];
+    s.keys[slot] = x[q];
+    s.rows[slot] = r[q];
+    s.dest[slot] = (unsigned short)d[q];
+  }
+  __syncthreads();
+  const unsigned total = s.start[ndest - 1] + s.hist[ndest - 1];
+  for (unsigned k = threadIdx.x; k < total; k += blockDim.x) {
+    const unsigned dd = s.dest[k];
+    const unsigned g = s.gcur[dd] + (k - s.start[dd]);
+    out_keys[g] = s.keys[k];
+    out_rows[g] = s.rows[k];
+  }
+  __syncthreads();
+}
+
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
 __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
@@ -388,73 +453,84 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
                                                              const unsigned* __restrict__ super_base,
                                                              unsigned long long* __restrict__ keys1,
                                                              unsigned* __restrict__ rows1, unsigned* err) {
-  __shared__ unsigned cur[kMaxSupers];
+  extern __shared__ unsigned long long stage_raw[];
+  StageLds& s = *reinterpret_cast<StageLds*>(stage_raw);
   const int64_t t = blockIdx.x;
-  for (int B = threadIdx.x; B < kMaxSupers; B += blockDim.x) cur[B] = 0;
+  const int nd = (int)kp.n_supers;
+  for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] = 0;
   __syncthreads();
   // rows of super-bucket B in tiles < t = sum over its buckets of (offset[b][t] - offset[b][0])
   for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) {
     const unsigned v = counts[b * kp.n_tiles + t] - counts[b * kp.n_tiles];
-    if (v) atomicAdd(cur + (b >> kp.super_bits), v);
+    if (v) atomicAdd(s.gcur + (b >> kp.super_bits), v);
   }
   __syncthreads();
-  for (int B = threadIdx.x; B < kp.n_supers; B += blockDim.x) cur[B] += super_base[B];
+  for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += super_base[B];
   __syncthreads();
   const int64_t t0 = t * kTileRows;
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
   const int mid_bits = kp.bucket_bits + kp.super_bits;
   const uint64_t mid_mask = (1ULL << mid_bits) - 1;
   const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
-  for (int64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += (int64_t)blockDim.x * kUnroll) {
-    int64_t u[kUnroll], k[kUnroll];
+  for (int64_t c0 = t0; c0 < t1; c0 += kStageRows) {
+    int64_t u[kStageItems], k[kStageItems];
 #pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      const int64_t i = i0 + (int64_t)q * blockDim.x;
+    for (int q = 0; q < kStageItems; ++q) {
+      const int64_t i = c0 + threadIdx.x + (int64_t)q * blockDim.x;
       u[q] = i < t1 ? pid[i] : -1;
       k[q] = i < t1 ? pk[i] : 0;
     }
+    int d[kStageItems];
+    unsigned long long x[kStageItems];
+    unsigned r[kStageItems];
 #pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      if (u[q] < 0 || u[q] >= kp.U) continue;  // flagged by k_part_hist, not counted
+    for (int q = 0; q < kStageItems; ++q) {
+      r[q] = (unsigned)(c0 + threadIdx.x + (int64_t)q * blockDim.x);
+      if (u[q] < 0 || u[q] >= kp.U) {  // flagged by k_part_hist, not counted
+        d[q] = -1;
+        x[q] = 0;
+        continue;
+      }
+      d[q] = (int)(u[q] >> mid_bits);
       const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
-      uint64_t x;
       if (k[q] < 0 || k[q] >= kp.P) {
         atomicOr(err, 1u);
-        x = dead | midv;
+        x[q] = dead | midv;
       } else if (allowed != nullptr && allowed[k[q]] == 0) {
-        x = dead | midv;
+        x[q] = dead | midv;
       } else {
-        x = pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift);
+        x[q] = pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift);
       }
-      const unsigned pos = atomicAdd(cur + (u[q] >> mid_bits), 1u);
-      keys1[pos] = x;
-      rows1[pos] = (unsigned)(i0 + (int64_t)q * blockDim.x);
     }
+    unsigned rank[kStageItems];
+    stage_count(s, nd, d, rank);
+    stage_write(s, nd, d, rank, x, r, keys1, rows1);
+    for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += s.hist[B];
+    __syncthreads();
   }
 }
 
-// Level 2: chunks of one super-bucket -> its 2^super_bits bucket regions.
+// Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
 __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
                                                              unsigned* __restrict__ cursor,
                                                              const unsigned long long* __restrict__ keys1,
                                                              const unsigned* __restrict__ rows1,
                                                              unsigned long long* __restrict__ keys2,
                                                              unsigned* __restrict__ rows2) {
-  extern __shared__ unsigned lds[];
+  extern __shared__ unsigned long long stage_raw[];
+  StageLds& s = *reinterpret_cast<StageLds*>(stage_raw);
   __shared__ int64_t s_first, s_r0, s_r1;
   const int nsub = 1 << kp.super_bits;
-  unsigned* hist = lds;          // [nsub]
-  unsigned* cur = lds + nsub;    // [nsub]
   if (threadIdx.x == 0) {
     // locate this workgroup's (super-bucket, chunk)
-    int64_t g = blockIdx.x, B = 0, first = -1, r0 = 0, r1 = 0;
-    for (; B < kp.n_supers; ++B) {
+    int64_t g = blockIdx.x, first = -1, r0 = 0, r1 = 0;
+    for (int64_t B = 0; B < kp.n_supers; ++B) {
       const int64_t lo = super_base[B], hi = super_base[B + 1];
-      const int64_t nch = (hi - lo + kL2Chunk - 1) / kL2Chunk;
+      const int64_t nch = (hi - lo + kStageRows - 1) / kStageRows;
       if (g < nch) {
         first = B << kp.super_bits;
-        r0 = lo + g * kL2Chunk;
-        r1 = r0 + kL2Chunk < hi ? r0 + kL2Chunk : hi;
+        r0 = lo + g * kStageRows;
+        r1 = r0 + kStageRows < hi ? r0 + kStageRows : hi;
         break;
       }
       g -= nch;
@@ -463,39 +539,29 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
     s_r0 = r0;
     s_r1 = r1;
   }
-  for (int s = threadIdx.x; s < nsub; s += blockDim.x) hist[s] = 0;
   __syncthreads();
   if (s_first < 0) return;  // grid is an upper bound on the chunk count
   const int64_t r0 = s_r0, r1 = s_r1;
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
-  unsigned long long x[kL2Items];
-  unsigned r[kL2Items];
+  unsigned long long x[kStageItems];
+  unsigned r[kStageItems];
+  int d[kStageItems];
 #pragma unroll
-  for (int q = 0; q < kL2Items; ++q) {
+  for (int q = 0; q < kStageItems; ++q) {
     const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
     x[q] = i < r1 ? keys1[i] : 0;
     r[q] = i < r1 ? rows1[i] : 0;
+    d[q] = i < r1 ? (int)((x[q] >> sub_shift) & sub_mask) : -1;
   }
-#pragma unroll
-  for (int q = 0; q < kL2Items; ++q) {
-    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
-    if (i < r1) atomicAdd(hist + ((x[q] >> sub_shift) & sub_mask), 1u);
-  }
-  __syncthreads();
-  for (int s = threadIdx.x; s < nsub; s += blockDim.x) {
-    const int64_t b = s_first + s;
-    cur[s] = (hist[s] && b < kp.n_buckets) ? atomicAdd(cursor + b, hist[s]) : 0;
+  unsigned rank[kStageItems];
+  stage_count(s, nsub, d, rank);
+  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+    const int64_t b = s_first + t;
+    s.gcur[t] = (s.hist[t] && b < kp.n_buckets) ? atomicAdd(cursor + b, s.hist[t]) : 0;
   }
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kL2Items; ++q) {
-    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
-    if (i >= r1) continue;
-    const unsigned pos = atomicAdd(cur + ((x[q] >> sub_shift) & sub_mask), 1u);
-    keys2[pos] = x[q];
-    rows2[pos] = r[q];
-  }
+  stage_write(s, nsub, d, rank, x, r, keys2, rows2);
 }
 
 template <int VALUE_KIND, bool KEEP_ALL_ROWS>
@@ -873,16 +939,19 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_scatter_l1", st);
-  hipLaunchKernelGGL(k_scatter_l1, dim3((unsigned)p.n_tiles), dim3(kPartThreads), 0, st, kp, privacy_id,
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(StageLds)));
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l2, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(StageLds)));
+  hipLaunchKernelGGL(k_scatter_l1, dim3((unsigned)p.n_tiles), dim3(kPartThreads), sizeof(StageLds), st, kp, privacy_id,
                      partition_key, pk_allowed, counts, super_base, (unsigned long long*)(ws + w.keys1),
                      (unsigned*)(ws + w.rows1), err);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
-    const int64_t n_l2 = (cfg->n_rows + kL2Chunk - 1) / kL2Chunk + p.n_supers;
-    const size_t l2_lds = (size_t)2 * ((size_t)1 << p.super_bits) * 4;
+    const int64_t n_l2 = (cfg->n_rows + kStageRows - 1) / kStageRows + p.n_supers;
     PDP_PROF_BEGIN("k_scatter_l2", st);
-    hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)n_l2), dim3(kPartThreads), l2_lds, st, kp, super_base, cursor,
+    hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)n_l2), dim3(kPartThreads), sizeof(StageLds), st, kp, super_base, cursor,
                        (const unsigned long long*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
                        (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
     PDP_PROF_END(st);

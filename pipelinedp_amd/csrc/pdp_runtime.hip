@@ -50,7 +50,7 @@ void profiler_begin(const char* name, hipStream_t stream) {
   std::lock_guard<std::mutex> lock(g_prof_mu);
   g_open_start = take_event();
   g_open_name = name;
-  if (g_open_start) hipEventRecord(g_open_start, stream);
+  if (g_open_start) (void)hipEventRecord(g_open_start, stream);
 }
 
 void profiler_end(hipStream_t stream) {
@@ -58,7 +58,7 @@ void profiler_end(hipStream_t stream) {
   if (!g_open_start) return;
   hipEvent_t stop = take_event();
   if (!stop) return;
-  hipEventRecord(stop, stream);
+  (void)hipEventRecord(stop, stream);
   g_prof.push_back(ProfRecord{g_open_name, g_open_start, stop});
   g_open_start = nullptr;
 }
