@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=ROWS_PER_GPU, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=600_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
     return ap.parse_args()
 
 

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 1
+#define PDP_ABI_VERSION 2
 
 /* error codes */
 #define PDP_OK 0
@@ -64,7 +64,7 @@ typedef struct pdp_bound_config {
   int64_t row_offset;    /* global index of this shard's row 0 (row priorities) */
   uint64_t seed;         /* sampling seed */
   int32_t algorithm;     /* PDP_ALGO_*; every algorithm keeps the same samples */
-  int32_t reserved;
+  int32_t merge;         /* PDP_MERGE_*: how BUCKETED merges kept pairs per partition */
 } pdp_bound_config;
 
 #define PDP_MAX_L0 256
@@ -75,6 +75,12 @@ typedef struct pdp_bound_config {
 #define PDP_ALGO_GLOBAL_SKETCH 1 /* per-pid / per-pair sketches in HBM, device atomics */
 #define PDP_ALGO_BUCKETED 2      /* rows partitioned by pid bucket, sketches in LDS */
 
+/* per-partition merge of the kept pairs (BUCKETED; identical sums up to fp
+ * summation order) */
+#define PDP_MERGE_AUTO 0
+#define PDP_MERGE_ATOMIC 1 /* one device atomic per kept pair and field */
+#define PDP_MERGE_RANGES 2 /* pair records grouped by partition range, LDS reduction */
+
 typedef struct pdp_bound_plan_info {
   int32_t algorithm;   /* resolved PDP_ALGO_* */
   int32_t bucket_bits; /* privacy ids per bucket = 2^bucket_bits */
@@ -83,6 +89,9 @@ typedef struct pdp_bound_plan_info {
   int64_t n_buckets;
   int64_t n_tiles;
   int64_t lds_bytes;   /* per bucket workgroup */
+  int32_t merge;       /* resolved PDP_MERGE_* (0 for GLOBAL_SKETCH) */
+  int32_t n_ranges;    /* PDP_MERGE_RANGES: partition ranges of 2^11 keys */
+  int64_t range_group; /* PDP_MERGE_RANGES: buckets per range-reduce workgroup */
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */
@@ -127,7 +136,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
  * (BUCKETED: the per-bucket sampling itself runs here, in LDS).
  * `acc` arrays are ADDED to (zero them first, or chain shards). */
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value,
-                          const void* workspace, uint64_t workspace_bytes,
+                          void* workspace, uint64_t workspace_bytes,
                           const pdp_partition_accumulators* acc, void* stream);
 
 /* partition selection strategies */

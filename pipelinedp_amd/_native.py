@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
                         "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 1
+ABI_VERSION = 2
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 SELECT_ALL_NONEMPTY = 0
@@ -28,6 +28,7 @@ SELECT_PUBLIC = 4
 OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID = 1, 2, 3, 4, 5, 6
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
 ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED = 0, 1, 2
+MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
 MAX_L0 = 256
 MAX_LINF = 256
 MAX_OPS = 8
@@ -71,7 +72,7 @@ class BoundConfig(ctypes.Structure):
         ("row_offset", ctypes.c_int64),
         ("seed", ctypes.c_uint64),
         ("algorithm", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("merge", ctypes.c_int32),
     ]
 
 
@@ -84,6 +85,9 @@ class BoundPlanInfo(ctypes.Structure):
         ("n_buckets", ctypes.c_int64),
         ("n_tiles", ctypes.c_int64),
         ("lds_bytes", ctypes.c_int64),
+        ("merge", ctypes.c_int32),
+        ("n_ranges", ctypes.c_int32),
+        ("range_group", ctypes.c_int64),
     ]
 
 

@@ -42,6 +42,12 @@ constexpr int64_t kLdsBudget = 128 * 1024;
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
 constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
+constexpr int kRangeBits = 11;                // partitions per merge range = 2048
+constexpr int kRangeParts = 1 << kRangeBits;
+constexpr int kMaxRanges = 1024;              // per-bucket range histogram <= one block scan
+constexpr int kRangeThreads = 256;
+constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
+constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
@@ -55,6 +61,10 @@ struct Plan {
   int64_t n_supers;
   int64_t n_tiles;
   int64_t lds_bytes;
+  int merge;            // PDP_MERGE_* (bucketed)
+  int n_ranges;         // PDP_MERGE_RANGES: ceil(P / 2^kRangeBits)
+  int64_t range_group;  // buckets per range-reduce workgroup
+  int64_t n_groups;
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -89,6 +99,27 @@ Plan make_plan(const pdp_bound_config* c) {
   p.n_tiles = (c->n_rows + kTileRows - 1) / kTileRows;
   if (p.n_tiles < 1) p.n_tiles = 1;
   p.lds_bytes = ((int64_t)1 << p.bucket_bits) * per_pid;
+  p.n_ranges = (int)((c->n_partitions + kRangeParts - 1) >> kRangeBits);
+  const bool ranges_ok = p.n_ranges <= kMaxRanges;
+  if (p.algorithm != PDP_ALGO_BUCKETED) {
+    p.merge = 0;
+  } else if (c->merge == PDP_MERGE_AUTO) {
+    p.merge = ranges_ok ? PDP_MERGE_RANGES : PDP_MERGE_ATOMIC;
+  } else {
+    p.merge = c->merge;
+    if (p.merge == PDP_MERGE_RANGES && !ranges_ok) p.algorithm = -1;  // infeasible
+  }
+  if (p.merge == PDP_MERGE_RANGES) {
+    // per-bucket range histogram + cursors + block-scan scratch after the sketches
+    p.lds_bytes += (2 * (int64_t)p.n_ranges + kBucketThreads / 64 + 1) * 4;
+    int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
+    p.range_group = g < 1 ? 1 : (g > kRangeThreads ? kRangeThreads : g);
+    p.n_groups = (p.n_buckets + p.range_group - 1) / p.range_group;
+  } else {
+    p.n_ranges = 0;
+    p.range_group = 0;
+    p.n_groups = 0;
+  }
   return p;
 }
 
@@ -99,6 +130,8 @@ struct Ws {
   uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
   // bucketed path
   uint64_t counts_tm, counts, chunk_sums, cursor, super_base, keys1, rows1, keys2, rows2;
+  // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
+  uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t total;
 };
 
@@ -136,6 +169,14 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.keys2 = w.keys1;
       w.rows2 = w.rows1;
     }
+    if (p.merge == PDP_MERGE_RANGES) {
+      const uint64_t recs = (uint64_t)p.n_buckets * ((uint64_t)c->l0 << p.bucket_bits);
+      w.runs = off; off = align256(off + (uint64_t)p.n_buckets * (p.n_ranges + 1) * 4);
+      w.rec_key = off; off = align256(off + recs * 8);
+      if (c->flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION)) { w.rec_f0 = off; off = align256(off + recs * 8); }
+      if (c->flags & PDP_ACC_NSUM) { w.rec_f1 = off; off = align256(off + recs * 8); }
+      if (c->flags & PDP_ACC_NSUM2) { w.rec_f2 = off; off = align256(off + recs * 8); }
+    }
   }
   w.total = off;
   return w;
@@ -159,8 +200,10 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "PDP_SUM_INT requires int64 values");
   if (c->algorithm < PDP_ALGO_AUTO || c->algorithm > PDP_ALGO_BUCKETED)
     return set_error(PDP_E_INVALID, "bad algorithm");
+  if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
+    return set_error(PDP_E_INVALID, "bad merge");
   if (make_plan(c).algorithm < 0)
-    return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm infeasible for this l0/linf/P");
+    return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge infeasible for this l0/linf/P");
   return PDP_OK;
 }
 
@@ -170,6 +213,8 @@ struct KP {  // kernel parameters
   int l0, linf;
   int pk_bits, bucket_bits, super_bits, rand_shift;
   int64_t n_buckets, n_supers, n_tiles;
+  int n_ranges;
+  int64_t range_group;
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
   ClipParams clip;
@@ -189,6 +234,8 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.n_buckets = p.n_buckets;
   k.n_supers = p.n_supers;
   k.n_tiles = p.n_tiles;
+  k.n_ranges = p.n_ranges;
+  k.range_group = p.range_group;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -564,12 +611,47 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
   stage_write(s, nsub, d, rank, x, r, keys2, rows2);
 }
 
-template <int VALUE_KIND, bool KEEP_ALL_ROWS>
+// exclusive block-wide scan of one u32 per thread; wsum = LDS[blockDim/64]
+__device__ __forceinline__ unsigned block_excl_scan(unsigned x, unsigned* wsum, unsigned* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned inc = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    const unsigned v = lane < nw ? wsum[lane] : 0;
+    unsigned vi = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned y = __shfl_up(vi, off, 64);
+      if (lane >= off) vi += y;
+    }
+    if (lane < nw) wsum[lane] = vi - v;
+    if (lane == nw - 1) wsum[nw] = vi;
+  }
+  __syncthreads();
+  *total = wsum[nw];
+  return wsum[w] + inc - x;
+}
+
+struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
+  unsigned* runs;                // [n_buckets][n_ranges + 1] run starts within the bucket block
+  unsigned long long* key;       // (partition << 32) | count
+  double* f0;                    // sum (int64 bits with PDP_SUM_INT)
+  double* f1;                    // normalized sum
+  double* f2;                    // normalized sum of squares
+};
+
+template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES>
 __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const unsigned long long* __restrict__ keys,
                                                                  const unsigned* __restrict__ rowidx,
                                                                  const unsigned* __restrict__ offsets,
                                                                  const void* __restrict__ value,
-                                                                 pdp_partition_accumulators acc) {
+                                                                 pdp_partition_accumulators acc, PairRecords rec) {
   extern __shared__ unsigned long long smem[];
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
@@ -578,10 +660,15 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
   unsigned long long* rsk = sk + n_slots;             // bounded: [S*l0*linf] row sketches
   double* tot = (double*)(sk + n_slots);              // keep-all: [3][S*l0] pair sums
   unsigned* cnt = KEEP_ALL_ROWS ? (unsigned*)(tot + 3 * n_slots) : (unsigned*)(rsk + n_slots * kp.linf);
+  unsigned* rh = cnt + n_slots;          // RANGES: [n_ranges] kept pairs per partition range
+  unsigned* rcur = rh + kp.n_ranges;     //         [n_ranges] write cursors
+  unsigned* wsum = rcur + kp.n_ranges;   //         block-scan scratch
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
   }
+  if (RANGES)
+    for (int t = threadIdx.x; t < kp.n_ranges; t += blockDim.x) rh[t] = 0;
   if (!KEEP_ALL_ROWS) {
     for (int64_t t = threadIdx.x; t < n_slots * kp.linf; t += blockDim.x) rsk[t] = kEmpty;
   } else {
@@ -660,7 +747,27 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
     }
   }
   __syncthreads();
-  // B3: merge every kept pair into its partition
+  unsigned* run = nullptr;
+  if (RANGES) {
+    // B3a: kept pairs per partition range -> this bucket's run starts
+    for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
+      const uint64_t x = sk[slot];
+      if (x == kEmpty || cnt[slot] == 0) continue;
+      atomicAdd(rh + ((x & kp.pk_mask) >> kRangeBits), 1u);
+    }
+    __syncthreads();
+    const unsigned h = threadIdx.x < kp.n_ranges ? rh[threadIdx.x] : 0u;  // n_ranges <= blockDim
+    unsigned total;
+    const unsigned ex = block_excl_scan(h, wsum, &total);
+    run = rec.runs + b * (kp.n_ranges + 1);
+    if (threadIdx.x < kp.n_ranges) {
+      run[threadIdx.x] = ex;
+      rcur[threadIdx.x] = ex;
+    }
+    if (threadIdx.x == 0) run[kp.n_ranges] = total;
+    __syncthreads();
+  }
+  // B3: merge every kept pair into its partition (RANGES: emit a pair record)
   for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
     const uint64_t x = sk[slot];
     if (x == kEmpty) continue;
@@ -676,7 +783,93 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
     } else {
       ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
     }
-    add_pair_to_partition(acc, p, ps, flags);
+    if (RANGES) {
+      const int64_t i = b * n_slots + atomicAdd(rcur + (p >> kRangeBits), 1u);
+      rec.key[i] = ((unsigned long long)p << 32) | (unsigned long long)(uint32_t)ps.count;
+      if (flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION))
+        rec.f0[i] = (flags & PDP_SUM_INT) ? __longlong_as_double(ps.isum) : ps.fsum;
+      if (flags & PDP_ACC_NSUM) rec.f1[i] = ps.nsum;
+      if (flags & PDP_ACC_NSUM2) rec.f2[i] = ps.nsum2;
+    } else {
+      add_pair_to_partition(acc, p, ps, flags);
+    }
+  }
+}
+
+// PDP_MERGE_RANGES: workgroup (range r, bucket group g) sums the records of
+// partitions [r*2^11, (r+1)*2^11) emitted by buckets [g*G, (g+1)*G) in LDS,
+// then adds the partial sums with coalesced device atomics.
+__global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec,
+                                                               pdp_partition_accumulators acc) {
+  extern __shared__ unsigned long long smem[];
+  double* s0 = (double*)smem;               // [kRangeParts] sum
+  double* s1 = s0 + kRangeParts;            // normalized sum
+  double* s2 = s1 + kRangeParts;            // normalized sum of squares
+  unsigned long long* start = (unsigned long long*)(s2 + kRangeParts);  // [kRangeThreads]
+  unsigned* pc = (unsigned*)(start + kRangeThreads);  // [kRangeParts] kept pairs
+  unsigned* cn = pc + kRangeParts;                    // [kRangeParts] row count
+  unsigned* pre = cn + kRangeParts;                   // [kRangeThreads] run prefix
+  unsigned* wsum = pre + kRangeThreads;               // block-scan scratch
+  const int flags = kp.clip.flags;
+  const bool f0 = flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION), f1 = flags & PDP_ACC_NSUM,
+             f2 = flags & PDP_ACC_NSUM2, sum_int = flags & PDP_SUM_INT;
+  for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
+    pc[t] = 0;
+    cn[t] = 0;
+    s0[t] = 0.0;
+    s1[t] = 0.0;
+    s2[t] = 0.0;
+  }
+  const int r = blockIdx.x;
+  const int64_t p0 = (int64_t)r << kRangeBits;
+  const int64_t b0 = (int64_t)blockIdx.y * kp.range_group;
+  int64_t nb = kp.n_buckets - b0;
+  if (nb > kp.range_group) nb = kp.range_group;
+  const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
+  unsigned len = 0;
+  if (threadIdx.x < nb) {
+    const unsigned* run = rec.runs + (b0 + threadIdx.x) * (kp.n_ranges + 1) + r;
+    const unsigned s = run[0];
+    len = run[1] - s;
+    start[threadIdx.x] = (unsigned long long)((b0 + threadIdx.x) * n_slots + s);
+  }
+  unsigned total;
+  const unsigned ex = block_excl_scan(len, wsum, &total);
+  pre[threadIdx.x] = ex;
+  __syncthreads();
+  for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
+    int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint64_t idx = start[lo] + (i - pre[lo]);
+    const unsigned long long key = rec.key[idx];
+    const int lp = (int)((key >> 32) - (uint64_t)p0);
+    atomicAdd(pc + lp, 1u);
+    atomicAdd(cn + lp, (unsigned)key);
+    if (f0) {
+      if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(rec.f0[idx]));
+      else atomicAdd(s0 + lp, rec.f0[idx]);
+    }
+    if (f1) atomicAdd(s1 + lp, rec.f1[idx]);
+    if (f2) atomicAdd(s2 + lp, rec.f2[idx]);
+  }
+  __syncthreads();
+  int64_t plen = kp.P - p0;
+  if (plen > kRangeParts) plen = kRangeParts;
+  for (int t = threadIdx.x; t < plen; t += blockDim.x) {
+    if (pc[t] == 0) continue;
+    const int64_t p = p0 + t;
+    atomicAdd((unsigned long long*)(acc.privacy_id_count + p), (unsigned long long)pc[t]);
+    if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)cn[t]);
+    if (f0) {
+      if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(s0[t]));
+      else unsafeAtomicAdd((double*)acc.sum + p, s0[t]);
+    }
+    if (f1) unsafeAtomicAdd(acc.normalized_sum + p, s1[t]);
+    if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, s2[t]);
   }
 }
 
@@ -782,17 +975,35 @@ int launch_global_reduce(const KP& kp, hipStream_t st, const void* value, const 
 }
 
 template <int VK, bool KA>
-int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, const char* ws, const Ws& w, const void* value,
+int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w, const void* value,
                   const pdp_partition_accumulators& acc) {
-  auto kern = k_bucket_bound<VK, KA>;
+  const bool ranges = p.merge == PDP_MERGE_RANGES;
+  auto kern = ranges ? k_bucket_bound<VK, KA, true> : k_bucket_bound<VK, KA, false>;
+  PairRecords rec{};
+  if (ranges) {
+    rec.runs = (unsigned*)(ws + w.runs);
+    rec.key = (unsigned long long*)(ws + w.rec_key);
+    rec.f0 = w.rec_f0 ? (double*)(ws + w.rec_f0) : nullptr;
+    rec.f1 = w.rec_f1 ? (double*)(ws + w.rec_f1) : nullptr;
+    rec.f2 = w.rec_f2 ? (double*)(ws + w.rec_f2) : nullptr;
+  }
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)p.lds_bytes));
   PDP_PROF_BEGIN("k_bucket_bound", st);
   hipLaunchKernelGGL(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), (unsigned)p.lds_bytes, st, kp,
                      (const unsigned long long*)(ws + w.keys2), (const unsigned*)(ws + w.rows2),
-                     (const unsigned*)(ws + w.counts), value, acc);
+                     (const unsigned*)(ws + w.counts), value, acc, rec);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  if (ranges) {
+    PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_range_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kRangeLds));
+    PDP_PROF_BEGIN("k_range_reduce", st);
+    hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_ranges, (unsigned)p.n_groups), dim3(kRangeThreads),
+                       kRangeLds, st, kp, rec, acc);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
   return PDP_OK;
 }
 
@@ -853,6 +1064,9 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->n_buckets = p.algorithm == PDP_ALGO_BUCKETED ? p.n_buckets : 0;
   info->n_tiles = p.n_tiles;
   info->lds_bytes = p.algorithm == PDP_ALGO_BUCKETED ? p.lds_bytes : 0;
+  info->merge = p.merge;
+  info->n_ranges = p.n_ranges;
+  info->range_group = p.range_group;
   return PDP_OK;
 }
 
@@ -960,7 +1174,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   return PDP_OK;
 }
 
-int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, const void* workspace,
+int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,
                           uint64_t workspace_bytes, const pdp_partition_accumulators* acc, void* stream) {
   Plan p;
   Ws w;
@@ -981,7 +1195,7 @@ int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, const 
     return set_error(PDP_E_INVALID, "value column is NULL");
   hipStream_t st = (hipStream_t)stream;
   const KP kp = make_kp(cfg, p);
-  const char* ws = (const char*)workspace;
+  char* ws = (char*)workspace;
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH)
     return dispatch<GlobalReduce>(cfg->value_kind, cfg->linf == 0, kp, st, value, ws, w, *acc);
   if (cfg->n_rows == 0) return PDP_OK;

@@ -36,7 +36,7 @@ def _rand_shift(n, U, P, spec, algorithm=0):
     return X.bound_plan(n, U, P, spec, algorithm).rand_shift
 
 
-def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0):
+def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0, merge=0):
     import torch
     from pipelinedp_amd import executor as X
     tp = torch.as_tensor(pid).to(device)
@@ -44,7 +44,7 @@ def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0,
     tv = None if val is None else torch.as_tensor(val).to(device)
     ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
     acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
-                             allowed=ta, row_offset=row_offset, algorithm=algorithm)
+                             allowed=ta, row_offset=row_offset, algorithm=algorithm, merge=merge)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
@@ -94,7 +94,8 @@ CASES = [
 ]
 
 
-ALGOS = {"global": 1, "bucketed": 2}
+# name -> (PDP_ALGO_*, PDP_MERGE_*)
+ALGOS = {"global": (1, 0), "bucketed-atomic": (2, 1), "bucketed-ranges": (2, 2)}
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
@@ -111,11 +112,12 @@ def test_bound_and_reduce_matches_oracle(device, case, skew, algo):
                           middle=mid, min_sum=pp[0] if pp else 0.0, max_sum=pp[1] if pp else 0.0)
     seed = 0x1234_5678_9ABC_DEF0 + l0
     try:
-        X.bound_plan(n, U, P, spec, ALGOS[algo])
+        X.bound_plan(n, U, P, spec, *ALGOS[algo])
     except N.NativeLibraryError:
         pytest.skip(f"{algo} infeasible for l0={l0}, linf={linf}")
-    got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo])
-    want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo])
+    got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo][0],
+                   merge=ALGOS[algo][1])
+    want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo][0])
     _compare(got, want, _abs_scale(pid, pk, val, P, lo, hi, mid))
 
 
@@ -148,8 +150,9 @@ def test_public_filter(device, algo):
     allowed = np.zeros(P, dtype=bool)
     allowed[::3] = True
     spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0, max_value=10)
-    got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo])
-    want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo])
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo][0],
+                   merge=ALGOS[algo][1])
+    want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo][0])
     _compare(got, want, _abs_scale(pid, pk, val, P, 0, 10, 0))
     assert np.all(got["count"][~allowed] == 0)
 
@@ -164,7 +167,7 @@ def test_out_of_range_keys_raise(device, algo, bad):
     spec = X.BoundingSpec(l0=1, linf=1, value_kind=O.VALUE_NONE, flags=0)
     with pytest.raises(ValueError):
         X.bound_and_reduce(pid, pk, None, n_privacy_ids=3, n_partitions=2, bounding=spec, seed=1,
-                           algorithm=ALGOS[algo])
+                           algorithm=ALGOS[algo][0], merge=ALGOS[algo][1])
 
 
 @pytest.mark.parametrize("heavy", [False, True])
@@ -183,12 +186,28 @@ def test_algorithms_agree_at_scale(device, heavy):
     spec = X.BoundingSpec(l0=4, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM,
                           min_value=0.0, max_value=10.0, middle=5.0)
     a = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=1)
-    b = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=2)
-    np.testing.assert_array_equal(a["privacy_id_count"], b["privacy_id_count"])
-    np.testing.assert_array_equal(a["count"], b["count"])
     sc = _abs_scale(pid, pk, val, P, 0.0, 10.0, 5.0)
-    assert np.all(np.abs(a["sum"] - b["sum"]) <= FLOAT_RTOL * sc)
-    assert np.all(np.abs(a["normalized_sum"] - b["normalized_sum"]) <= FLOAT_RTOL * sc)
+    for merge in (1, 2):  # 30k partitions = 15 merge ranges
+        b = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=2, merge=merge)
+        np.testing.assert_array_equal(a["privacy_id_count"], b["privacy_id_count"])
+        np.testing.assert_array_equal(a["count"], b["count"])
+        assert np.all(np.abs(a["sum"] - b["sum"]) <= FLOAT_RTOL * sc)
+        assert np.all(np.abs(a["normalized_sum"] - b["normalized_sum"]) <= FLOAT_RTOL * sc)
+
+
+@pytest.mark.parametrize("P", [2047, 2048, 2049, 100_000, 2_000_000])
+def test_range_merge_matches_oracle_many_ranges(device, P):
+    """Range merge at range boundaries and up to the 1024-range limit (P = 2M)."""
+    from pipelinedp_amd import executor as X
+    n, U = 300_000, 20_000
+    pid, pk, val = _gen(P, n, U, P, O.VALUE_I64)
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_I64, flags=O.ACC_SUM | O.SUM_INT | O.ACC_NSUM,
+                          min_value=0, max_value=9, middle=4.5)
+    info = X.bound_plan(n, U, P, spec, 2, 2)
+    assert info.merge == 2 and info.n_ranges == (P + 2047) // 2048
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 21, algorithm=2, merge=2)
+    want = _oracle(pid, pk, val, U, P, spec, 21, algorithm=2)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0, 9, 4.5))
 
 
 def test_empty_input(device):
