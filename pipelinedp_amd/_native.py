@@ -13,8 +13,8 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
-                        "libpipelinedp_amd.so")
+LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
 ABI_VERSION = 2

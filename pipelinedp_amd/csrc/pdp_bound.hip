@@ -38,7 +38,7 @@ constexpr int kPartThreads = 512;
 constexpr int64_t kTileRows = 65536;
 constexpr int kUnroll = 8;
 constexpr int kBucketThreads = 1024;
-constexpr int64_t kLdsBudget = 128 * 1024;
+constexpr int64_t kLdsBudget = 124 * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
 constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
@@ -48,6 +48,7 @@ constexpr int kMaxRanges = 1024;              // per-bucket range histogram <= o
 constexpr int kRangeThreads = 256;
 constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
+constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
@@ -70,7 +71,7 @@ struct Plan {
 int64_t per_pid_lds(const pdp_bound_config* c) {
   const int64_t l0 = c->l0;
   const int64_t pair = 4 + (c->linf > 0 ? 8 * (int64_t)c->linf : 24);
-  return l0 * 8 + l0 * pair;
+  return l0 * 8 + l0 * pair;  // pair sketch + per-pair state
 }
 
 Plan make_plan(const pdp_bound_config* c) {
@@ -112,6 +113,11 @@ Plan make_plan(const pdp_bound_config* c) {
   if (p.merge == PDP_MERGE_RANGES) {
     // per-bucket range histogram + cursors + block-scan scratch after the sketches
     p.lds_bytes += (2 * (int64_t)p.n_ranges + kBucketThreads / 64 + 1) * 4;
+  }
+  if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave
+    p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
+  }
+  if (p.merge == PDP_MERGE_RANGES) {
     int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
     p.range_group = g < 1 ? 1 : (g > kRangeThreads ? kRangeThreads : g);
     p.n_groups = (p.n_buckets + p.range_group - 1) / p.range_group;
@@ -215,6 +221,7 @@ struct KP {  // kernel parameters
   int64_t n_buckets, n_supers, n_tiles;
   int n_ranges;
   int64_t range_group;
+  int keys_vec;  // privacy_id / partition_key columns are 16-byte aligned
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
   ClipParams clip;
@@ -236,6 +243,7 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.n_tiles = p.n_tiles;
   k.n_ranges = p.n_ranges;
   k.range_group = p.range_group;
+  k.keys_vec = 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -374,12 +382,19 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
   __syncthreads();
   const int64_t t0 = (int64_t)blockIdx.x * kTileRows;
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
-  for (int64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += (int64_t)blockDim.x * kUnroll) {
-    int64_t u[kUnroll];
+  for (int64_t i0 = t0 + 2 * (int64_t)threadIdx.x; i0 < t1; i0 += (int64_t)blockDim.x * kUnroll) {
+    int64_t u[kUnroll];  // two consecutive rows per 16-byte load
 #pragma unroll
-    for (int k = 0; k < kUnroll; ++k) {
+    for (int k = 0; k < kUnroll; k += 2) {
       const int64_t i = i0 + (int64_t)k * blockDim.x;
-      u[k] = i < t1 ? pid[i] : INT64_MIN;
+      if (kp.keys_vec && i + 1 < t1) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+        u[k] = a.x;
+        u[k + 1] = a.y;
+      } else {
+        u[k] = i < t1 ? pid[i] : INT64_MIN;
+        u[k + 1] = i + 1 < t1 ? pid[i + 1] : INT64_MIN;
+      }
     }
 #pragma unroll
     for (int k = 0; k < kUnroll; ++k) {
@@ -520,19 +535,31 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
   const uint64_t mid_mask = (1ULL << mid_bits) - 1;
   const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
   for (int64_t c0 = t0; c0 < t1; c0 += kStageRows) {
+    // two consecutive rows per 16-byte load (tiles and chunks start even)
     int64_t u[kStageItems], k[kStageItems];
 #pragma unroll
-    for (int q = 0; q < kStageItems; ++q) {
-      const int64_t i = c0 + threadIdx.x + (int64_t)q * blockDim.x;
-      u[q] = i < t1 ? pid[i] : -1;
-      k[q] = i < t1 ? pk[i] : 0;
+    for (int q = 0; q < kStageItems; q += 2) {
+      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+      if (kp.keys_vec && i + 1 < t1) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+        const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
+        u[q] = a.x;
+        u[q + 1] = a.y;
+        k[q] = c.x;
+        k[q + 1] = c.y;
+      } else {
+        u[q] = i < t1 ? pid[i] : -1;
+        k[q] = i < t1 ? pk[i] : 0;
+        u[q + 1] = -1;
+        k[q + 1] = 0;
+      }
     }
     int d[kStageItems];
     unsigned long long x[kStageItems];
     unsigned r[kStageItems];
 #pragma unroll
     for (int q = 0; q < kStageItems; ++q) {
-      r[q] = (unsigned)(c0 + threadIdx.x + (int64_t)q * blockDim.x);
+      r[q] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
       if (u[q] < 0 || u[q] >= kp.U) {  // flagged by k_part_hist, not counted
         d[q] = -1;
         x[q] = 0;
@@ -566,40 +593,65 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
                                                              unsigned* __restrict__ rows2) {
   extern __shared__ unsigned long long stage_raw[];
   StageLds& s = *reinterpret_cast<StageLds*>(stage_raw);
-  __shared__ int64_t s_first, s_r0, s_r1;
+  __shared__ int64_t s_first, s_base, s_r0, s_r1;
   const int nsub = 1 << kp.super_bits;
-  if (threadIdx.x == 0) {
-    // locate this workgroup's (super-bucket, chunk)
-    int64_t g = blockIdx.x, first = -1, r0 = 0, r1 = 0;
-    for (int64_t B = 0; B < kp.n_supers; ++B) {
-      const int64_t lo = super_base[B], hi = super_base[B + 1];
-      const int64_t nch = (hi - lo + kStageRows - 1) / kStageRows;
-      if (g < nch) {
-        first = B << kp.super_bits;
-        r0 = lo + g * kStageRows;
-        r1 = r0 + kStageRows < hi ? r0 + kStageRows : hi;
-        break;
-      }
-      g -= nch;
+  if (threadIdx.x < 64) {
+    // locate this workgroup's (super-bucket, chunk): chunks of a super-bucket
+    // are 4096-row windows aligned at its first even row (n_supers <= 64)
+    const int lane = threadIdx.x;
+    int64_t lo = 0, hi = 0, nch = 0;
+    if (lane < kp.n_supers) {
+      lo = super_base[lane];
+      hi = super_base[lane + 1];
+      nch = hi > lo ? (hi - (lo & ~(int64_t)1) + kStageRows - 1) / kStageRows : 0;
     }
-    s_first = first;
-    s_r0 = r0;
-    s_r1 = r1;
+    int64_t inc = nch;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += y;
+    }
+    const int64_t g = blockIdx.x;
+    const bool mine = g >= inc - nch && g < inc;
+    const unsigned long long hit = __ballot(mine);
+    if (lane == 0 && hit == 0) s_first = -1;  // grid is an upper bound on the chunk count
+    if (mine) {
+      const int64_t base = (lo & ~(int64_t)1) + (g - (inc - nch)) * kStageRows;
+      s_first = (int64_t)lane << kp.super_bits;
+      s_base = base;
+      s_r0 = base > lo ? base : lo;
+      s_r1 = base + kStageRows < hi ? base + kStageRows : hi;
+    }
   }
   __syncthreads();
-  if (s_first < 0) return;  // grid is an upper bound on the chunk count
-  const int64_t r0 = s_r0, r1 = s_r1;
+  if (s_first < 0) return;
+  const int64_t base = s_base, r0 = s_r0, r1 = s_r1;
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
   unsigned long long x[kStageItems];
   unsigned r[kStageItems];
   int d[kStageItems];
 #pragma unroll
-  for (int q = 0; q < kStageItems; ++q) {
-    const int64_t i = r0 + threadIdx.x + (int64_t)q * blockDim.x;
-    x[q] = i < r1 ? keys1[i] : 0;
-    r[q] = i < r1 ? rows1[i] : 0;
-    d[q] = i < r1 ? (int)((x[q] >> sub_shift) & sub_mask) : -1;
+  for (int q = 0; q < kStageItems; q += 2) {  // two rows per 16-byte key load
+    const int64_t i = base + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+    if (i >= r0 && i + 1 < r1) {
+      const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
+      const uint2 c = *reinterpret_cast<const uint2*>(rows1 + i);
+      x[q] = a.x;
+      x[q + 1] = a.y;
+      r[q] = c.x;
+      r[q + 1] = c.y;
+      d[q] = (int)((x[q] >> sub_shift) & sub_mask);
+      d[q + 1] = (int)((x[q + 1] >> sub_shift) & sub_mask);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const bool ok = i + e >= r0 && i + e < r1;
+        x[q + e] = ok ? keys1[i + e] : 0;
+        r[q + e] = ok ? rows1[i + e] : 0;
+        d[q + e] = ok ? (int)((x[q + e] >> sub_shift) & sub_mask) : -1;
+      }
+    }
   }
   unsigned rank[kStageItems];
   stage_count(s, nsub, d, rank);
@@ -638,6 +690,105 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned x, unsigned* wsum, 
   return wsum[w] + inc - x;
 }
 
+// Per-wave LDS queue of candidate rows (capacity 2 waves' worth): rows that
+// pass a cheap per-row test are compacted here and the expensive per-candidate
+// work then runs on full wavefronts instead of on the few lanes of each
+// load that happen to hold a candidate.
+struct WaveQueue {
+  unsigned long long* key;  // [kQueueCap]
+  unsigned* row;            // [kQueueCap]
+};
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Streams the rows [begin, end) of one bucket: pred(key) selects candidates,
+// work(key, row) handles each candidate on compacted wavefronts.  Two rows per
+// lane per 16-byte key load (8-byte row load when ROWS), KU loads in flight per
+// lane; every wave runs the same trip count so the queue stays convergent.
+template <int KU, bool ROWS, typename P, typename W>
+__device__ __forceinline__ void stream_bucket(const unsigned long long* __restrict__ keys,
+                                              const unsigned* __restrict__ rows, int64_t begin, int64_t end,
+                                              WaveQueue q, P&& pred, W&& work) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  int n = 0;  // wave-uniform queue length
+  auto push = [&](uint64_t x, uint32_t r) {
+    const bool p = pred(x);
+    const unsigned long long m = __ballot(p);
+    if (p) {
+      const int pos = n + __popcll(m & below);
+      q.key[pos] = x;
+      if (ROWS) q.row[pos] = r;
+    }
+    n += __popcll(m);
+    if (n >= 64) {
+      wave_lds_fence();
+      const uint64_t wx = q.key[lane];
+      const uint32_t wr = ROWS ? q.row[lane] : 0u;
+      n -= 64;
+      uint64_t mx = 0;
+      uint32_t mr = 0;
+      if (lane < n) {
+        mx = q.key[64 + lane];
+        if (ROWS) mr = q.row[64 + lane];
+      }
+      wave_lds_fence();
+      if (lane < n) {
+        q.key[lane] = mx;
+        if (ROWS) q.row[lane] = mr;
+      }
+      work(wx, wr);
+    }
+  };
+  int64_t a0 = (begin + 1) & ~(int64_t)1;
+  if (a0 > end) a0 = end;
+  const int64_t a1 = a0 + ((end - a0) & ~(int64_t)1);
+  {  // odd head / tail row (lanes 0 / 1 of wave 0)
+    uint64_t x = kEmpty;
+    uint32_t r = 0;
+    if (threadIdx.x == 0 && begin < a0) {
+      x = keys[begin];
+      if (ROWS) r = rows[begin];
+    }
+    if (threadIdx.x == 1 && a1 < end) {
+      x = keys[a1];
+      if (ROWS) r = rows[a1];
+    }
+    push(x, r);
+  }
+  const int64_t np = (a1 - a0) >> 1;
+  const ulonglong2* kv = reinterpret_cast<const ulonglong2*>(keys + a0);
+  const uint2* rv = reinterpret_cast<const uint2*>(rows + a0);
+  for (int64_t g0 = 0; g0 < np; g0 += (int64_t)blockDim.x * KU) {
+    ulonglong2 kx[KU];
+    uint2 rx[KU];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      const int64_t g = g0 + (int64_t)u * blockDim.x + threadIdx.x;
+      if (g < np) {
+        kx[u] = kv[g];
+        if (ROWS) rx[u] = rv[g];
+      } else {
+        kx[u] = make_ulonglong2(kEmpty, kEmpty);
+        if (ROWS) rx[u] = make_uint2(0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      push((uint64_t)kx[u].x, ROWS ? rx[u].x : 0u);
+      push((uint64_t)kx[u].y, ROWS ? rx[u].y : 0u);
+    }
+  }
+  if (n > 0) {  // partial wave
+    wave_lds_fence();
+    if (lane < n) work((uint64_t)q.key[lane], ROWS ? q.row[lane] : 0u);
+  }
+}
+
 struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
   unsigned* runs;                // [n_buckets][n_ranges + 1] run starts within the bucket block
   unsigned long long* key;       // (partition << 32) | count
@@ -663,6 +814,11 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
   unsigned* rh = cnt + n_slots;          // RANGES: [n_ranges] kept pairs per partition range
   unsigned* rcur = rh + kp.n_ranges;     //         [n_ranges] write cursors
   unsigned* wsum = rcur + kp.n_ranges;   //         block-scan scratch
+  unsigned* tail = RANGES ? wsum + kBucketThreads / 64 + 1 : rh;
+  unsigned long long* qbase = (unsigned long long*)(((uintptr_t)tail + 7) & ~(uintptr_t)7);
+  const int wave = threadIdx.x >> 6;
+  const WaveQueue wq{qbase + wave * kQueueCap,
+                     (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
@@ -679,48 +835,35 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
   const int64_t begin = offsets[b * kp.n_tiles];
   const int64_t end = offsets[(b + 1) * kp.n_tiles];  // offsets has n_buckets*n_tiles+1 entries
   const uint64_t bmask = (uint64_t)S - 1;
-  const int64_t step = (int64_t)blockDim.x * kUnroll;
-  // B1: bottom-l0 distinct pair keys per privacy id
-  for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += step) {
-    uint64_t xs[kUnroll];
-#pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      const int64_t i = i0 + (int64_t)q * blockDim.x;
-      xs[q] = i < end ? keys[i] : kEmpty;
-    }
-#pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      const uint64_t x = xs[q];
-      if (dead_key(x, kp.rand_shift)) continue;
-      unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
-      if (x >= s[l0 - 1]) continue;
-      sketch_insert(s, l0, x);
-    }
-  }
+  // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys below
+  // their sketch's current maximum
+  stream_bucket<kUnroll, false>(
+      keys, rowidx, begin, end, wq,
+      [&](uint64_t x) {
+        return !dead_key(x, kp.rand_shift) && x < sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
+      },
+      [&](uint64_t x, uint32_t) {
+        unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
+        if (x < s[l0 - 1]) sketch_insert(s, l0, x);
+      });
   __syncthreads();
+#ifdef PDP_ABL_B1_ONLY
+  return;
+#endif
   // B2: rows of kept pairs
   const int flags = kp.clip.flags;
-  for (int64_t i0 = begin + threadIdx.x; i0 < end; i0 += step) {
-    uint64_t xs[kUnroll];
-    uint32_t rs_[kUnroll];
-#pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      const int64_t i = i0 + (int64_t)q * blockDim.x;
-      xs[q] = i < end ? keys[i] : kEmpty;
-      rs_[q] = i < end ? rowidx[i] : 0;
-    }
-#pragma unroll
-    for (int q = 0; q < kUnroll; ++q) {
-      const uint64_t x = xs[q];
-      if (dead_key(x, kp.rand_shift)) continue;
+  stream_bucket<kUnroll / 2, true>(
+      keys, rowidx, begin, end, wq,
+      [&](uint64_t x) {
+        return !dead_key(x, kp.rand_shift) && x <= sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
+      },
+      [&](uint64_t x, uint32_t r) {
       const int64_t pl = (x >> kp.pk_bits) & bmask;
       const unsigned long long* s = sk + pl * l0;
-      if (x > s[l0 - 1]) continue;
       const int j = sketch_find(s, l0, x);
-      if (j < 0) continue;
+      if (j < 0) return;
       const int64_t slot = pl * l0 + j;
       atomicAdd(cnt + slot, 1u);
-      const uint32_t r = rs_[q];
       if (!KEEP_ALL_ROWS) {
         const uint64_t y = row_key(kp.row_seed, kp.row_offset + r, r);
         unsigned long long* rs = rsk + slot * kp.linf;
@@ -744,9 +887,11 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
           if (flags & PDP_ACC_NSUM2) atomicAdd(tot + 2 * n_slots + slot, c * c);
         }
       }
-    }
-  }
+  });
   __syncthreads();
+#ifdef PDP_ABL_NO_B3
+  return;
+#endif
   unsigned* run = nullptr;
   if (RANGES) {
     // B3a: kept pairs per partition range -> this bucket's run starts
@@ -1091,7 +1236,8 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     return set_error(PDP_E_INVALID, "value column is NULL");
   hipStream_t st = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  const KP kp = make_kp(cfg, p);
+  KP kp = make_kp(cfg, p);
+  kp.keys_vec = ((((uintptr_t)privacy_id) | ((uintptr_t)partition_key)) & 15) == 0;
   unsigned* err = (unsigned*)(ws + w.err);
   PDP_HIP_CHECK(hipMemsetAsync(err, 0, 16, st));
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH) {
@@ -1163,7 +1309,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
-    const int64_t n_l2 = (cfg->n_rows + kStageRows - 1) / kStageRows + p.n_supers;
+    const int64_t n_l2 = (cfg->n_rows + p.n_supers) / kStageRows + p.n_supers + 1;
     PDP_PROF_BEGIN("k_scatter_l2", st);
     hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)n_l2), dim3(kPartThreads), sizeof(StageLds), st, kp, super_base, cursor,
                        (const unsigned long long*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),

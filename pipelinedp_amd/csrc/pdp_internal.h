@@ -134,6 +134,10 @@ __device__ __forceinline__ double draw_noise(int kind, double scale, U4 r) {
 // inserted (kEmpty = free).  Lock-free: each atomicMin keeps the array
 // sorted and hands the displaced key to the next slot; meeting an equal key
 // means it is already present.  Works on LDS and global pointers.
+// Sorted bottom-k sketches of u64 keys (kEmpty = free), lock-free under
+// concurrent inserts: the array stays sorted and every position only ever
+// decreases.  Insert x (no-op if present or not among the k smallest) by an
+// atomicMin cascade carrying the displaced key one position up.
 __device__ __forceinline__ void sketch_insert(unsigned long long* s, int k, uint64_t x) {
   for (int j = 0; j < k; ++j) {
     const uint64_t old = atomicMin(s + j, (unsigned long long)x);
@@ -145,6 +149,7 @@ __device__ __forceinline__ void sketch_insert(unsigned long long* s, int k, uint
   }
 }
 
+// Position of x in a quiescent sorted sketch, or -1.
 __device__ __forceinline__ int sketch_find(const unsigned long long* s, int k, uint64_t x) {
   int lo = 0, hi = k;
   while (lo < hi) {

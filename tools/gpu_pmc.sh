@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES"; do
+for C in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY"; do
   N=$(echo $C | tr ' ' '_')
   timeout -s KILL 120 rocprofv3 --pmc $C -d $OUT/$N -o run --output-format csv -- python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/$N.log 2>&1 || { echo "PMC pass $C failed"; exit 1; }
 done
