@@ -50,19 +50,35 @@ def pk_bits(n_partitions):
     return b
 
 
+def fmix32(h):
+    """MurmurHash3 32-bit finaliser on uint32 arrays (wrapping arithmetic)."""
+    h = np.asarray(h, dtype=np.uint32)
+    with np.errstate(over="ignore"):
+        h = h ^ (h >> np.uint32(16))
+        h = h * np.uint32(0x85EBCA6B)
+        h = h ^ (h >> np.uint32(13))
+        h = h * np.uint32(0xC2B2AE35)
+        return h ^ (h >> np.uint32(16))
+
+
 def pair_hash(seed, pid, pk):
+    """32 random bits per (pid, pk) pair (kernels: pdp_internal.h pair_hash)."""
     pid = np.asarray(pid).astype(np.uint64)
     pk = np.asarray(pk).astype(np.uint64)
+    s0, s1 = np.uint32(int(seed) & 0xFFFFFFFF), np.uint32((int(seed) >> 32) & 0xFFFFFFFF)
+    lo = (pid & _U64(0xFFFFFFFF)).astype(np.uint32)
+    hi = (pid >> _U64(32)).astype(np.uint32)
+    pk32 = (pk & _U64(0xFFFFFFFF)).astype(np.uint32)
     with np.errstate(over="ignore"):
-        h = mix64(_U64(seed) ^ (pid * _U64(0x9E3779B97F4A7C15)))
-        return mix64(h + pk * _U64(0xC2B2AE3D27D4EB4F) + _U64(0x165667B19E3779F9))
+        h = fmix32((lo * np.uint32(0x9E3779B1)) ^ (hi * np.uint32(0x7FEB352D)) ^ s0)
+        return fmix32(h ^ (pk32 * np.uint32(0xC2B2AE3D) + s1))
 
 
 def pair_priority(seed, pid, pk, rand_shift):
-    """Sampling key of (pid, pk): random bits [rand_shift, 64), then pk (the
-    kernels may also place the bucket-local pid in between; that does not change
-    the order among one pid's pairs)."""
-    h = pair_hash(seed, pid, pk)
+    """Sampling key of (pid, pk): the pair hash in bits [32, 64), cleared below
+    rand_shift, then pk (the kernels may also place the bucket-local pid in
+    between; that does not change the order among one pid's pairs)."""
+    h = pair_hash(seed, pid, pk).astype(np.uint64) << _U64(32)
     low = _U64((1 << rand_shift) - 1)
     x = (h & ~low) | np.asarray(pk).astype(np.uint64)
     bad = (x | low) == EMPTY

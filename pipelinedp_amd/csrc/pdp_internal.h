@@ -52,19 +52,32 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__host__ __device__ __forceinline__ uint64_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {
-  uint64_t h = mix64(seed ^ ((uint64_t)pid * 0x9E3779B97F4A7C15ULL));
-  return mix64(h + (uint64_t)pk * 0xC2B2AE3D27D4EB4FULL + 0x165667B19E3779F9ULL);
+// MurmurHash3 32-bit finaliser
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6BU;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35U;
+  return h ^ (h >> 16);
 }
 
-// Sampling key of the pair (pid, pk): bits [rand_shift, 64) are random, bits
-// [pk_bits, rand_shift) carry `mid` (the bucket-local pid, or 0) and bits
-// [0, pk_bits) the partition.  Within one privacy id keys order by (random
-// part, partition) whatever `mid` is, so every execution path samples the
-// same pairs.  Never equal to kEmpty.
+// 32 random bits of the pair (pid, pk) under `seed`: a per-pid hash, then the
+// partition folded in as an odd-multiplier progression (32-bit multiplies only;
+// ties between one pid's pairs, p ~ 2^-32, break by partition).
+__host__ __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {
+  const uint32_t h = fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^
+                            (uint32_t)seed);
+  return fmix32(h ^ ((uint32_t)pk * 0xC2B2AE3DU + (uint32_t)(seed >> 32)));
+}
+
+// Sampling key of the pair (pid, pk): bits [rand_shift, 64) are random (the
+// pair hash from bit 32 up, zero below), bits [pk_bits, rand_shift) carry
+// `mid` (the bucket-local pid, or 0) and bits [0, pk_bits) the partition.
+// Within one privacy id keys order by (random part, partition) whatever `mid`
+// is, so every execution path samples the same pairs.  Never equal to kEmpty.
 __host__ __device__ __forceinline__ uint64_t pair_key(uint64_t seed, int64_t pid, int64_t pk,
                                                       uint64_t mid_bits, int rand_shift) {
-  const uint64_t h = pair_hash(seed, pid, pk);
+  const uint64_t h = (uint64_t)pair_hash(seed, pid, pk) << 32;
   const uint64_t low = (1ULL << rand_shift) - 1;
   uint64_t x = (h & ~low) | mid_bits | (uint64_t)pk;
   if ((x | low) == kEmpty) x &= ~(1ULL << rand_shift);
