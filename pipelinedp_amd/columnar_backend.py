@@ -32,6 +32,7 @@ from pipelinedp_amd import _native as N
 from pipelinedp_amd import columnar as C
 from pipelinedp_amd import combiners as pdc
 from pipelinedp_amd import dp_computations as dpc
+from pipelinedp_amd import parallel
 from pipelinedp_amd import partition_selection as ps
 from pipelinedp_amd import pipeline_backend
 
@@ -462,6 +463,10 @@ class AggregateRun:
         public_codes = None
         if public is not None:
             pk_enc, public_codes = C.extend_with_keys(pk_enc, public)
+        if parallel.world_info()[0] > 1:  # one partition dictionary for all ranks
+            pk_enc = parallel.global_partition_keys(pk_enc)
+            if public is not None and pk_enc.decode is not None:
+                public_codes = np.asarray([pk_enc.encode[k] for k in public], dtype=np.int64)
         pid_t = torch.as_tensor(pid_enc.codes).to(device=device, dtype=torch.int64).contiguous()
         pk_t = torch.as_tensor(pk_enc.codes).to(device=device, dtype=torch.int64).contiguous()
         val_t = None
@@ -470,6 +475,8 @@ class AggregateRun:
             if val_raw is None:
                 raise ValueError("the value extractor must return a value column for SUM/MEAN/VARIANCE")
             val_t = _value_tensor(val_raw, device)
+            if parallel.all_ranks_any(val_t.dtype != torch.int64):  # one value kind on every rank
+                val_t = val_t.to(torch.float64)
             value_kind = N.VALUE_I64 if val_t.dtype == torch.int64 else N.VALUE_F64
         return pid_t, pk_t, val_t, value_kind, pid_enc, pk_enc, public_codes
 
@@ -492,7 +499,9 @@ class AggregateRun:
         import torch
         pid_t, pk_t, val_t, vk, pid_enc, pk_enc, public_codes = self._columns()
         spec = self._bounding_spec(vk)
-        P = pk_enc.n
+        world, _ = parallel.world_info()
+        P, _ = parallel.partition_slices(pk_enc.n, world)  # padded to a multiple of the ranks
+        row_offset = parallel.row_offset(pid_t.numel())
         allowed = None
         if public_codes is not None:
             mask = np.zeros(P, dtype=np.uint8)
@@ -503,7 +512,7 @@ class AggregateRun:
             acc = X.new_accumulators(P, spec, pid_t.device)
         else:
             acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=pid_enc.n, n_partitions=P,
-                                     bounding=spec, seed=seed_bound, allowed=allowed)
+                                     bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset)
             self.backend.last_plan_info = X.bound_plan(pid_t.numel(), pid_enc.n, P, spec)
         return acc, spec, pk_enc, allowed
 
@@ -530,15 +539,25 @@ class AggregateRun:
         return strat.device_spec(int(max_rows))
 
     def run(self) -> List:
+        """Single GPU: every partition.  Under torch.distributed (one rank per
+        GPU, each holding its own rows; privacy ids must not span ranks): the
+        partitions this rank owns after the accumulator exchange — the union
+        over ranks is the result."""
         import torch
         from pipelinedp_amd import executor as X
         acc, spec, pk_enc, allowed = self._bound()
+        acc, first = parallel.exchange_accumulators(acc)  # identity on one rank
         sel = self._selection()
-        public_mask = allowed if (self.plan.public_keys is not None or self.plan.public_padding is not None) else None
+        public = self.plan.public_keys is not None or self.plan.public_padding is not None
+        public_mask = None
+        if public:
+            n_mine = acc["privacy_id_count"].shape[0]
+            public_mask = allowed[first:first + n_mine].contiguous()
         _, seed_select, seed_noise = self._seeds
         index, out, n_kept = X.select_and_noise(acc, selection=sel, ops=self.prog.ops,
                                                 n_cols=len(self.prog.fields), seed_select=seed_select,
-                                                seed_noise=seed_noise, public_mask=public_mask)
+                                                seed_noise=seed_noise, public_mask=public_mask,
+                                                partition_offset=first)
         idx = index.cpu().numpy()
         vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((len(self.prog.fields), 0))
         nt = pdc._get_or_create_named_tuple("MetricsTuple", tuple(self.prog.fields))
@@ -550,7 +569,7 @@ class AggregateRun:
             row = tuple(col[j] for col in columns)
             if drop_nan_pid and row[pid_col] != row[pid_col]:
                 continue
-            result.append((pk_enc.key_of(p), nt(*row)))
+            result.append((pk_enc.key_of(first + p), nt(*row)))
         return result
 
     def raw_accumulators(self):
@@ -586,7 +605,7 @@ class AggregateRun:
     @property
     def _seeds(self):
         if not hasattr(self, "_seed_cache"):
-            self._seed_cache = self.backend._seeds()
+            self._seed_cache = parallel.broadcast_seeds(self.backend._seeds())
         return self._seed_cache
 
 

@@ -326,7 +326,8 @@ class GaussianMechanism(AdditiveMechanism):
 
 def create_additive_mechanism(mechanism_spec, sensitivities: Sensitivities) -> AdditiveMechanism:
     """dp_computations.py:621-646."""
-    noise_kind = mechanism_spec.mechanism_type.to_noise_kind()
+    # by value, so the reference's own MechanismSpec / enums work too
+    noise_kind = agg.NoiseKind(getattr(mechanism_spec.mechanism_type.to_noise_kind(), "value", None))
     if noise_kind == agg.NoiseKind.LAPLACE:
         if sensitivities.l1 is None:
             raise ValueError("L1 or (L0 and Linf) sensitivities must be set for Laplace mechanism.")

@@ -70,3 +70,72 @@ def shard_by_privacy_id(privacy_ids, world: int, rank: int):
     import hashlib
     return np.fromiter((int(hashlib.blake2b(repr(p).encode(), digest_size=8).hexdigest(), 16) % world == rank
                         for p in pid), dtype=bool, count=len(pid))
+
+
+def row_offset(n_rows: int, group=None) -> int:
+    """Global index of this rank's first row (ranks' shards concatenated in
+    rank order); row sampling priorities are keyed by it."""
+    world, rank = world_info(group)
+    if world == 1:
+        return 0
+    import torch.distributed as dist
+    counts = [None] * world
+    dist.all_gather_object(counts, int(n_rows), group=group)
+    return int(sum(counts[:rank]))
+
+
+def global_partition_keys(enc, group=None):
+    """Makes a rank-local partition-key encoding (columnar.EncodedKeys) global:
+    every rank gets the same dense code for the same key, so the per-partition
+    accumulators of all ranks line up for the exchange.  Dense integer keys
+    keep the identity encoding (range = max over ranks); other keys get one
+    dictionary in rank-then-first-appearance order."""
+    world, rank = world_info(group)
+    if world == 1:
+        return enc
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from pipelinedp_amd.columnar import EncodedKeys
+    mine = ("ids", int(enc.n)) if enc.decode is None else ("dict", list(enc.decode))
+    objs = [None] * world
+    dist.all_gather_object(objs, mine, group=group)
+    if all(kind == "ids" for kind, _ in objs):
+        return EncodedKeys(enc.codes, max(n for _, n in objs), None)
+    mapping, decode = {}, []
+    for kind, payload in objs:
+        keys = range(payload) if kind == "ids" else payload
+        for k in keys:
+            if k not in mapping:
+                mapping[k] = len(decode)
+                decode.append(k)
+    local = range(enc.n) if enc.decode is None else enc.decode
+    remap = np.fromiter((mapping[k] for k in local), dtype=np.int64, count=len(local))
+    codes = enc.codes
+    if type(codes).__module__.startswith("torch"):
+        codes = torch.as_tensor(remap, device=codes.device)[codes]
+    else:
+        codes = remap[np.asarray(codes)] if len(remap) else np.asarray(codes, dtype=np.int64)
+    return EncodedKeys(codes, len(decode), np.asarray(decode, dtype=object), mapping)
+
+
+def broadcast_seeds(seeds, group=None):
+    """Rank 0's seeds on every rank (selection and noise are keyed by global
+    partition index, so all ranks must draw from the same streams)."""
+    world, _ = world_info(group)
+    if world == 1:
+        return tuple(seeds)
+    import torch.distributed as dist
+    obj = [tuple(seeds)]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return tuple(obj[0])
+
+
+def all_ranks_any(flag: bool, group=None) -> bool:
+    world, _ = world_info(group)
+    if world == 1:
+        return bool(flag)
+    import torch.distributed as dist
+    objs = [None] * world
+    dist.all_gather_object(objs, bool(flag), group=group)
+    return any(objs)

@@ -1,0 +1,171 @@
+"""The C-ABI boundary (include/pipelinedp_amd.h) on the CPU: the library loads,
+exports every declared entry point, its ctypes mirror has the C struct layout
+and constants, and the host-only entry points (plan, workspace sizing, argument
+validation, error reporting) behave.  No device work is launched."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from pipelinedp_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pipelinedp_amd.h")
+
+STRUCTS = {
+    "pdp_bound_config": N.BoundConfig,
+    "pdp_bound_plan_info": N.BoundPlanInfo,
+    "pdp_partition_accumulators": N.PartitionAccumulators,
+    "pdp_select_config": N.SelectConfig,
+    "pdp_metric_op": N.MetricOp,
+}
+
+
+def _header_text():
+    with open(HEADER) as f:
+        src = f.read()
+    return re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+
+
+def declared_functions():
+    return sorted(set(re.findall(r"\b(pdp_[a-z0-9_]+)\s*\(", _header_text())))
+
+
+def declared_constants():
+    return {m.group(1): int(m.group(2), 0) for m in
+            re.finditer(r"#define\s+PDP_([A-Z0-9_]+)\s+\(?(-?(?:0x[0-9A-Fa-f]+|\d+))\)?", _header_text())}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(N.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    return N.lib()
+
+
+def test_every_declared_function_is_exported(lib):
+    fns = declared_functions()
+    assert len(fns) >= 13
+    assert set(fns) == set(N.EXPORTED_SYMBOLS)
+    for name in fns:
+        assert hasattr(lib, name), name
+
+
+def test_constants_match_header():
+    consts = declared_constants()
+    skip = {"ABI_VERSION"}
+    checked = 0
+    for name, value in consts.items():
+        if name.startswith("E_") or name == "OK" or name in skip:
+            continue
+        py = name[:-4] if name.endswith("_MAX") else name
+        if hasattr(N, py):
+            assert getattr(N, py) == value, name
+            checked += 1
+    assert checked >= 25
+    assert consts["ABI_VERSION"] == N.ABI_VERSION
+
+
+def test_struct_layouts_match_c(tmp_path):
+    """sizeof / offsetof of every ABI struct, compiled by gcc from the header,
+    equal the ctypes mirror's."""
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "pipelinedp_amd.h"', "int main(void) {"]
+    for cname, cls in STRUCTS.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for field, _ in cls._fields_:
+            lines.append(f'  printf("{cname} {field} %zu\\n", offsetof({cname}, {field}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    got = {}
+    for line in out.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, cls in STRUCTS.items():
+        assert got[(cname, "size")] == ctypes.sizeof(cls), cname
+        for field, _ in cls._fields_:
+            assert got[(cname, field)] == getattr(cls, field).offset, (cname, field)
+
+
+def _cfg(**kw):
+    c = N.BoundConfig()
+    c.n_rows, c.n_privacy_ids, c.n_partitions = 100_000_000, 1_000_000, 100_000
+    c.l0, c.linf, c.value_kind, c.flags = 8, 2, N.VALUE_F64, N.ACC_NSUM
+    c.min_value, c.max_value, c.middle = 0.0, 10.0, 5.0
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def test_abi_version_and_plan(lib):
+    assert lib.pdp_abi_version() == N.ABI_VERSION
+    info = N.BoundPlanInfo()
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg()), ctypes.byref(info)) == 0
+    assert info.algorithm == N.ALGO_BUCKETED and info.merge == N.MERGE_RANGES
+    assert info.pk_bits == 17 and info.n_ranges == 49
+    assert info.n_buckets << info.bucket_bits >= 1_000_000
+    assert info.lds_bytes <= 160 * 1024
+    assert 64 - info.rand_shift >= 24
+    # forced global path and forced atomic merge resolve as asked
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(algorithm=N.ALGO_GLOBAL_SKETCH)), ctypes.byref(info)) == 0
+    assert info.algorithm == N.ALGO_GLOBAL_SKETCH and info.n_buckets == 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(merge=N.MERGE_ATOMIC)), ctypes.byref(info)) == 0
+    assert info.merge == N.MERGE_ATOMIC
+    # > 1024 partition ranges: AUTO falls back to atomics, forced RANGES is unsupported
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(n_partitions=10_000_000)), ctypes.byref(info)) == 0
+    assert info.merge == N.MERGE_ATOMIC
+    rc = lib.pdp_bound_plan(ctypes.byref(_cfg(n_partitions=10_000_000, merge=N.MERGE_RANGES)),
+                            ctypes.byref(info))
+    assert rc == -4 and b"infeasible" in lib.pdp_last_error()
+
+
+def test_workspace_bytes(lib):
+    small, big = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(n_rows=1000)), ctypes.byref(small)) == 0
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg()), ctypes.byref(big)) == 0
+    assert 0 < small.value < big.value
+    # bucketed: two levels of (8 B key + 4 B row) + pair records (8 B key + 8 B nsum per kept slot)
+    assert big.value >= 100_000_000 * 24 + 1_000_000 * 8 * 16
+    assert big.value < 100_000_000 * 26 + 1_000_000 * 8 * 16 + (64 << 20)
+    cb = ctypes.c_uint64(0)
+    assert lib.pdp_compact_workspace_bytes(1 << 20, ctypes.byref(cb)) == 0 and cb.value > 0
+
+
+@pytest.mark.parametrize("field,value,code,msg", [
+    ("l0", 0, -4, b"l0"), ("l0", 257, -4, b"l0"), ("linf", -1, -4, b"linf"),
+    ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
+    ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
+    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"),
+])
+def test_invalid_configs_are_rejected(lib, field, value, code, msg):
+    info = N.BoundPlanInfo()
+    rc = lib.pdp_bound_plan(ctypes.byref(_cfg(**{field: value})), ctypes.byref(info))
+    assert rc == code
+    assert msg in lib.pdp_last_error()
+
+
+def test_sum_int_needs_int_values(lib):
+    info = N.BoundPlanInfo()
+    rc = lib.pdp_bound_plan(ctypes.byref(_cfg(flags=N.ACC_SUM | N.SUM_INT)), ctypes.byref(info))
+    assert rc == -1 and b"PDP_SUM_INT" in lib.pdp_last_error()
+
+
+def test_null_arguments_are_rejected_before_device_work(lib):
+    cfg = _cfg(n_rows=10)
+    assert lib.pdp_bound_plan(ctypes.byref(cfg), None) == -1
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), None) == -1
+    assert lib.pdp_bound_plan(None, ctypes.byref(N.BoundPlanInfo())) == -1
+    # workspace too small: refused before any launch
+    rc = lib.pdp_bound_contributions(ctypes.byref(cfg), None, None, None, None, None, 0, None)
+    assert rc == -3
+    # key columns missing with a big enough (fake, never dereferenced) workspace pointer
+    need = ctypes.c_uint64(0)
+    lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(need))
+    rc = lib.pdp_bound_contributions(ctypes.byref(cfg), None, None, None, None, ctypes.c_void_p(256),
+                                     need.value, None)
+    assert rc == -1 and b"key columns" in lib.pdp_last_error()

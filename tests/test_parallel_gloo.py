@@ -1,0 +1,129 @@
+"""Multi-rank path on the CPU (gloo, world_size 2): rows sharded by privacy id,
+each rank bounds and reduces its own shard, one accumulator exchange.  The
+per-rank bounding is the CPU oracle here (the kernels' restatement), so this
+checks the sharding design: the exchanged slices equal the unsharded
+aggregation of the concatenated shards bit-exactly for counts."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import columnar as O
+from pipelinedp_amd import parallel
+
+U, P, N_PER_RANK, WORLD = 400, 37, 6000, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _shard(rank):
+    """Rank r's rows: the privacy ids shard_by_privacy_id assigns to it."""
+    rng = np.random.default_rng(100 + rank)
+    pid = rng.integers(0, U, 4 * N_PER_RANK)
+    mine = parallel.shard_by_privacy_id(pid, WORLD, rank)
+    pid = pid[mine][:N_PER_RANK]
+    pk = rng.integers(0, P, pid.shape[0])
+    val = rng.normal(3.0, 2.0, pid.shape[0])
+    return pid, pk, val
+
+
+def _oracle(pid, pk, val, P_pad, row_offset):
+    return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P_pad, l0=3, linf=2,
+                              value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM, min_value=0.0,
+                              max_value=6.0, middle=3.0, seed=77, row_offset=row_offset,
+                              rand_shift=O.pk_bits(P_pad) + 8)
+
+
+def _worker(rank, port, results):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        P_pad, slice_len = parallel.partition_slices(P, WORLD)
+        shards = [_shard(r) for r in range(WORLD)]
+        offsets = np.cumsum([0] + [s[0].shape[0] for s in shards])
+        pid, pk, val = shards[rank]
+        acc = _oracle(pid, pk, val, P_pad, int(offsets[rank]))
+        tens = {k: (None if v is None else torch.as_tensor(v)) for k, v in acc.items()}
+        mine, first = parallel.exchange_accumulators(tens)
+        assert first == rank * slice_len
+        full = _oracle(np.concatenate([s[0] for s in shards]), np.concatenate([s[1] for s in shards]),
+                       np.concatenate([s[2] for s in shards]), P_pad, 0)
+        sl = slice(first, first + slice_len)
+        np.testing.assert_array_equal(mine["privacy_id_count"].numpy(), full["privacy_id_count"][sl])
+        np.testing.assert_array_equal(mine["count"].numpy(), full["count"][sl])
+        np.testing.assert_allclose(mine["sum"].numpy(), full["sum"][sl], rtol=1e-12, atol=1e-9)
+        np.testing.assert_allclose(mine["normalized_sum"].numpy(), full["normalized_sum"][sl],
+                                   rtol=1e-12, atol=1e-9)
+        results[rank] = "ok"
+    except Exception as e:  # reported to the parent
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_matches_unsharded_aggregation():
+    import torch.multiprocessing as mp
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_worker, args=(_free_port(), results), nprocs=WORLD, join=True)
+    assert dict(results) == {0: "ok", 1: "ok"}
+
+
+def test_partition_slices_and_validation():
+    import torch
+    assert parallel.partition_slices(100_000, 8) == (100_000, 12_500)
+    assert parallel.partition_slices(37, 2) == (38, 19)
+    assert parallel.partition_slices(5, 1) == (5, 5)
+    acc = {"privacy_id_count": torch.zeros(5, dtype=torch.int64)}
+    assert parallel.exchange_accumulators(acc) == (acc, 0)  # not initialised: one rank
+
+
+def test_shard_by_privacy_id_partitions_rows():
+    pid = np.arange(10_000)
+    masks = [parallel.shard_by_privacy_id(pid, 4, r) for r in range(4)]
+    assert np.all(sum(m.astype(int) for m in masks) == 1)
+    assert all(abs(m.sum() - 2500) < 300 for m in masks)
+    keys = np.array(["a", "b", "c", "d"] * 10, dtype=object)
+    m0 = parallel.shard_by_privacy_id(keys, 2, 0)
+    m1 = parallel.shard_by_privacy_id(keys, 2, 1)
+    assert np.all(m0 ^ m1)
+
+
+def _dict_worker(rank, port, results):
+    import torch.distributed as dist
+    from pipelinedp_amd import columnar as C
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        # string partition keys, overlapping between ranks, in different orders
+        keys = [["b", "a", "c", "a"], ["d", "c", "b"]][rank]
+        enc = parallel.global_partition_keys(C.encode_keys(np.asarray(keys, dtype=object)))
+        assert list(enc.decode) == ["b", "a", "c", "d"]
+        assert [enc.key_of(c) for c in enc.codes] == keys
+        # dense integer keys keep identity codes, range = max over ranks
+        ids = parallel.global_partition_keys(C.encode_keys(np.arange(3 + 4 * rank)))
+        assert ids.decode is None and ids.n == 7
+        assert parallel.row_offset(10 + rank) == (0 if rank == 0 else 10)
+        seeds = parallel.broadcast_seeds((rank + 1, rank + 2, rank + 3))
+        assert seeds == (1, 2, 3)
+        assert parallel.all_ranks_any(rank == 1) is True
+        results[rank] = "ok"
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_global_partition_dictionary_and_offsets():
+    import torch.multiprocessing as mp
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_dict_worker, args=(_free_port(), results), nprocs=WORLD, join=True)
+    assert dict(results) == {0: "ok", 1: "ok"}
