@@ -1,0 +1,220 @@
+"""End-to-end GPU tests through the drop-in API: DPEngine.aggregate on
+ColumnarBackend (HIP kernels via the C ABI).
+
+* pre-noise accumulators equal the reference's golden accumulators
+  (tests/golden, made by running the reference's DPEngine on LocalBackend);
+* noise added to exactly-known aggregates follows the calibrated Laplace /
+  Gaussian distributions (KS, p > 1e-4, the reference's own gate in
+  dp_computations_test.py:472-545);
+* private partition selection keeps partitions at the truncated-geometric
+  rate pi(n) (binomial bound per n);
+* two ranks (gloo, sharing the one GPU) give the single-process result.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import pipelinedp_amd as pdp
+from pipelinedp_amd import _native as N
+from pipelinedp_amd import columnar_backend as CB
+from pipelinedp_amd import dp_computations as dpc
+from tests import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _ext():
+    return pdp.DataExtractors(privacy_id_extractor=pdp.ColumnExtractor("pid"),
+                              partition_extractor=pdp.ColumnExtractor("pk"),
+                              value_extractor=pdp.ColumnExtractor("v"))
+
+
+def _aggregate(table, params, eps, delta, public=None, seed=None):
+    backend = CB.ColumnarBackend(seed=seed)
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=eps, total_delta=delta)
+    engine = pdp.DPEngine(acc, backend)
+    sink = engine.aggregate(table, params, _ext(), public_partitions=public)
+    acc.compute_budgets()
+    return sink, backend
+
+
+@pytest.mark.parametrize("fx", G.fixtures(), ids=G.fixture_ids())
+def test_backend_accumulators_match_reference_golden(device, fx):
+    case = fx["case"]
+    rows = [tuple(r) for r in fx["rows"]]
+    backend = CB.ColumnarBackend(device=device, seed=5)
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+    engine = pdp.DPEngine(acc, backend)
+    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                             value_extractor=lambda r: r[2])
+    sink = engine.aggregate(rows, G.aggregate_params(case), ext, public_partitions=case.get("public"))
+    acc.compute_budgets()
+    got = backend.accumulators(sink)
+    want = G.expected_map(fx)
+    assert set(G._key(k) for k in got) == set(want)
+    for k, v in got.items():
+        G.assert_acc_equal(want[G._key(k)], v, f"{fx['name']}[{k}]")
+
+
+def _public_table(P, per_partition, value):
+    """Partition p holds `per_partition` rows from distinct privacy ids, each
+    with value `value` (no sampling fires with L0 = Linf = 1)."""
+    pid = np.arange(P * per_partition, dtype=np.int64)
+    pk = pid // per_partition
+    v = np.full(pid.shape[0], value, dtype=np.float64)
+    return pdp.ColumnTable({"pid": pid, "pk": pk, "v": v})
+
+
+def _ks(samples, cdf):
+    from scipy.stats import kstest
+    return kstest(samples, cdf).pvalue
+
+
+def test_laplace_count_and_sum_noise_distribution(device):
+    from scipy.stats import laplace
+    P, c, v = 6000, 5, 3.0
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM], noise_kind=pdp.NoiseKind.LAPLACE,
+                                 max_partitions_contributed=1, max_contributions_per_partition=1,
+                                 min_value=0.0, max_value=4.0)
+    sink, _ = _aggregate(_public_table(P, c, v), params, eps=1.0, delta=0.0, public=list(range(P)), seed=11)
+    out = list(sink)
+    assert len(out) == P
+    count = np.array([m.count for _, m in out])
+    s = np.array([m.sum for _, m in out])
+    b_count = dpc.laplace_diversity(0.5, 1)       # eps split between COUNT and SUM
+    b_sum = dpc.laplace_diversity(0.5, 4.0)
+    assert _ks(count - c, laplace(scale=b_count).cdf) > 1e-4
+    assert _ks(s - c * v, laplace(scale=b_sum).cdf) > 1e-4
+    assert not np.any(count == np.round(count))  # continuous noise: non-integers (dp_computations_test.py:162)
+
+
+def test_gaussian_sum_noise_distribution(device):
+    from scipy.stats import norm
+    P, c, v = 6000, 3, 1.5
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.SUM], noise_kind=pdp.NoiseKind.GAUSSIAN,
+                                 max_partitions_contributed=1, max_contributions_per_partition=1,
+                                 min_value=-2.0, max_value=2.0)
+    sink, _ = _aggregate(_public_table(P, c, v), params, eps=1.0, delta=1e-5, public=list(range(P)), seed=12)
+    s = np.array([m.sum for _, m in sink])
+    sigma = dpc.compute_sigma(1.0, 1e-5, 2.0)
+    assert _ks(s - c * v, norm(scale=sigma).cdf) > 1e-4
+
+
+def test_truncated_geometric_keep_rates(device):
+    """Partitions with n = 1..7 privacy ids are kept with probability pi(n)."""
+    per_n, ns = 3000, list(range(1, 8))
+    pid, pk = [], []
+    nxt, part = 0, 0
+    for n in ns:
+        for _ in range(per_n):
+            pid.extend(range(nxt, nxt + n))
+            pk.extend([part] * n)
+            nxt += n
+            part += 1
+    table = pdp.ColumnTable({"pid": np.asarray(pid, np.int64), "pk": np.asarray(pk, np.int64),
+                             "v": np.zeros(len(pid))})
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT], noise_kind=pdp.NoiseKind.LAPLACE,
+                                 max_partitions_contributed=1, max_contributions_per_partition=1)
+    sink, _ = _aggregate(table, params, eps=2.0, delta=0.01, seed=13)
+    plan = CB.recognise(sink)
+    keep = np.asarray(CB.AggregateRun(CB.ColumnarBackend(), plan)._selection().keep_prob)
+    kept = np.zeros(part, dtype=bool)
+    for k, _ in sink:
+        kept[int(k)] = True
+    for i, n in enumerate(ns):
+        p = float(keep[min(n, len(keep) - 1)])
+        k = int(kept[i * per_n:(i + 1) * per_n].sum())
+        sd = math.sqrt(per_n * p * (1 - p))
+        assert abs(k - per_n * p) <= 5 * sd + 1, (n, k, per_n * p)
+
+
+def test_mean_metrics_consistent(device):
+    """MEAN output: mean = middle + noisy_nsum / max(1, noisy_count) and
+    sum = mean * noisy_count (MeanMechanism, dp_computations.py:562-568), with
+    enormous epsilon so the noise is negligible."""
+    rng = np.random.default_rng(4)
+    n, U, P = 50_000, 2_000, 40
+    pid = rng.integers(0, U, n)
+    pk = rng.integers(0, P, n)
+    v = rng.uniform(0, 10, n)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.MEAN, pdp.Metrics.COUNT, pdp.Metrics.SUM],
+                                 noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=P,
+                                 max_contributions_per_partition=64, min_value=0.0, max_value=10.0)
+    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": v})
+    sink, _ = _aggregate(table, params, eps=1e9, delta=1e-6, public=list(range(P)), seed=14)
+    out = dict(sink)
+    for p in range(P):
+        m = out[p]
+        sel = pk == p
+        assert m.count == pytest.approx(sel.sum(), abs=1e-3)
+        assert m.mean == pytest.approx(v[sel].mean(), rel=1e-6)
+        assert m.sum == pytest.approx(v[sel].sum(), rel=1e-6)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_data():
+    rng = np.random.default_rng(21)
+    n, U, P = 40_000, 3_000, 500
+    pid = rng.integers(0, U, n)
+    pk = rng.integers(0, P, n)
+    v = rng.normal(4, 2, n)
+    owner = pid % 2  # privacy ids never span ranks
+    order = np.argsort(owner, kind="stable")  # rank 0's rows first, then rank 1's
+    return pid[order], pk[order], v[order], owner[order], P
+
+
+def _params_2rank():
+    return pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.PRIVACY_ID_COUNT],
+                               noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=3,
+                               max_contributions_per_partition=2, min_value=0.0, max_value=8.0)
+
+
+def _two_rank_worker(rank, port, results):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        pid, pk, v, owner, P = _rank_data()
+        mine = owner == rank
+        table = pdp.ColumnTable({"pid": pid[mine], "pk": pk[mine], "v": v[mine]},
+                                n_privacy_ids=int(pid.max()) + 1, n_partitions=P)
+        sink, _ = _aggregate(table, _params_2rank(), eps=1.0, delta=1e-6, seed=99)
+        results[rank] = [(int(k), tuple(m)) for k, m in sink]
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_match_single_process(device):
+    """Rows sharded by privacy id over two ranks (gloo exchange, both on this
+    GPU): the union of the ranks' partitions equals the single-process result
+    (same samples, same selection, same noise streams; fp sums within 1e-9)."""
+    import torch.multiprocessing as mp
+    pid, pk, v, owner, P = _rank_data()
+    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": v}, n_privacy_ids=int(pid.max()) + 1, n_partitions=P)
+    sink, _ = _aggregate(table, _params_2rank(), eps=1.0, delta=1e-6, seed=99)
+    single = {int(k): tuple(m) for k, m in sink}
+    ctx = mp.get_context("spawn")
+    manager = ctx.Manager()
+    results = manager.dict()
+    mp.spawn(_two_rank_worker, args=(_free_port(), results), nprocs=2, join=True)
+    res = dict(results)
+    assert all(isinstance(res[r], list) for r in (0, 1)), res
+    merged = {}
+    for r in (0, 1):
+        for k, m in res[r]:
+            assert k not in merged
+            merged[k] = m
+    assert set(merged) == set(single)
+    for k in single:
+        np.testing.assert_allclose(merged[k], single[k], rtol=1e-9, atol=1e-6)
