@@ -105,6 +105,7 @@ def main():
     import torch.distributed as dist
     from pipelinedp_amd import _native as N
     from pipelinedp_amd import executor as X
+    from pipelinedp_amd import parallel
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -127,12 +128,11 @@ def main():
         MIN_VALUE, MAX_VALUE)
     torch.cuda.synchronize()
 
-    P_pad = ((P + world - 1) // world) * world
-    slice_len = P_pad // world
+    P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
     plan = X.bound_plan(n, U, P_pad, bounding)
     acc = X.new_accumulators(P_pad, bounding, device)
-    seed_base = int.from_bytes(os.urandom(8), "little")
+    seed_base = parallel.broadcast_seeds((int.from_bytes(os.urandom(8), "little"),))[0]
 
     def step(i):
         for t in acc.values():
@@ -141,21 +141,11 @@ def main():
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
                            check_keys=False)
-        if world > 1:
-            part = {}
-            for k, t in acc.items():
-                if t is None:
-                    continue
-                out = torch.empty(slice_len, dtype=t.dtype, device=device)
-                dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM)
-                part[k] = out
-            mine = {k: part.get(k) for k in acc}
-        else:
-            mine = acc
+        mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
                                           seed_noise=seed_base ^ (i * 104729 + 2),
-                                          partition_offset=rank * slice_len)
+                                          partition_offset=first)
         return n_kept
 
     for i in range(args.warmup):

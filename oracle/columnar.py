@@ -16,7 +16,8 @@ Restates, for one shard of dense columns (privacy_id, partition_key, value):
 
 Uniform sampling without replacement is "keep the k smallest i.i.d. uniform
 priorities".  With ``priorities="hash"`` the priorities are the exact
-counter-based values the HIP kernels compute (SplitMix64 finaliser), so the
+counter-based values the HIP kernels compute (pair keys: a MurmurHash3 fmix32
+hash of (seed, pid, pk); row keys: SplitMix64 of the global row index), so the
 sampled sets match the GPU bit-for-bit; with ``priorities="rng"`` they come
 from a NumPy Generator (the reference's np.random.choice distribution).
 Noise and selection use the same Philox4x32-10 streams as the kernels.
