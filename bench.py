@@ -34,10 +34,19 @@ if HERE not in sys.path:
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
-# HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 gfx950 wide-load
-# correction + WRITE_SIZE, MI355X_MICROARCH.md "HBM"), profiles/r01/pmc_*.txt;
-# None where not measured for the current kernel set.
-TRAFFIC_BYTES = {}
+# HBM bytes per launch from rocprofv3 PMC passes over this same bench command
+# (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
+# wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for the
+# default C2 shape only; None otherwise.
+PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "s2_pmc.json")
+
+
+def pmc_traffic(n_rows):
+    if n_rows != ROWS_PER_GPU or not os.path.exists(PMC_SUMMARY):
+        return {}
+    with open(PMC_SUMMARY) as f:
+        kernels = json.load(f)["kernels"]
+    return {k: v["hbm_bytes"] for k, v in kernels.items() if "hbm_bytes" in v}
 
 # workload constants (C2)
 ROWS_PER_GPU = 100_000_000
@@ -181,6 +190,7 @@ def main():
     total_rows = n * world * args.steps
     value_rows_s = total_rows / elapsed
     path_bytes = 24.0 * n + kept * (8 + 8 * 3 + 8 * 3)
+    traffic = pmc_traffic(n)
     result = {
         "metric": "input rows/sec aggregated (whole node) + achieved HBM GB/s vs peak",
         "value": value_rows_s,
@@ -207,7 +217,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": TRAFFIC_BYTES.get(dom),
+            "traffic": traffic.get(dom),
+            "traffic_source": os.path.relpath(PMC_SUMMARY, HERE) if dom in traffic else None,
             "bytes_per_launch": alg_bytes,
             "avg_ms": kernel_ms[dom],
         },
@@ -216,6 +227,7 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "bytes_per_step": path_bytes,
+            "traffic_per_step": sum(traffic.values()) if traffic else None,
         },
         "kernel_ms": kernel_ms,
         "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
