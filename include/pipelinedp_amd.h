@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 2
+#define PDP_ABI_VERSION 3
 
 /* error codes */
 #define PDP_OK 0
@@ -52,7 +52,8 @@ typedef struct pdp_bound_config {
   int64_t n_rows;        /* rows in this shard (< 2^32) */
   int64_t n_privacy_ids; /* U: privacy ids are dense in [0, U) */
   int64_t n_partitions;  /* P: partition keys are dense in [0, P) (< 2^32) */
-  int32_t l0;            /* max_partitions_contributed (1..PDP_MAX_L0) */
+  int32_t l0;            /* max_partitions_contributed (1..PDP_MAX_L0); 0 = no
+                            cross-partition bounding (LinfSampler / NoOpSampler) */
   int32_t linf;          /* max_contributions_per_partition (1..PDP_MAX_LINF); 0 = keep all rows */
   int32_t value_kind;    /* PDP_VALUE_* */
   int32_t flags;         /* PDP_ACC_* | PDP_SUM_* */
@@ -65,15 +66,24 @@ typedef struct pdp_bound_config {
   uint64_t seed;         /* sampling seed */
   int32_t algorithm;     /* PDP_ALGO_*; every algorithm keeps the same samples */
   int32_t merge;         /* PDP_MERGE_*: how BUCKETED merges kept pairs per partition */
+  int32_t max_contributions; /* > 0: SamplingPerPrivacyIdContributionBounder — keep a
+                                uniform sample of <= this many rows per privacy id
+                                (1..PDP_MAX_CONTRIBUTIONS); needs l0 = linf = 0 */
+  int32_t rows_are_units;    /* != 0: contribution_bounds_already_enforced — every row is
+                                its own accumulator; privacy_id may be NULL */
 } pdp_bound_config;
 
 #define PDP_MAX_L0 256
 #define PDP_MAX_LINF 256
+#define PDP_MAX_CONTRIBUTIONS 256
 
 /* bounding algorithms (identical results, different data movement) */
 #define PDP_ALGO_AUTO 0
 #define PDP_ALGO_GLOBAL_SKETCH 1 /* per-pid / per-pair sketches in HBM, device atomics */
 #define PDP_ALGO_BUCKETED 2      /* rows partitioned by pid bucket, sketches in LDS */
+#define PDP_ALGO_PAIR_TABLE 3    /* device hash table of (pid, pk) pairs: the bounders
+                                    without cross-partition sampling (l0 = 0,
+                                    max_contributions, rows_are_units); chosen by AUTO */
 
 /* per-partition merge of the kept pairs (BUCKETED; identical sums up to fp
  * summation order) */
@@ -121,6 +131,10 @@ int pdp_bound_workspace_bytes(const pdp_bound_config* cfg, uint64_t* bytes);
  * (contribution_bounders.py:72-111) and, with linf = 0,
  * SamplingCrossPartitionContributionBounder (contribution_bounders.py:168-201),
  * i.e. LocalBackend.sample_fixed_per_key (pipeline_backend.py:531-547) twice.
+ * With l0 = 0: LinfSampler (linf > 0, :204-230) or NoOpSampler (linf = 0,
+ * :233-246); with max_contributions: SamplingPerPrivacyIdContributionBounder
+ * (:114-156); with rows_are_units: DPEngine's contribution_bounds_already_enforced
+ * branch ("Wrap values into accumulators", dp_engine.py:143-150).
  * `pk_allowed` (nullable, u8[n_partitions]) drops rows of non-public
  * partitions first (DPEngine._drop_partitions, dp_engine.py:290-296).
  * The workspace is fully (re)initialised on `stream` by this call. */

@@ -6,7 +6,10 @@ Restates, for one shard of dense columns (privacy_id, partition_key, value):
   (reference pipeline_dp/contribution_bounders.py:72-111): per (pid, pk) keep a
   uniform sample of <= linf rows, per pid keep a uniform sample of <= l0 of its
   distinct partitions; linf = 0 restates SamplingCrossPartitionContributionBounder
-  (:168-201, every row of a kept pair);
+  (:168-201, every row of a kept pair); l0 = 0 restates LinfSampler (:204-230)
+  and, with linf = 0, NoOpSampler (:233-246); max_contributions restates
+  SamplingPerPrivacyIdContributionBounder (:114-156); rows_are_units restates
+  DPEngine's contribution_bounds_already_enforced branch (dp_engine.py:143-150);
 * CompoundCombiner.create_accumulator + merge (combiners.py:749-764) for the
   Count/Sum/Mean/Variance/PrivacyIdCount children (combiners.py:241-587);
 * LocalBackend.combine_accumulators_per_key (pipeline_backend.py:555-565);
@@ -156,13 +159,25 @@ def _ranks_within(groups_sorted):
     return np.arange(n, dtype=np.int64) - starts[gid]
 
 
+def derive_pid_row_seed(seed):
+    """Row priorities of SamplingPerPrivacyIdContributionBounder (pdp_pairs.hip)."""
+    return derive_row_seed(int(seed) ^ 0x2545F4914F6CDD1D)
+
+
 def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, value_kind,
                      flags, min_value=0.0, max_value=0.0, middle=0.0, min_sum=0.0,
                      max_sum=0.0, seed=0, row_offset=0, allowed=None, priorities="hash",
-                     rng=None, rand_shift=None):
-    """Returns dense per-partition accumulators (dict of numpy arrays, length P)."""
-    pid = np.asarray(pid, dtype=np.int64)
+                     rng=None, rand_shift=None, max_contributions=0, rows_are_units=False):
+    """Returns dense per-partition accumulators (dict of numpy arrays, length P).
+
+    l0 = 0: no cross-partition sampling (every pair kept).  max_contributions:
+    per pid keep the rows of the max_contributions smallest row priorities
+    first.  rows_are_units: every row is its own pair (pid is ignored)."""
     pk = np.asarray(pk, dtype=np.int64)
+    if rows_are_units:  # one privacy unit per row: the row index is the pid
+        pid = np.arange(len(pk), dtype=np.int64)
+        n_privacy_ids = max(1, len(pk))
+    pid = np.asarray(pid, dtype=np.int64)
     n = len(pid)
     P = int(n_partitions)
     out = {
@@ -177,6 +192,17 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
     if allowed is not None:
         valid &= np.asarray(allowed, dtype=bool)[np.clip(pk, 0, P - 1)]
     pid, pk, local = pid[valid], pk[valid], local[valid]
+    if max_contributions:
+        # per pid, the rows of the max_contributions smallest row priorities
+        if priorities == "hash":
+            prio = row_priority(derive_pid_row_seed(seed), row_offset + local, local)
+        else:
+            prio = (rng.integers(0, 1 << 32, size=len(local), dtype=np.uint64) << _U64(32)) | \
+                local.astype(np.uint64)
+        o = np.lexsort((prio, pid))
+        keep = np.zeros(len(pid), dtype=bool)
+        keep[o] = _ranks_within(pid[o]) < max_contributions
+        pid, pk, local = pid[keep], pk[keep], local[keep]
     if len(pid) == 0:
         return out
     if rand_shift is None:
@@ -197,7 +223,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
     o2 = np.lexsort((pprio, pair_pid))
     rank = np.empty(len(pair_pid), dtype=np.int64)
     rank[o2] = _ranks_within(pair_pid[o2])
-    kept_pair = rank < l0
+    kept_pair = rank < l0 if l0 > 0 else np.ones(len(pair_pid), dtype=bool)
     # rows of kept pairs
     rk = kept_pair[row_pair]
     r_pair, r_local = row_pair[rk], ls[rk]

@@ -44,13 +44,19 @@ def _py(x):
     return x
 
 
-def _no_sampling_rows(rng, n_pids, l0, linf, n_partitions, value_fn, pid_fmt=None, pk_fmt=None):
+def _no_sampling_rows(rng, n_pids, l0, linf, n_partitions, value_fn, pid_fmt=None, pk_fmt=None,
+                      rows_per_pid=None):
     rows = []
     for u in range(n_pids):
         d = int(rng.integers(1, l0 + 1))
         pks = rng.choice(n_partitions, size=d, replace=False)
+        budget = rows_per_pid  # SamplingPerPrivacyId: <= max_contributions rows per pid
         for k in pks:
-            for _ in range(int(rng.integers(1, linf + 1))):
+            r = int(rng.integers(1, linf + 1))
+            if budget is not None:
+                r = min(r, budget)
+                budget -= r
+            for _ in range(r):
                 pid = pid_fmt(u) if pid_fmt else u
                 pk = pk_fmt(int(k)) if pk_fmt else int(k)
                 rows.append([pid, pk, value_fn(rng)])
@@ -76,7 +82,41 @@ CASES = [
          public=[0, 1, 2, 3, 5, 8, 13, 21, 34, 55, 89]),
     dict(name="string_keys", metrics=["COUNT", "SUM"], noise="LAPLACE", l0=2, linf=2, min_value=0.0,
          max_value=3.0, n_pids=150, n_partitions=20, value="normal1_1", string_keys=True),
+    # bounders other than Cross+Per (dp_engine.py:380-400); "gen_*" shape the
+    # data so that no sampling fires under the case's bounds
+    dict(name="linf_sampler", bounder="linf", metrics=["COUNT", "SUM", "MEAN"], noise="LAPLACE", l0=2,
+         linf=2, min_value=0.0, max_value=8.0, n_pids=300, n_partitions=40, value="normal5_3",
+         gen_pairs_per_pid=7, gen_rows_per_pair=2),
+    dict(name="noop_sampler", bounder="noop", metrics=["SUM", "PRIVACY_ID_COUNT"],
+         noise="LAPLACE", l0=1, linf=1, min_sum=-5.0, max_sum=12.0, n_pids=300, n_partitions=40,
+         value="normal2_3", gen_pairs_per_pid=5, gen_rows_per_pair=4),
+    dict(name="max_contributions", bounder="per_pid", metrics=["COUNT", "SUM", "PRIVACY_ID_COUNT"],
+         noise="LAPLACE", max_contributions=6, min_value=1, max_value=4, n_pids=300, n_partitions=30,
+         value="int1_5", gen_pairs_per_pid=4, gen_rows_per_pair=3, public=list(range(0, 30, 2))),
+    dict(name="bounds_already_enforced", bounder="enforced", metrics=["COUNT", "SUM", "MEAN"],
+         noise="LAPLACE", l0=3, linf=2, min_value=0.0, max_value=6.0, n_pids=200, n_partitions=25,
+         value="normal2_3", gen_pairs_per_pid=3, gen_rows_per_pair=3),
 ]
+
+
+def case_params(pdp, case):
+    """AggregateParams of a fixture case (shared with tests/golden_util.py)."""
+    kw = {}
+    for k in ("min_value", "max_value", "min_sum", "max_sum"):
+        if k in case:
+            kw[{"min_sum": "min_sum_per_partition", "max_sum": "max_sum_per_partition"}.get(k, k)] = case[k]
+    bounder = case.get("bounder", "default")
+    if bounder == "per_pid":
+        kw["max_contributions"] = case["max_contributions"]
+    else:
+        kw["max_partitions_contributed"] = case["l0"]
+        kw["max_contributions_per_partition"] = case["linf"]
+    if bounder in ("linf", "noop"):
+        kw["perform_cross_partition_contribution_bounding"] = False
+    if bounder == "enforced":
+        kw["contribution_bounds_already_enforced"] = True
+    return pdp.AggregateParams(metrics=[getattr(pdp.Metrics, m) for m in case["metrics"]],
+                               noise_kind=getattr(pdp.NoiseKind, case["noise"]), **kw)
 
 VALUE_FNS = {
     "int1_5": lambda r: int(r.integers(1, 6)),
@@ -94,23 +134,16 @@ def run_case(pdp, case, seed):
     rng = np.random.default_rng(seed)
     fmt_pid = (lambda u: f"user-{u}") if case.get("string_keys") else None
     fmt_pk = (lambda k: f"item/{k}") if case.get("string_keys") else None
-    if case.get("rows_per_pair"):
-        rows = _no_sampling_rows(rng, case["n_pids"], case["l0"], case["rows_per_pair"],
-                                 case["n_partitions"], VALUE_FNS[case["value"]], fmt_pid, fmt_pk)
-    else:
-        rows = _no_sampling_rows(rng, case["n_pids"], case["l0"], case["linf"], case["n_partitions"],
-                                 VALUE_FNS[case["value"]], fmt_pid, fmt_pk)
-    kw = {}
-    for k in ("min_value", "max_value", "min_sum", "max_sum"):
-        if k in case:
-            kw[{"min_sum": "min_sum_per_partition", "max_sum": "max_sum_per_partition"}.get(k, k)] = case[k]
-    params = pdp.AggregateParams(metrics=[getattr(pdp.Metrics, m) for m in case["metrics"]],
-                                 noise_kind=getattr(pdp.NoiseKind, case["noise"]),
-                                 max_partitions_contributed=case["l0"],
-                                 max_contributions_per_partition=case["linf"], **kw)
+    pairs = case.get("gen_pairs_per_pid", case.get("l0"))
+    per_pair = case.get("gen_rows_per_pair", case.get("rows_per_pair", case.get("linf")))
+    rows = _no_sampling_rows(rng, case["n_pids"], pairs, per_pair, case["n_partitions"],
+                             VALUE_FNS[case["value"]], fmt_pid, fmt_pk,
+                             rows_per_pid=case.get("max_contributions"))
+    params = case_params(pdp, case)
     accountant = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
     engine = pdp.DPEngine(accountant, pdp.LocalBackend())
-    extractors = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0],
+    enforced = case.get("bounder") == "enforced"
+    extractors = pdp.DataExtractors(privacy_id_extractor=None if enforced else (lambda r: r[0]),
                                     partition_extractor=lambda r: r[1],
                                     value_extractor=lambda r: r[2])
 
@@ -133,7 +166,13 @@ def run_case(pdp, case, seed):
         partition_selection.create_partition_selection_strategy = saved_ps
     budgets = [[m.mechanism_spec.mechanism_type.value, m.mechanism_spec.eps, m.mechanism_spec.delta]
                for m in accountant._mechanisms]
-    return {"name": case["name"], "case": case, "rows": rows, "expected": result, "budgets": budgets}
+    # the bounder class the reference's DPEngine picks for these params (dp_engine.py:380-400)
+    probe = pdp.DPEngine(pdp.NaiveBudgetAccountant(1.0, 1e-6), pdp.LocalBackend())
+    comb = combiners.create_compound_combiner(params, pdp.NaiveBudgetAccountant(1.0, 1e-6))
+    bounder = None if params.contribution_bounds_already_enforced else type(
+        probe._create_contribution_bounder(params, comb.expects_per_partition_sampling())).__name__
+    return {"name": case["name"], "case": case, "rows": rows, "expected": result, "budgets": budgets,
+            "reference_bounder": bounder}
 
 
 def sampling_fixture(pdp, trials=4000):

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 2
+ABI_VERSION = 3
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 SELECT_ALL_NONEMPTY = 0
@@ -27,10 +27,11 @@ SELECT_GAUSSIAN_THRESHOLDING = 3
 SELECT_PUBLIC = 4
 OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID = 1, 2, 3, 4, 5, 6
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
-ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED = 0, 1, 2
+ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED, ALGO_PAIR_TABLE = 0, 1, 2, 3
 MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
 MAX_L0 = 256
 MAX_LINF = 256
+MAX_CONTRIBUTIONS = 256
 MAX_OPS = 8
 
 EXPORTED_SYMBOLS = (
@@ -73,6 +74,8 @@ class BoundConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("algorithm", ctypes.c_int32),
         ("merge", ctypes.c_int32),
+        ("max_contributions", ctypes.c_int32),
+        ("rows_are_units", ctypes.c_int32),
     ]
 
 

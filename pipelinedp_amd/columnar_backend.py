@@ -108,9 +108,11 @@ class AggregatePlan:
         self.extract_fn = None
         self.public_keys = None          # public partitions (filter) or None
         self.public_padding = None       # public partitions (padding) or None
-        self.bounder = None              # "cross_and_per" | "cross" | ...
-        self.linf_from_graph = None
-        self.l0_from_graph = None
+        self.bounder = None              # "cross_and_per" | "cross" | "linf" | "noop" |
+                                         # "per_privacy_id" | "already_enforced"
+        self.linf_from_graph = None      # n of "Sample per (privacy_id, partition_key)"
+        self.l0_from_graph = None        # n of "Sample per privacy_id" (Cross+Per: L0;
+                                         # PerPrivacyId: max_contributions)
         self.combiner = None
         self.selection = None            # functools.partial of filter_fn
         self.compute_metrics = False
@@ -176,14 +178,13 @@ def recognise(sink) -> AggregatePlan:
     elif stages == CROSS_ONLY:
         plan.bounder = "cross"
     elif stages == PER_PRIVACY_ID:
-        raise NotImplementedError("max_contributions (SamplingPerPrivacyIdContributionBounder) is "
-                                  "not on the pipelinedp_amd hot path yet")
-    elif stages == LINF_ONLY or stages == NOOP:
-        raise NotImplementedError("perform_cross_partition_contribution_bounding=False is not "
-                                  "supported by ColumnarBackend yet")
+        plan.bounder = "per_privacy_id"
+    elif stages == LINF_ONLY:
+        plan.bounder = "linf"
+    elif stages == NOOP:
+        plan.bounder = "noop"
     elif stages == ALREADY_ENFORCED:
-        raise NotImplementedError("contribution_bounds_already_enforced is not supported by "
-                                  "ColumnarBackend yet")
+        plan.bounder = "already_enforced"
     else:
         raise NotImplementedError(f"unrecognised stages for ColumnarBackend: {sorted(stages)}")
     if plan.combiner is None or not plan.compute_metrics:
@@ -453,9 +454,10 @@ class AggregateRun:
             val_raw = [r[2] for r in rows] if self.prog.needs_values else None
             n_pid = n_pk = None
             pk_decode = None
-        if pid_raw is None:
-            raise NotImplementedError("privacy_id_extractor=None needs contribution_bounds_already_enforced")
-        pid_enc = C.encode_keys(_host_or_device(pid_raw), n_pid)
+        units = self.plan.bounder == "already_enforced"  # no privacy ids on this path
+        if pid_raw is None and not units:
+            raise ValueError("privacy_id_extractor is required unless contribution_bounds_already_enforced")
+        pid_enc = None if units else C.encode_keys(_host_or_device(pid_raw), n_pid)
         pk_enc = C.encode_keys(_host_or_device(pk_raw), n_pk)
         if pk_decode is not None and pk_enc.decode is None:
             pk_enc.decode = np.asarray(pk_decode, dtype=object)
@@ -467,7 +469,8 @@ class AggregateRun:
             pk_enc = parallel.global_partition_keys(pk_enc)
             if public is not None and pk_enc.decode is not None:
                 public_codes = np.asarray([pk_enc.encode[k] for k in public], dtype=np.int64)
-        pid_t = torch.as_tensor(pid_enc.codes).to(device=device, dtype=torch.int64).contiguous()
+        pid_t = None if pid_enc is None else \
+            torch.as_tensor(pid_enc.codes).to(device=device, dtype=torch.int64).contiguous()
         pk_t = torch.as_tensor(pk_enc.codes).to(device=device, dtype=torch.int64).contiguous()
         val_t = None
         value_kind = N.VALUE_NONE
@@ -486,13 +489,23 @@ class AggregateRun:
         flags = self.prog.flags
         if (flags & (N.ACC_SUM | N.SUM_PER_PARTITION)) and value_kind == N.VALUE_I64 and self.prog.int_bounds:
             flags |= N.SUM_INT
-        l0 = int(p.max_partitions_contributed)
-        linf = int(p.max_contributions_per_partition) if self.plan.bounder == "cross_and_per" else 0
-        if self.plan.l0_from_graph is not None and self.plan.l0_from_graph != l0:
-            raise ValueError("inconsistent max_partitions_contributed in the graph")
+        bounder = self.plan.bounder
+        l0 = linf = max_contributions = 0
+        if bounder in ("cross_and_per", "cross"):  # contribution_bounders.py:62-111, 159-201
+            l0 = int(p.max_partitions_contributed)
+            if self.plan.l0_from_graph is not None and self.plan.l0_from_graph != l0:
+                raise ValueError("inconsistent max_partitions_contributed in the graph")
+        if bounder in ("cross_and_per", "linf"):   # :72-111, :204-230
+            linf = int(p.max_contributions_per_partition)
+            if self.plan.linf_from_graph is not None and self.plan.linf_from_graph != linf:
+                raise ValueError("inconsistent max_contributions_per_partition in the graph")
+        if bounder == "per_privacy_id":             # :114-156
+            max_contributions = int(self.plan.l0_from_graph or p.max_contributions)
         return BoundingSpec(l0=l0, linf=linf, value_kind=value_kind, flags=flags,
                             min_value=self.prog.min_value, max_value=self.prog.max_value,
-                            middle=self.prog.middle, min_sum=self.prog.min_sum, max_sum=self.prog.max_sum)
+                            middle=self.prog.middle, min_sum=self.prog.min_sum, max_sum=self.prog.max_sum,
+                            max_contributions=max_contributions,
+                            rows_are_units=bounder == "already_enforced")
 
     def _bound(self):
         from pipelinedp_amd import executor as X
@@ -501,19 +514,20 @@ class AggregateRun:
         spec = self._bounding_spec(vk)
         world, _ = parallel.world_info()
         P, _ = parallel.partition_slices(pk_enc.n, world)  # padded to a multiple of the ranks
-        row_offset = parallel.row_offset(pid_t.numel())
+        row_offset = parallel.row_offset(pk_t.numel())
         allowed = None
         if public_codes is not None:
             mask = np.zeros(P, dtype=np.uint8)
             mask[public_codes] = 1
-            allowed = torch.as_tensor(mask).to(pid_t.device)
+            allowed = torch.as_tensor(mask).to(pk_t.device)
         seed_bound, _, _ = self._seeds
-        if pid_t.numel() == 0:
-            acc = X.new_accumulators(P, spec, pid_t.device)
+        n_pid = 1 if pid_enc is None else pid_enc.n
+        if pk_t.numel() == 0:
+            acc = X.new_accumulators(P, spec, pk_t.device)
         else:
-            acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=pid_enc.n, n_partitions=P,
+            acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=n_pid, n_partitions=P,
                                      bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset)
-            self.backend.last_plan_info = X.bound_plan(pid_t.numel(), pid_enc.n, P, spec)
+            self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec)
         return acc, spec, pk_enc, allowed
 
     def _selection(self):

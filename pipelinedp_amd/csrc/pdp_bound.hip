@@ -196,18 +196,21 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "n_privacy_ids must be in [1, 2^40)");
   if (c->n_partitions < 1 || c->n_partitions >= ((int64_t)1 << 32))
     return set_error(PDP_E_INVALID, "n_partitions must be in [1, 2^32)");
-  if (c->l0 < 1 || c->l0 > PDP_MAX_L0)
-    return set_error(PDP_E_UNSUPPORTED, "l0 out of supported range [1, 256]");
+  if (c->l0 < 0 || c->l0 > PDP_MAX_L0)
+    return set_error(PDP_E_UNSUPPORTED, "l0 out of supported range [0, 256]");
   if (c->linf < 0 || c->linf > PDP_MAX_LINF)
     return set_error(PDP_E_UNSUPPORTED, "linf out of supported range [0, 256]");
   if (c->value_kind < PDP_VALUE_NONE || c->value_kind > PDP_VALUE_I64)
     return set_error(PDP_E_INVALID, "bad value_kind");
   if (c->value_kind != PDP_VALUE_I64 && (c->flags & PDP_SUM_INT))
     return set_error(PDP_E_INVALID, "PDP_SUM_INT requires int64 values");
-  if (c->algorithm < PDP_ALGO_AUTO || c->algorithm > PDP_ALGO_BUCKETED)
+  if (c->algorithm < PDP_ALGO_AUTO || c->algorithm > PDP_ALGO_PAIR_TABLE)
     return set_error(PDP_E_INVALID, "bad algorithm");
   if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
     return set_error(PDP_E_INVALID, "bad merge");
+  if (pairs_mode(c)) return pairs_validate(c);
+  if (c->algorithm == PDP_ALGO_PAIR_TABLE)
+    return set_error(PDP_E_UNSUPPORTED, "PDP_ALGO_PAIR_TABLE runs only the bounders without L0 sampling");
   if (make_plan(c).algorithm < 0)
     return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge infeasible for this l0/linf/P");
   return PDP_OK;
@@ -283,7 +286,6 @@ __global__ void __launch_bounds__(kBlock) k_pair_rows(KP kp, const int64_t* __re
                                                       double* pair_fsum, double* pair_nsum,
                                                       double* pair_nsum2) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int flags = kp.clip.flags;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += stride) {
     const int64_t u = pid[i];
     const int64_t k = pk[i];
@@ -300,42 +302,10 @@ __global__ void __launch_bounds__(kBlock) k_pair_rows(KP kp, const int64_t* __re
       const uint64_t y = row_key(kp.row_seed, kp.row_offset + i, (uint32_t)i);
       unsigned long long* r = pair_rows + slot * kp.linf;
       if (y < r[kp.linf - 1]) sketch_insert(r, kp.linf, y);
-    } else if (VALUE_KIND != PDP_VALUE_NONE) {
-      double v;
-      long long iv;
-      load_value<VALUE_KIND>(value, (uint32_t)i, &v, &iv);
-      if (flags & PDP_SUM_PER_PARTITION) {
-        if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(pair_fsum + slot), (unsigned long long)iv);
-        else unsafeAtomicAdd(pair_fsum + slot, v);
-      } else if (flags & PDP_ACC_SUM) {
-        if (flags & PDP_SUM_INT)
-          atomicAdd((unsigned long long*)(pair_fsum + slot),
-                    (unsigned long long)clamp_ll(iv, (long long)kp.clip.lo, (long long)kp.clip.hi));
-        else unsafeAtomicAdd(pair_fsum + slot, fmin(fmax(v, kp.clip.lo), kp.clip.hi));
-      }
-      if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
-        const double c = fmin(fmax(v, kp.clip.lo), kp.clip.hi) - kp.clip.mid;
-        if (flags & PDP_ACC_NSUM) unsafeAtomicAdd(pair_nsum + slot, c);
-        if (flags & PDP_ACC_NSUM2) unsafeAtomicAdd(pair_nsum2 + slot, c * c);
-      }
+    } else {
+      accumulate_row<VALUE_KIND>(value, (uint32_t)i, slot, pair_fsum, pair_nsum, pair_nsum2, kp.clip);
     }
   }
-}
-
-// pair accumulator of a KEEP_ALL_ROWS pair from its summed slots
-__device__ __forceinline__ PairSums pair_sums_from_totals(long long cnt, double fsum_or_bits, double nsum,
-                                                          double nsum2, const ClipParams& cp) {
-  PairSums s{cnt, 0, 0.0, nsum, nsum2};
-  long long ibits = __double_as_longlong(fsum_or_bits);
-  if (cp.flags & PDP_SUM_PER_PARTITION) {
-    if (cp.flags & PDP_SUM_INT) s.isum = clamp_ll(ibits, (long long)cp.min_sum, (long long)cp.max_sum);
-    else s.fsum = fmin(fmax(fsum_or_bits, cp.min_sum), cp.max_sum);
-  } else if (cp.flags & PDP_SUM_INT) {
-    s.isum = ibits;
-  } else {
-    s.fsum = fsum_or_bits;
-  }
-  return s;
 }
 
 template <int VALUE_KIND, bool KEEP_ALL_ROWS>
@@ -1091,6 +1061,30 @@ __global__ void __launch_bounds__(kBlock) k_scan_apply(unsigned* v, int64_t n,
 }
 
 
+}  // namespace
+
+int64_t scan_chunk_sums_len(int64_t n) { return (n + kScanChunk - 1) / kScanChunk + 1; }
+
+int scan_u32(unsigned* v, int64_t n, unsigned* chunk_sums, hipStream_t st) {
+  const int64_t n_chunks = (n + kScanChunk - 1) / kScanChunk;
+  if (n_chunks == 0) return set_error(PDP_E_INVALID, "scan of an empty array");
+  PDP_PROF_BEGIN("k_scan_chunks", st);
+  hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, v, n, chunk_sums);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scan_top", st);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, st, chunk_sums, n_chunks);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_scan_apply", st);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, v, n, chunk_sums, n_chunks);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+namespace {
+
 // ---------------------------------------------------------- launchers --
 template <int VK, bool KA>
 int launch_global_rows(const KP& kp, hipStream_t st, const int64_t* pid, const int64_t* pk, const void* value,
@@ -1183,6 +1177,11 @@ struct Bucket {
 int check_ws(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes, Plan* p, Ws* w) {
   const int rc = validate(cfg);
   if (rc != PDP_OK) return rc;
+  if (pairs_mode(cfg)) {
+    if (workspace == nullptr || workspace_bytes < pairs_workspace_bytes(cfg))
+      return set_error(PDP_E_WORKSPACE, "workspace too small (see pdp_bound_workspace_bytes)");
+    return PDP_OK;
+  }
   *p = make_plan(cfg);
   *w = layout(cfg, *p);
   if (workspace == nullptr || workspace_bytes < w->total)
@@ -1201,6 +1200,12 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   const int rc = validate(cfg);
   if (rc != PDP_OK) return rc;
   if (info == nullptr) return set_error(PDP_E_INVALID, "info is NULL");
+  if (pairs_mode(cfg)) {
+    *info = pdp_bound_plan_info{};
+    info->algorithm = PDP_ALGO_PAIR_TABLE;
+    info->pk_bits = bits_for(cfg->n_partitions);
+    return PDP_OK;
+  }
   const Plan p = make_plan(cfg);
   info->algorithm = p.algorithm;
   info->bucket_bits = p.bucket_bits;
@@ -1219,7 +1224,7 @@ int pdp_bound_workspace_bytes(const pdp_bound_config* cfg, uint64_t* bytes) {
   const int rc = validate(cfg);
   if (rc != PDP_OK) return rc;
   if (bytes == nullptr) return set_error(PDP_E_INVALID, "bytes is NULL");
-  *bytes = layout(cfg, make_plan(cfg)).total;
+  *bytes = pairs_mode(cfg) ? pairs_workspace_bytes(cfg) : layout(cfg, make_plan(cfg)).total;
   return PDP_OK;
 }
 
@@ -1230,12 +1235,13 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   Ws w;
   int rc = check_ws(cfg, workspace, workspace_bytes, &p, &w);
   if (rc != PDP_OK) return rc;
-  if (cfg->n_rows > 0 && (privacy_id == nullptr || partition_key == nullptr))
+  if (cfg->n_rows > 0 && (partition_key == nullptr || (privacy_id == nullptr && !cfg->rows_are_units)))
     return set_error(PDP_E_INVALID, "key columns are NULL");
   if (cfg->value_kind != PDP_VALUE_NONE && cfg->n_rows > 0 && value == nullptr)
     return set_error(PDP_E_INVALID, "value column is NULL");
   hipStream_t st = (hipStream_t)stream;
   char* ws = (char*)workspace;
+  if (pairs_mode(cfg)) return pairs_bound(cfg, privacy_id, partition_key, value, pk_allowed, ws, st);
   KP kp = make_kp(cfg, p);
   kp.keys_vec = ((((uintptr_t)privacy_id) | ((uintptr_t)partition_key)) & 15) == 0;
   unsigned* err = (unsigned*)(ws + w.err);
@@ -1257,7 +1263,6 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   }
   // bucketed: histogram -> transpose -> scan -> cursors -> scatter (1 or 2 levels)
   const int64_t n_counts = p.n_buckets * p.n_tiles;
-  const int64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
   unsigned* counts = (unsigned*)(ws + w.counts);
   if (cfg->n_rows == 0) {
     PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (n_counts + 1) * 4, st));
@@ -1278,19 +1283,8 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
                      dim3(kBlock), 0, st, counts_tm, p.n_tiles, p.n_buckets, counts);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_scan_chunks", st);
-  hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_scan_top", st);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kBlock), 0, st, chunk_sums, n_chunks);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_scan_apply", st);
-  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, counts, n_counts, chunk_sums,
-                     n_chunks);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
+  rc = scan_u32(counts, n_counts, chunk_sums, st);
+  if (rc != PDP_OK) return rc;
   unsigned* cursor = (unsigned*)(ws + w.cursor);
   unsigned* super_base = (unsigned*)(ws + w.super_base);
   const int64_t n_init = (p.n_buckets > p.n_supers + 1 ? p.n_buckets : p.n_supers + 1);
@@ -1340,8 +1334,9 @@ int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* 
   if (cfg->value_kind != PDP_VALUE_NONE && cfg->n_rows > 0 && value == nullptr)
     return set_error(PDP_E_INVALID, "value column is NULL");
   hipStream_t st = (hipStream_t)stream;
-  const KP kp = make_kp(cfg, p);
   char* ws = (char*)workspace;
+  if (pairs_mode(cfg)) return pairs_reduce(cfg, value, ws, *acc, st);
+  const KP kp = make_kp(cfg, p);
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH)
     return dispatch<GlobalReduce>(cfg->value_kind, cfg->linf == 0, kp, st, value, ws, w, *acc);
   if (cfg->n_rows == 0) return PDP_OK;

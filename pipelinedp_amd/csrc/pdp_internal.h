@@ -232,6 +232,49 @@ __device__ __forceinline__ PairSums pair_sums_from_rows(const unsigned long long
   return s;
 }
 
+// Adds row `row`'s contribution to the running per-pair sums f0 (clipped or,
+// with PDP_SUM_PER_PARTITION, raw sum; int64 bits with PDP_SUM_INT), f1
+// (normalized sum), f2 (normalized sum of squares) with device atomics — the
+// keep-every-row form of create_accumulator, finished by pair_sums_from_totals.
+template <int VALUE_KIND>
+__device__ __forceinline__ void accumulate_row(const void* value, uint32_t row, int64_t slot, double* f0,
+                                               double* f1, double* f2, const ClipParams& cp) {
+  if (VALUE_KIND == PDP_VALUE_NONE) return;
+  double v;
+  long long iv;
+  load_value<VALUE_KIND>(value, row, &v, &iv);
+  const int flags = cp.flags;
+  if (flags & PDP_SUM_PER_PARTITION) {
+    if (flags & PDP_SUM_INT) atomicAdd((unsigned long long*)(f0 + slot), (unsigned long long)iv);
+    else unsafeAtomicAdd(f0 + slot, v);
+  } else if (flags & PDP_ACC_SUM) {
+    if (flags & PDP_SUM_INT)
+      atomicAdd((unsigned long long*)(f0 + slot), (unsigned long long)clamp_ll(iv, (long long)cp.lo, (long long)cp.hi));
+    else unsafeAtomicAdd(f0 + slot, fmin(fmax(v, cp.lo), cp.hi));
+  }
+  if (flags & (PDP_ACC_NSUM | PDP_ACC_NSUM2)) {
+    const double c = fmin(fmax(v, cp.lo), cp.hi) - cp.mid;
+    if (flags & PDP_ACC_NSUM) unsafeAtomicAdd(f1 + slot, c);
+    if (flags & PDP_ACC_NSUM2) unsafeAtomicAdd(f2 + slot, c * c);
+  }
+}
+
+// pair accumulator of a keep-every-row pair from its summed slots
+__device__ __forceinline__ PairSums pair_sums_from_totals(long long cnt, double fsum_or_bits, double nsum,
+                                                          double nsum2, const ClipParams& cp) {
+  PairSums s{cnt, 0, 0.0, nsum, nsum2};
+  const long long ibits = __double_as_longlong(fsum_or_bits);
+  if (cp.flags & PDP_SUM_PER_PARTITION) {
+    if (cp.flags & PDP_SUM_INT) s.isum = clamp_ll(ibits, (long long)cp.min_sum, (long long)cp.max_sum);
+    else s.fsum = fmin(fmax(fsum_or_bits, cp.min_sum), cp.max_sum);
+  } else if (cp.flags & PDP_SUM_INT) {
+    s.isum = ibits;
+  } else {
+    s.fsum = fsum_or_bits;
+  }
+  return s;
+}
+
 // merge one pair's accumulator into the partition accumulators
 __device__ __forceinline__ void add_pair_to_partition(const pdp_partition_accumulators& acc, int64_t p,
                                                       const PairSums& s, int flags) {
@@ -244,6 +287,25 @@ __device__ __forceinline__ void add_pair_to_partition(const pdp_partition_accumu
   if (acc.normalized_sum && (flags & PDP_ACC_NSUM)) unsafeAtomicAdd(acc.normalized_sum + p, s.nsum);
   if (acc.normalized_sum_sq && (flags & PDP_ACC_NSUM2)) unsafeAtomicAdd(acc.normalized_sum_sq + p, s.nsum2);
 }
+
+// ------------------------------------------- host helpers across files --
+// Device-wide exclusive scan of v[0..n) in place, total -> v[n] (u32; every
+// caller's totals are < 2^32).  chunk_sums needs scan_chunk_sums_len(n) words.
+int64_t scan_chunk_sums_len(int64_t n);
+int scan_u32(unsigned* v, int64_t n, unsigned* chunk_sums, hipStream_t st);
+
+// Pair-table path (pdp_pairs.hip): LinfSampler / NoOpSampler (l0 == 0),
+// SamplingPerPrivacyIdContributionBounder (max_contributions > 0) and
+// contribution_bounds_already_enforced (rows_are_units).
+inline bool pairs_mode(const pdp_bound_config* c) {
+  return c->l0 == 0 || c->max_contributions > 0 || c->rows_are_units != 0;
+}
+int pairs_validate(const pdp_bound_config* c);
+uint64_t pairs_workspace_bytes(const pdp_bound_config* c);
+int pairs_bound(const pdp_bound_config* c, const int64_t* pid, const int64_t* pk, const void* value,
+                const uint8_t* allowed, char* ws, hipStream_t st);
+int pairs_reduce(const pdp_bound_config* c, const void* value, char* ws, const pdp_partition_accumulators& acc,
+                 hipStream_t st);
 
 }  // namespace pdp
 

@@ -22,8 +22,13 @@ from pipelinedp_amd import _native as N
 
 @dataclasses.dataclass
 class BoundingSpec:
-    """Columnar form of the bounder + combiner-accumulator parameters."""
-    l0: int
+    """Columnar form of the bounder + combiner-accumulator parameters.
+
+    l0 > 0: SamplingCross[AndPer]PartitionContributionBounder; l0 = 0:
+    LinfSampler (linf > 0) / NoOpSampler (linf = 0); max_contributions > 0:
+    SamplingPerPrivacyIdContributionBounder; rows_are_units:
+    contribution_bounds_already_enforced (no privacy ids)."""
+    l0: int                        # 0: no cross-partition sampling
     linf: int                      # 0: keep every row of a kept pair
     value_kind: int                # N.VALUE_*
     flags: int                     # N.ACC_* | N.SUM_*
@@ -32,6 +37,8 @@ class BoundingSpec:
     middle: float = 0.0
     min_sum: float = 0.0
     max_sum: float = 0.0
+    max_contributions: int = 0
+    rows_are_units: bool = False
 
     @property
     def sum_is_int(self) -> bool:
@@ -193,6 +200,8 @@ def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, se
     c.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     c.algorithm = int(algorithm)
     c.merge = int(merge)
+    c.max_contributions = int(bounding.max_contributions or 0)
+    c.rows_are_units = 1 if bounding.rows_are_units else 0
     return c
 
 
@@ -225,15 +234,18 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                      algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO):
     """Bounds contributions of one shard and ADDS its per-partition accumulators.
 
-    pid, pk: int64 device tensors of length n (dense keys); value: float64 or
-    int64 device tensor (or None for COUNT/PRIVACY_ID_COUNT only).
-    Returns the accumulator dict.
+    pid, pk: int64 device tensors of length n (dense keys; pid may be None
+    with bounding.rows_are_units); value: float64 or int64 device tensor (or
+    None for COUNT/PRIVACY_ID_COUNT only).  Returns the accumulator dict.
     """
     torch = _torch()
     lib = N.lib()
-    device = pid.device
-    n = int(pid.shape[0])
-    _check_col(pid, "privacy_id", (torch.int64,), n, device)
+    device = pk.device
+    n = int(pk.shape[0])
+    if pid is None and not bounding.rows_are_units:
+        raise ValueError("privacy_id is required unless contribution bounds are already enforced")
+    if pid is not None:
+        _check_col(pid, "privacy_id", (torch.int64,), n, device)
     _check_col(pk, "partition_key", (torch.int64,), n, device)
     if bounding.value_kind == N.VALUE_F64:
         _check_col(value, "value", (torch.float64,), n, device)
@@ -243,9 +255,12 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         value = None
     if allowed is not None:
         _check_col(allowed, "pk_allowed", (torch.uint8,), int(n_partitions), device)
-    if bounding.l0 < 1 or bounding.l0 > N.MAX_L0:
+    if bounding.l0 < 0 or bounding.l0 > N.MAX_L0:
         raise NotImplementedError(f"max_partitions_contributed={bounding.l0} is outside the "
                                   f"supported range [1, {N.MAX_L0}]")
+    if bounding.max_contributions < 0 or bounding.max_contributions > N.MAX_CONTRIBUTIONS:
+        raise NotImplementedError(f"max_contributions={bounding.max_contributions} is outside the "
+                                  f"supported range [1, {N.MAX_CONTRIBUTIONS}]")
     if bounding.linf < 0 or bounding.linf > N.MAX_LINF:
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")

@@ -29,16 +29,37 @@ def fixture_ids():
             if not p.endswith("sampling_inclusion.json")]
 
 
-def aggregate_params(case):
+def aggregate_params(case, module=pdp):
+    """AggregateParams of a fixture case (as oracle/gen_golden.py:case_params
+    built them for the reference); `module` is pipelinedp_amd or pipeline_dp."""
     kw = {}
     for k, name in (("min_value", "min_value"), ("max_value", "max_value"),
                     ("min_sum", "min_sum_per_partition"), ("max_sum", "max_sum_per_partition")):
         if k in case:
             kw[name] = case[k]
-    return pdp.AggregateParams(metrics=[getattr(pdp.Metrics, m) for m in case["metrics"]],
-                               noise_kind=getattr(pdp.NoiseKind, case["noise"]),
-                               max_partitions_contributed=case["l0"],
-                               max_contributions_per_partition=case["linf"], **kw)
+    bounder = bounder_of(case)
+    if bounder == "per_pid":
+        kw["max_contributions"] = case["max_contributions"]
+    else:
+        kw["max_partitions_contributed"] = case["l0"]
+        kw["max_contributions_per_partition"] = case["linf"]
+    if bounder in ("linf", "noop"):
+        kw["perform_cross_partition_contribution_bounding"] = False
+    if bounder == "enforced":
+        kw["contribution_bounds_already_enforced"] = True
+    return module.AggregateParams(metrics=[getattr(module.Metrics, m) for m in case["metrics"]],
+                                  noise_kind=getattr(module.NoiseKind, case["noise"]), **kw)
+
+
+def bounder_of(case):
+    """'default' (Cross+Per or Cross), 'linf', 'noop', 'per_pid' or 'enforced'."""
+    return case.get("bounder", "default")
+
+
+def extractors(case, module=pdp):
+    pid = None if bounder_of(case) == "enforced" else (lambda r: r[0])
+    return module.DataExtractors(privacy_id_extractor=pid, partition_extractor=lambda r: r[1],
+                                 value_extractor=lambda r: r[2])
 
 
 def combiner_kinds(case):

@@ -137,7 +137,8 @@ def test_workspace_bytes(lib):
 
 
 @pytest.mark.parametrize("field,value,code,msg", [
-    ("l0", 0, -4, b"l0"), ("l0", 257, -4, b"l0"), ("linf", -1, -4, b"linf"),
+    ("l0", -1, -4, b"l0"), ("l0", 257, -4, b"l0"), ("linf", -1, -4, b"linf"),
+    ("max_contributions", 257, -4, b"max_contributions"),
     ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
     ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
     ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"),
@@ -147,6 +148,32 @@ def test_invalid_configs_are_rejected(lib, field, value, code, msg):
     rc = lib.pdp_bound_plan(ctypes.byref(_cfg(**{field: value})), ctypes.byref(info))
     assert rc == code
     assert msg in lib.pdp_last_error()
+
+
+def test_pair_table_modes_plan(lib):
+    """l0 = 0 (LinfSampler / NoOpSampler), max_contributions and
+    rows_are_units resolve to the pair-table algorithm; their exclusions
+    mirror AggregateParams (aggregate_params.py:344-369)."""
+    info = N.BoundPlanInfo()
+    for kw in (dict(l0=0), dict(l0=0, linf=0), dict(l0=0, linf=0, max_contributions=5),
+               dict(l0=0, linf=0, rows_are_units=1)):
+        assert lib.pdp_bound_plan(ctypes.byref(_cfg(**kw)), ctypes.byref(info)) == 0, kw
+        assert info.algorithm == N.ALGO_PAIR_TABLE
+        ws = ctypes.c_uint64(0)
+        assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(**kw)), ctypes.byref(ws)) == 0
+        assert ws.value > 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=2, linf=0, max_contributions=5)), ctypes.byref(info)) == -1
+    assert b"max_contributions" in lib.pdp_last_error()
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=0, linf=1, rows_are_units=1)), ctypes.byref(info)) == -1
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=0, algorithm=N.ALGO_BUCKETED)), ctypes.byref(info)) == -4
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=2, algorithm=N.ALGO_PAIR_TABLE)), ctypes.byref(info)) == -4
+    # rows_are_units needs no privacy-id column
+    cfg = _cfg(n_rows=10, l0=0, linf=0, rows_are_units=1)
+    need = ctypes.c_uint64(0)
+    lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(need))
+    rc = lib.pdp_bound_contributions(ctypes.byref(cfg), None, None, None, None, ctypes.c_void_p(256),
+                                     need.value, None)
+    assert rc == -1 and b"key columns" in lib.pdp_last_error()
 
 
 def test_sum_int_needs_int_values(lib):

@@ -141,19 +141,62 @@ def test_post_aggregation_thresholding():
     assert run._selection().strategy == N.SELECT_LAPLACE_THRESHOLDING
 
 
-@pytest.mark.parametrize("kw,exc", [
-    (dict(max_contributions=3, max_partitions_contributed=None, max_contributions_per_partition=None),
-     NotImplementedError),
-    (dict(perform_cross_partition_contribution_bounding=False), NotImplementedError),
-    (dict(contribution_bounds_already_enforced=True), NotImplementedError),
-])
-def test_unsupported_bounding_modes_raise(kw, exc):
-    try:
-        sink, _, _ = _graph(_params(**kw))
-    except (ValueError, TypeError) as e:  # rejected by AggregateParams/DPEngine like the reference
-        pytest.skip(f"rejected at graph construction: {e}")
-    with pytest.raises(exc):
-        CB.recognise(sink)
+_MODES = {  # AggregateParams kwargs -> (plan.bounder, l0, linf, max_contributions, rows_are_units)
+    "linf": (dict(perform_cross_partition_contribution_bounding=False), ("linf", 0, 3, 0, False)),
+    "noop": (dict(metrics=[pdp.Metrics.SUM], min_value=None, max_value=None, min_sum_per_partition=-3.0,
+                  max_sum_per_partition=9.0, perform_cross_partition_contribution_bounding=False),
+             ("noop", 0, 0, 0, False)),
+    "per_privacy_id": (dict(max_contributions=3, max_partitions_contributed=None,
+                            max_contributions_per_partition=None), ("per_privacy_id", 0, 0, 3, False)),
+    "already_enforced": (dict(contribution_bounds_already_enforced=True),
+                         ("already_enforced", 0, 0, 0, True)),
+}
+
+
+@pytest.mark.parametrize("mode", sorted(_MODES))
+def test_bounding_modes_recognised(mode):
+    """Every bounder DPEngine can pick (dp_engine.py:380-400, and the
+    contribution_bounds_already_enforced branch :143-150) maps to one kernel
+    configuration (pdp_pairs.hip for all but Cross+Per / Cross)."""
+    kw, (bounder, l0, linf, maxc, units) = _MODES[mode]
+    public = [0, 1, 2, 3] if mode == "per_privacy_id" else None  # PyDP needs l0 for private selection
+    sink, _, _ = _graph(_params(**kw), public=public)
+    plan, run = _run_of(sink)
+    assert plan.bounder == bounder
+    spec = run._bounding_spec(N.VALUE_F64)
+    assert (spec.l0, spec.linf, spec.max_contributions, spec.rows_are_units) == (l0, linf, maxc, units)
+
+
+@pytest.mark.parametrize("mode", sorted(_MODES))
+def test_reference_dpengine_bounding_modes_recognised(mode):
+    """The reference's own DPEngine builds the same bounder stages."""
+    pipeline_dp = _import_reference()
+    kw, (bounder, l0, linf, maxc, units) = _MODES[mode]
+    base = dict(metrics=[pipeline_dp.Metrics.COUNT, pipeline_dp.Metrics.SUM],
+                noise_kind=pipeline_dp.NoiseKind.LAPLACE, max_partitions_contributed=2,
+                max_contributions_per_partition=3, min_value=0.0, max_value=10.0)
+    for k, v in kw.items():
+        base[k] = [getattr(pipeline_dp.Metrics, m.name) for m in v] if k == "metrics" else v
+    params = pipeline_dp.AggregateParams(**base)
+    acc = pipeline_dp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+    engine = pipeline_dp.DPEngine(acc, CB.ColumnarBackend())
+    pid = None if units else (lambda r: r[0])
+    ext = pipeline_dp.DataExtractors(privacy_id_extractor=pid, partition_extractor=lambda r: r[1],
+                                     value_extractor=lambda r: r[2])
+    public = [0, 1, 2, 3] if mode == "per_privacy_id" else None
+    sink = engine.aggregate(ROWS, params, ext, public_partitions=public)
+    acc.compute_budgets()
+    plan, run = _run_of(sink)
+    assert plan.bounder == bounder
+    spec = run._bounding_spec(N.VALUE_F64)
+    assert (spec.l0, spec.linf, spec.max_contributions, spec.rows_are_units) == (l0, linf, maxc, units)
+
+
+def test_unrecognised_graph_raises():
+    backend = CB.ColumnarBackend()
+    col = backend.map([1, 2, 3], lambda x: x, "some other pipeline")
+    with pytest.raises(NotImplementedError):
+        CB.recognise(col)
 
 
 @pytest.mark.parametrize("kw", [

@@ -48,9 +48,8 @@ def test_backend_accumulators_match_reference_golden(device, fx):
     backend = CB.ColumnarBackend(device=device, seed=5)
     acc = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
     engine = pdp.DPEngine(acc, backend)
-    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
-                             value_extractor=lambda r: r[2])
-    sink = engine.aggregate(rows, G.aggregate_params(case), ext, public_partitions=case.get("public"))
+    sink = engine.aggregate(rows, G.aggregate_params(case), G.extractors(case),
+                            public_partitions=case.get("public"))
     acc.compute_budgets()
     got = backend.accumulators(sink)
     want = G.expected_map(fx)

@@ -1,0 +1,157 @@
+"""GPU parity of the pair-table bounders (csrc/pdp_pairs.hip) against the CPU
+oracle: LinfSampler and NoOpSampler (perform_cross_partition_contribution_
+bounding=False), SamplingPerPrivacyIdContributionBounder (max_contributions)
+and contribution_bounds_already_enforced (rows_are_units).
+
+Counts, privacy-id counts and int sums are bit-exact (the sampled rows are the
+oracle's: same counter-based row priorities); fp64 sums within 1e-9 of the
+per-partition sum of |terms| (atomic summation order differs).
+"""
+import numpy as np
+import pytest
+
+from oracle import columnar as O
+from tests.test_gpu_kernels import _abs_scale, _compare
+
+pytestmark = pytest.mark.gpu
+
+# (l0, linf, max_contributions, rows_are_units, value_kind, flags)
+MODES = {
+    "linf_f64_mean": (0, 2, 0, False, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
+    "linf1_var": (0, 1, 0, False, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2),
+    "linf_int_sum": (0, 3, 0, False, O.VALUE_I64, O.ACC_SUM | O.SUM_INT),
+    "noop_sum_per_partition": (0, 0, 0, False, O.VALUE_F64, O.SUM_PER_PARTITION),
+    "noop_int_per_partition": (0, 0, 0, False, O.VALUE_I64, O.SUM_PER_PARTITION | O.SUM_INT),
+    "noop_count_only": (0, 0, 0, False, O.VALUE_NONE, 0),
+    "max_contrib_5": (0, 0, 5, False, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
+    "max_contrib_1_int": (0, 0, 1, False, O.VALUE_I64, O.ACC_SUM | O.SUM_INT),
+    "max_contrib_40": (0, 0, 40, False, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2),
+    "units_f64": (0, 0, 0, True, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
+    "units_per_partition": (0, 0, 0, True, O.VALUE_I64, O.SUM_PER_PARTITION | O.SUM_INT),
+}
+
+
+def _spec(mode):
+    from pipelinedp_amd import executor as X
+    l0, linf, maxc, units, vk, flags = MODES[mode]
+    return X.BoundingSpec(l0=l0, linf=linf, value_kind=vk, flags=flags, min_value=0.0, max_value=10.0,
+                          middle=5.0, min_sum=-4.0, max_sum=30.0, max_contributions=maxc, rows_are_units=units)
+
+
+def _data(seed, n, U, P, vk, heavy):
+    rng = np.random.default_rng(seed)
+    pid = rng.integers(0, U, n, dtype=np.int64)
+    pk = rng.integers(0, P, n, dtype=np.int64)
+    if heavy:  # a few privacy ids with many rows, some pairs with many rows
+        h = rng.random(n) < 0.2
+        pid[h] = rng.integers(0, 5, h.sum())
+        pk[h] = rng.integers(0, 4, h.sum())
+    if vk == O.VALUE_F64:
+        val = rng.normal(5.0, 4.0, n)
+    elif vk == O.VALUE_I64:
+        val = rng.integers(-3, 12, n, dtype=np.int64)
+    else:
+        val = None
+    return pid, pk, val
+
+
+def _gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+    import torch
+    from pipelinedp_amd import executor as X
+    tp = None if spec.rows_are_units else torch.as_tensor(pid).to(device)
+    tk = torch.as_tensor(pk).to(device)
+    tv = None if val is None else torch.as_tensor(val).to(device)
+    ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
+    acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
+                             allowed=ta, row_offset=row_offset)
+    torch.cuda.synchronize()
+    return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+
+
+def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+    return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0, linf=spec.linf,
+                              value_kind=spec.value_kind, flags=spec.flags, min_value=spec.min_value,
+                              max_value=spec.max_value, middle=spec.middle, min_sum=spec.min_sum,
+                              max_sum=spec.max_sum, seed=seed, row_offset=row_offset, allowed=allowed,
+                              max_contributions=spec.max_contributions, rows_are_units=spec.rows_are_units)
+
+
+@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_pair_table_matches_oracle(device, mode, heavy):
+    spec = _spec(mode)
+    n, U, P = 60_000, 3_000, 700
+    pid, pk, val = _data(11, n, U, P, spec.value_kind, heavy)
+    got = _gpu(device, pid, pk, val, U, P, spec, seed=1234)
+    want = _oracle(pid, pk, val, U, P, spec, seed=1234)
+    _compare(got, want, _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle) + 40.0)
+    if heavy and (spec.max_contributions or spec.linf):
+        # sampling really fired on this data
+        full = _oracle(pid, pk, val, U, P, _spec("noop_count_only"), seed=1234)
+        assert got["count"].sum() < full["count"].sum()
+
+
+@pytest.mark.parametrize("mode", ["linf_f64_mean", "max_contrib_5", "units_f64"])
+def test_pair_table_public_filter_and_row_offset(device, mode):
+    """Rows of non-public partitions are dropped before sampling; priorities
+    are keyed by the global row index, so a shard at row_offset r reproduces
+    the oracle run at r."""
+    spec = _spec(mode)
+    n, U, P = 20_000, 500, 300
+    pid, pk, val = _data(5, n, U, P, spec.value_kind, heavy=True)
+    allowed = np.random.default_rng(3).random(P) < 0.5
+    got = _gpu(device, pid, pk, val, U, P, spec, seed=77, allowed=allowed, row_offset=123_456)
+    want = _oracle(pid, pk, val, U, P, spec, seed=77, allowed=allowed, row_offset=123_456)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 10.0, 5.0) + 40.0)
+    assert got["privacy_id_count"][~allowed].sum() == 0
+
+
+@pytest.mark.parametrize("mode", ["linf_f64_mean", "max_contrib_5", "units_f64"])
+def test_pair_table_out_of_range_keys_raise(device, mode):
+    spec = _spec(mode)
+    pid, pk, val = _data(2, 1000, 50, 40, spec.value_kind, heavy=False)
+    pk[17] = 40
+    with pytest.raises(ValueError):
+        _gpu(device, pid, pk, val, 50, 40, spec, seed=1)
+
+
+@pytest.mark.parametrize("mode", ["linf_f64_mean", "max_contrib_5", "noop_count_only", "units_f64"])
+def test_pair_table_empty_input(device, mode):
+    spec = _spec(mode)
+    pid, pk, val = _data(2, 0, 50, 40, spec.value_kind, heavy=False)
+    got = _gpu(device, pid, pk, val, 50, 40, spec, seed=1)
+    assert got["privacy_id_count"].sum() == 0 and got["count"].sum() == 0
+
+
+def test_max_contributions_sampling_is_uniform(device):
+    """One privacy id with 6 rows, keep 2: over many seeds every row is kept
+    equally often (the reference's np.random.choice distribution)."""
+    from scipy.stats import chisquare
+    import torch
+    from pipelinedp_amd import executor as X
+    spec = X.BoundingSpec(l0=0, linf=0, value_kind=O.VALUE_NONE, flags=0, max_contributions=2)
+    pid = torch.zeros(6, dtype=torch.int64, device=device)
+    pk = torch.arange(6, dtype=torch.int64, device=device)
+    counts = np.zeros(6)
+    for s in range(3000):
+        acc = X.bound_and_reduce(pid, pk, None, n_privacy_ids=1, n_partitions=6, bounding=spec, seed=s)
+        counts += acc["count"].cpu().numpy()
+    assert counts.sum() == 2 * 3000
+    assert chisquare(counts).pvalue > 1e-4
+
+
+def test_pair_table_at_scale_count_identity(device):
+    """4M rows, NoOp: privacy_id_count sums to the number of distinct pairs and
+    count to the number of rows (size-independent property)."""
+    import torch
+    from pipelinedp_amd import executor as X
+    n, U, P = 4_000_000, 200_000, 50_000
+    g = torch.Generator(device=device)
+    g.manual_seed(9)
+    pid = torch.randint(0, U, (n,), generator=g, device=device)
+    pk = torch.randint(0, P, (n,), generator=g, device=device)
+    spec = X.BoundingSpec(l0=0, linf=0, value_kind=O.VALUE_NONE, flags=0)
+    acc = X.bound_and_reduce(pid, pk, None, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=3)
+    distinct = torch.unique(pid * P + pk).numel()
+    assert int(acc["privacy_id_count"].sum()) == distinct
+    assert int(acc["count"].sum()) == n
