@@ -202,9 +202,37 @@ def sampling_fixture(pdp, trials=4000):
             "l0": {"partitions": 6, "n": 2, "counts": l0_counts}}
 
 
+def select_partitions_fixture(pdp, seed=300):
+    """DPEngine.select_partitions on LocalBackend: every pid has <= L0 distinct
+    partitions (no sampling fires); eps = 1e4, delta = 1e-12 makes truncated-
+    geometric selection keep every partition with >= 2 privacy ids and drop
+    those with 1 (keep probabilities 1 - O(e^-1e4) and delta' = O(1e-12))."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for u in range(400):
+        for k in rng.choice(120, size=int(rng.integers(1, 4)), replace=False):
+            rows.extend([[u, f"p{int(k)}"]] * int(rng.integers(1, 3)))
+    params = pdp.SelectPartitionsParams(max_partitions_contributed=3)
+    accountant = pdp.NaiveBudgetAccountant(total_epsilon=1e4, total_delta=1e-12)
+    engine = pdp.DPEngine(accountant, pdp.LocalBackend())
+    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1])
+    out = engine.select_partitions(rows, params, ext)
+    accountant.compute_budgets()
+    keys = sorted(out)
+    pids = {}
+    for u, k in rows:
+        pids.setdefault(k, set()).add(u)
+    assert keys == sorted(k for k, s in pids.items() if len(s) >= 2)
+    return {"name": "select_partitions", "rows": rows, "max_partitions_contributed": 3,
+            "eps": 1e4, "delta": 1e-12, "expected_keys": keys}
+
+
 def main():
     pdp = _import_reference()
     os.makedirs(OUT, exist_ok=True)
+    with open(os.path.join(OUT, "select_partitions.json"), "w") as f:
+        json.dump(select_partitions_fixture(pdp), f)
+    print("select_partitions written")
     for i, case in enumerate(CASES):
         fx = run_case(pdp, case, seed=100 + i)
         with open(os.path.join(OUT, f"{case['name']}.json"), "w") as f:

@@ -118,11 +118,14 @@ class ColumnTable:
 
 def probe_columns(extract_fn, table: ColumnTable):
     """Resolves DPEngine's extraction function to (pid, pk, value) column
-    specs: ColumnRef, a constant, or None; returns None when it cannot."""
+    specs: ColumnRef, a constant, or None; returns None when it cannot.
+    select_partitions extracts (pid, pk) only (dp_engine.py:241-244): value None."""
     try:
         out = extract_fn(_ProbeRow())
     except Exception:
         return None
+    if isinstance(out, tuple) and len(out) == 2:
+        out = out + (None,)
     if not isinstance(out, tuple) or len(out) != 3:
         return None
     specs = []

@@ -49,6 +49,12 @@ ST_THRESHOLD_DROP = "Drop partitions under threshold"                # dp_engine
 ST_PUBLIC_JOIN = "Join public partitions with partitions from data"  # dp_engine.py:311-313
 ST_PUBLIC_TO_COL = "Public partitions to collection"                 # dp_engine.py:305-306
 ST_EMPTY_ACCS = "Build empty accumulators"                           # dp_engine.py:307-309
+# DPEngine.select_partitions (dp_engine.py:235-288)
+ST_SP_EXTRACT = "Extract (privacy_id, partition_key))"               # :241-244
+ST_SP_COMBINE = "Combine accumulators per partition key"             # :276-277
+ST_SP_KEYS = "Drop accumulators, keep only partition keys"           # :286-287
+SELECT_PARTITIONS = {"Group by privacy_id", "Sample cross-partition contributions",
+                     "Drop privacy id and add accumulator"}                          # :248-273
 
 # bounder stage sets (contribution_bounders.py)
 CROSS_AND_PER = {"Rekey to ( (privacy_id, partition_key), value))",
@@ -119,6 +125,7 @@ class AggregatePlan:
         self.threshold_drop = False
         self.params = None
         self.budget = None
+        self.keys_only = False           # DPEngine.select_partitions: yield partition keys
 
 
 def _chain(sink):
@@ -134,6 +141,8 @@ def _chain(sink):
 def recognise(sink) -> AggregatePlan:
     """Maps a recorded chain to an AggregatePlan; NotImplementedError otherwise."""
     nodes, source = _chain(sink)
+    if any(n.op == "map" and n.stage == ST_SP_EXTRACT for n in nodes):
+        return _recognise_select_partitions(nodes, source)
     plan = AggregatePlan()
     plan.source = source
     stages = set()
@@ -191,6 +200,37 @@ def recognise(sink) -> AggregatePlan:
         raise NotImplementedError("incomplete DPEngine.aggregate graph")
     if plan.params is None:
         raise NotImplementedError("DPEngine.aggregate graph without annotate(params=...)")
+    return plan
+
+
+def _recognise_select_partitions(nodes, source) -> AggregatePlan:
+    """DPEngine.select_partitions = Cross-partition bounding (L0 only) +
+    privacy-id count per partition + private selection, keys out."""
+    plan = AggregatePlan()
+    plan.source = source
+    plan.bounder = "cross"
+    plan.keys_only = True
+    plan.compute_metrics = True
+    stages = set()
+    for node in nodes:
+        st = node.stage
+        if node.op == "map" and st == ST_SP_EXTRACT:
+            plan.extract_fn = node.fn
+        elif node.op == "combine_accumulators_per_key" and st == ST_SP_COMBINE:
+            plan.combiner = node.arg
+        elif node.op == "filter" and st == ST_SELECT:
+            plan.selection = node.fn
+        elif node.op == "keys" and st == ST_SP_KEYS:
+            pass
+        elif node.op == "annotate":
+            plan.params = node.kwargs.get("params")
+            plan.budget = node.kwargs.get("budget")
+        else:
+            stages.add(st)
+    if stages != SELECT_PARTITIONS or plan.combiner is None or plan.selection is None:
+        raise NotImplementedError(f"unrecognised select_partitions stages: {sorted(stages)}")
+    if plan.params is None:
+        raise NotImplementedError("select_partitions graph without annotate(params=...)")
     return plan
 
 
@@ -573,6 +613,8 @@ class AggregateRun:
                                                 seed_noise=seed_noise, public_mask=public_mask,
                                                 partition_offset=first)
         idx = index.cpu().numpy()
+        if self.plan.keys_only:  # select_partitions: "Drop accumulators, keep only partition keys"
+            return [pk_enc.key_of(first + p) for p in idx.tolist()]
         vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((len(self.prog.fields), 0))
         nt = pdc._get_or_create_named_tuple("MetricsTuple", tuple(self.prog.fields))
         result = []

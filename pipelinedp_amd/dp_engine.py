@@ -116,6 +116,53 @@ class DPEngine:
             col = self._drop_partitions_under_threshold(col)
         return col
 
+    # ---------------------------------------------- select_partitions --
+    def select_partitions(self, col, params: agg.SelectPartitionsParams, data_extractors: de.DataExtractors):
+        """DP set of partition keys (reference dp_engine.py:212-233): per
+        privacy id a uniform sample of <= max_partitions_contributed distinct
+        partitions, privacy-id count per partition, private selection."""
+        self._check_select_private_partitions(col, params, data_extractors)
+        self._check_budget_accountant_compatibility(False, [], False)
+        with self._budget_accountant.scope(weight=params.budget_weight):
+            self._add_report_generator(params, "select_partitions")
+            col = self._select_partitions(col, params, data_extractors)
+            budget = self._budget_accountant._compute_budget_for_aggregation(params.budget_weight)
+            return self._annotate(col, params=params, budget=budget)
+
+    def _select_partitions(self, col, params: agg.SelectPartitionsParams, data_extractors: de.DataExtractors):
+        """Stage chain of dp_engine.py:235-288 (ColumnarBackend runs it on the GPU)."""
+        l0 = params.max_partitions_contributed
+        backend = self._backend
+        col = backend.map(col, lambda row: (data_extractors.privacy_id_extractor(row),
+                                            data_extractors.partition_extractor(row)),
+                          "Extract (privacy_id, partition_key))")
+        col = backend.group_by_key(col, "Group by privacy_id")
+
+        def sample_unique(pid_and_pks):
+            pid, pks = pid_and_pks
+            sampled = contribution_bounders.choose_from_list_without_replacement(list(set(pks)), l0)
+            return ((pid, pk) for pk in sampled)
+
+        col = backend.flat_map(col, sample_unique, "Sample cross-partition contributions")
+        compound = combiners.CompoundCombiner([], return_named_tuple=False)
+        col = backend.map_tuple(col, lambda pid, pk: (pk, compound.create_accumulator([])),
+                                "Drop privacy id and add accumulator")
+        col = backend.combine_accumulators_per_key(col, compound, "Combine accumulators per partition key")
+        col = self._select_private_partitions_internal(col, l0, 1, params.partition_selection_strategy,
+                                                       params.pre_threshold)
+        return backend.keys(col, "Drop accumulators, keep only partition keys")
+
+    def _check_select_private_partitions(self, col, params, data_extractors):
+        """dp_engine.py:189-210."""
+        _require_col(col)
+        if params is None:
+            raise ValueError("params must be set to a valid SelectPrivatePartitionsParams")
+        if not isinstance(params, agg.SelectPartitionsParams):
+            raise TypeError("params must be set to a valid SelectPrivatePartitionsParams")
+        if not isinstance(params.max_partitions_contributed, int) or params.max_partitions_contributed <= 0:
+            raise ValueError("params.max_partitions_contributed must be set (to a positive integer)")
+        _require_extractors(data_extractors)
+
     def _extract_columns(self, col, data_extractors: de.DataExtractors):
         pid_fn = data_extractors.privacy_id_extractor or (lambda row: None)
         pk_fn = data_extractors.partition_extractor

@@ -17,7 +17,7 @@ REL_TOL = 1e-9  # fp64 sums: north-star tolerance (order of summation differs)
 def fixtures():
     out = []
     for path in sorted(glob.glob(os.path.join(GOLDEN, "*.json"))):
-        if path.endswith("sampling_inclusion.json"):
+        if path.endswith(("sampling_inclusion.json", "select_partitions.json")):
             continue
         with open(path) as f:
             out.append(json.load(f))
@@ -26,7 +26,7 @@ def fixtures():
 
 def fixture_ids():
     return [os.path.basename(p)[:-5] for p in sorted(glob.glob(os.path.join(GOLDEN, "*.json")))
-            if not p.endswith("sampling_inclusion.json")]
+            if not p.endswith(("sampling_inclusion.json", "select_partitions.json"))]
 
 
 def aggregate_params(case, module=pdp):

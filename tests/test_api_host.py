@@ -320,3 +320,38 @@ def test_reference_dpengine_variants_recognised(case):
     rs, os_ = ref_run._selection(), our_run._selection()
     assert (rs.strategy, rs.pre_threshold, rs.threshold, rs.noise_scale) == \
         (os_.strategy, os_.pre_threshold, os_.threshold, os_.noise_scale)
+
+
+@pytest.mark.parametrize("engine_name", ["mirror", "reference"])
+def test_select_partitions_recognised(engine_name):
+    """DPEngine.select_partitions (dp_engine.py:212-288) maps to the Cross
+    bounder (L0 sampling, no values) + private selection, keys out."""
+    mod = pdp if engine_name == "mirror" else _import_reference()
+    acc = mod.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+    engine = mod.DPEngine(acc, CB.ColumnarBackend())
+    ext = mod.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1])
+    params = mod.SelectPartitionsParams(
+        max_partitions_contributed=4,
+        partition_selection_strategy=mod.PartitionSelectionStrategy.LAPLACE_THRESHOLDING, pre_threshold=2)
+    sink = engine.select_partitions(ROWS, params, ext)
+    acc.compute_budgets()
+    plan, run = _run_of(sink)
+    assert plan.keys_only and plan.bounder == "cross"
+    spec = run._bounding_spec(N.VALUE_NONE)
+    assert (spec.l0, spec.linf, spec.flags) == (4, 0, 0)
+    assert run.prog.ops == [] and not run.prog.needs_values
+    sel = run._selection()
+    assert sel.strategy == N.SELECT_LAPLACE_THRESHOLDING and sel.pre_threshold == 2
+    # the whole budget goes to selection: b = l0 / eps
+    assert math.isclose(sel.noise_scale, 4.0, rel_tol=1e-12)
+
+
+def test_select_partitions_validation_like_reference():
+    engine = pdp.DPEngine(pdp.NaiveBudgetAccountant(1.0, 1e-6), CB.ColumnarBackend())
+    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1])
+    with pytest.raises(ValueError):
+        engine.select_partitions(ROWS, pdp.SelectPartitionsParams(max_partitions_contributed=0), ext)
+    with pytest.raises(TypeError):
+        engine.select_partitions(ROWS, _params(), ext)
+    with pytest.raises(ValueError):
+        engine.select_partitions([], pdp.SelectPartitionsParams(max_partitions_contributed=1), ext)

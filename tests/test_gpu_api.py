@@ -217,3 +217,52 @@ def test_two_ranks_match_single_process(device):
     assert set(merged) == set(single)
     for k in single:
         np.testing.assert_allclose(merged[k], single[k], rtol=1e-9, atol=1e-6)
+
+
+def test_select_partitions_matches_reference_golden(device):
+    """DPEngine.select_partitions on ColumnarBackend returns the reference's
+    kept keys (tests/golden/select_partitions.json, eps = 1e4)."""
+    import json
+    with open(os.path.join(G.GOLDEN, "select_partitions.json")) as f:
+        fx = json.load(f)
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=fx["eps"], total_delta=fx["delta"])
+    engine = pdp.DPEngine(acc, CB.ColumnarBackend(device=device, seed=11))
+    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1])
+    sink = engine.select_partitions([tuple(r) for r in fx["rows"]],
+                                    pdp.SelectPartitionsParams(max_partitions_contributed=3), ext)
+    acc.compute_budgets()
+    assert sorted(sink) == fx["expected_keys"]
+
+
+@pytest.mark.parametrize("strategy", [pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC,
+                                      pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING])
+def test_select_partitions_matches_oracle_with_sampling(device, strategy):
+    """200k rows where L0 sampling fires: the kept keys equal the oracle's
+    (same pair priorities, same Philox selection stream)."""
+    from oracle import columnar as O
+    rng = np.random.default_rng(4)
+    n, U, P = 200_000, 5_000, 3_000
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.2, n) - 1, P - 1)
+    table = pdp.ColumnTable({"pid": pid, "pk": pk}, n_privacy_ids=U, n_partitions=P)
+    backend = CB.ColumnarBackend(device=device, seed=21)
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=2.0, total_delta=1e-5)
+    engine = pdp.DPEngine(acc, backend)
+    ext = pdp.DataExtractors(privacy_id_extractor=pdp.ColumnExtractor("pid"),
+                             partition_extractor=pdp.ColumnExtractor("pk"))
+    sink = engine.select_partitions(table, pdp.SelectPartitionsParams(
+        max_partitions_contributed=3, partition_selection_strategy=strategy), ext)
+    acc.compute_budgets()
+    got = sorted(sink)
+    run = CB.AggregateRun(backend, CB.recognise(sink))
+    seed_bound, seed_select, _ = run._seeds
+    sel = run._selection()
+    spec = run._bounding_spec(N.VALUE_NONE)
+    oacc = O.bound_and_reduce(pid, pk, None, n_privacy_ids=U, n_partitions=P, l0=3, linf=0,
+                              value_kind=O.VALUE_NONE, flags=0, seed=seed_bound,
+                              rand_shift=__import__("pipelinedp_amd.executor", fromlist=["x"]).bound_plan(
+                                  n, U, P, spec).rand_shift)
+    keep, _ = O.select(oacc["privacy_id_count"], sel.strategy, keep_prob=sel.keep_prob,
+                       noise_scale=sel.noise_scale, threshold=sel.threshold, seed=seed_select)
+    assert got == np.flatnonzero(keep).tolist()
+    assert 0 < len(got) < P
