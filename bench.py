@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--rows", type=int, default=ROWS_PER_GPU, help="rows per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
+    ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto, 1 wide, 2 compact)")
     return ap.parse_args()
 
 
@@ -139,7 +140,7 @@ def main():
 
     P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
-    plan = X.bound_plan(n, U, P_pad, bounding)
+    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format)
     acc = X.new_accumulators(P_pad, bounding, device)
     seed_base = parallel.broadcast_seeds((int.from_bytes(os.urandom(8), "little"),))[0]
 
@@ -149,7 +150,7 @@ def main():
                 t.zero_()
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
-                           check_keys=False)
+                           check_keys=False, key_format=args.key_format)
         mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
@@ -231,7 +232,8 @@ def main():
         },
         "kernel_ms": kernel_ms,
         "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
-                       "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes},
+                       "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
+                       "key_format": {1: "wide", 2: "compact"}.get(plan.key_format, plan.key_format)},
         "partitions_kept": kept,
         "cpu_baseline": None,
     }

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 3
+#define PDP_ABI_VERSION 4
 
 /* error codes */
 #define PDP_OK 0
@@ -71,6 +71,8 @@ typedef struct pdp_bound_config {
                                 (1..PDP_MAX_CONTRIBUTIONS); needs l0 = linf = 0 */
   int32_t rows_are_units;    /* != 0: contribution_bounds_already_enforced — every row is
                                 its own accumulator; privacy_id may be NULL */
+  int32_t key_format;        /* PDP_KEYS_*: row record format of the BUCKETED partition passes */
+  int32_t reserved;
 } pdp_bound_config;
 
 #define PDP_MAX_L0 256
@@ -84,6 +86,12 @@ typedef struct pdp_bound_config {
 #define PDP_ALGO_PAIR_TABLE 3    /* device hash table of (pid, pk) pairs: the bounders
                                     without cross-partition sampling (l0 = 0,
                                     max_contributions, rows_are_units); chosen by AUTO */
+
+/* row records moved by the BUCKETED partition passes (identical results) */
+#define PDP_KEYS_AUTO 0
+#define PDP_KEYS_WIDE 1    /* u64 pair key + u32 row: 12 B per row and pass */
+#define PDP_KEYS_COMPACT 2 /* u32 (bucket-local pid, partition) + u32 row: 8 B per row and pass;
+                              needs super/bucket/partition bits <= 31 (AUTO picks it then) */
 
 /* per-partition merge of the kept pairs (BUCKETED; identical sums up to fp
  * summation order) */
@@ -102,6 +110,8 @@ typedef struct pdp_bound_plan_info {
   int32_t merge;       /* resolved PDP_MERGE_* (0 for GLOBAL_SKETCH) */
   int32_t n_ranges;    /* PDP_MERGE_RANGES: partition ranges of 2^11 keys */
   int64_t range_group; /* PDP_MERGE_RANGES: buckets per range-reduce workgroup */
+  int32_t key_format;  /* resolved PDP_KEYS_* (BUCKETED) */
+  int32_t reserved;
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */

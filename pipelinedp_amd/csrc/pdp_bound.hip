@@ -29,6 +29,8 @@
 //  GLOBAL (fallback for large l0 * linf)
 //    k_pair_sketch / k_pair_rows / k_reduce_pairs: the same sketches in HBM,
 //    updated with device-scope atomics.
+#include <type_traits>
+
 #include "pdp_internal.h"
 
 namespace pdp {
@@ -49,6 +51,13 @@ constexpr int kRangeThreads = 256;
 constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
+// 16-byte key loads in flight per lane in the bucket kernel's B1 / B2 passes
+#ifndef PDP_B1_KU_COMPACT
+#define PDP_B1_KU_COMPACT 4
+#endif
+#ifndef PDP_B2_KU_COMPACT
+#define PDP_B2_KU_COMPACT 2
+#endif
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
@@ -66,6 +75,7 @@ struct Plan {
   int n_ranges;         // PDP_MERGE_RANGES: ceil(P / 2^kRangeBits)
   int64_t range_group;  // buckets per range-reduce workgroup
   int64_t n_groups;
+  int key_format;       // PDP_KEYS_WIDE / PDP_KEYS_COMPACT (bucketed)
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -114,8 +124,17 @@ Plan make_plan(const pdp_bound_config* c) {
     // per-bucket range histogram + cursors + block-scan scratch after the sketches
     p.lds_bytes += (2 * (int64_t)p.n_ranges + kBucketThreads / 64 + 1) * 4;
   }
-  if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave
+  // row records of the partition passes: u32 (sub-bucket, local pid,
+  // partition) with bit 31 = dead when those fields fit, else the u64 pair key
+  const bool compact_ok = p.super_bits + p.bucket_bits + p.pk_bits <= 31;
+  p.key_format = 0;
+  if (p.algorithm == PDP_ALGO_BUCKETED) {
+    if (c->key_format == PDP_KEYS_COMPACT && !compact_ok) p.algorithm = -1;  // infeasible
+    p.key_format = (c->key_format == PDP_KEYS_WIDE || !compact_ok) ? PDP_KEYS_WIDE : PDP_KEYS_COMPACT;
+  }
+  if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave [+ pid hashes]
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
+    if (p.key_format == PDP_KEYS_COMPACT) p.lds_bytes += ((int64_t)4 << p.bucket_bits);
   }
   if (p.merge == PDP_MERGE_RANGES) {
     int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
@@ -166,10 +185,11 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     w.cursor = off; off = align256(off + (uint64_t)p.n_buckets * 4);
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
-    w.keys1 = off; off = align256(off + n * 8);
+    const uint64_t kb = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;
+    w.keys1 = off; off = align256(off + n * kb);
     w.rows1 = off; off = align256(off + n * 4);
     if (p.super_bits > 0) {
-      w.keys2 = off; off = align256(off + n * 8);
+      w.keys2 = off; off = align256(off + n * kb);
       w.rows2 = off; off = align256(off + n * 4);
     } else {
       w.keys2 = w.keys1;
@@ -208,11 +228,13 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad algorithm");
   if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
     return set_error(PDP_E_INVALID, "bad merge");
+  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_COMPACT)
+    return set_error(PDP_E_INVALID, "bad key_format");
   if (pairs_mode(c)) return pairs_validate(c);
   if (c->algorithm == PDP_ALGO_PAIR_TABLE)
     return set_error(PDP_E_UNSUPPORTED, "PDP_ALGO_PAIR_TABLE runs only the bounders without L0 sampling");
   if (make_plan(c).algorithm < 0)
-    return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge infeasible for this l0/linf/P");
+    return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge / compact keys infeasible for this l0/linf/U/P");
   return PDP_OK;
 }
 
@@ -417,17 +439,24 @@ constexpr int kStageItems = 8;
 constexpr int kStageRows = kPartThreads * kStageItems;  // 4096
 constexpr int kMaxDest = 1024;
 
+// row record key of the partition passes: u64 pair key (PDP_KEYS_WIDE) or u32
+// compact record (PDP_KEYS_COMPACT)
+template <bool COMPACT>
+using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>::type;
+
+template <typename K>
 struct StageLds {
   unsigned hist[kMaxDest];
   unsigned start[kMaxDest];
   unsigned gcur[kMaxDest];
-  unsigned long long keys[kStageRows];
+  K keys[kStageRows];
   unsigned rows[kStageRows];
   unsigned short dest[kStageRows];
 };
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
-__device__ __forceinline__ void stage_count(StageLds& s, int ndest, const int (&d)[kStageItems],
+template <typename K>
+__device__ __forceinline__ void stage_count(StageLds<K>& s, int ndest, const int (&d)[kStageItems],
                                             unsigned (&rank)[kStageItems]) {
   for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
   __syncthreads();
@@ -452,11 +481,10 @@ __device__ __forceinline__ void stage_count(StageLds& s, int ndest, const int (&
 }
 
 // phase 2: place into the LDS stage, then write every run at gcur[dest]
-__device__ __forceinline__ void stage_write(StageLds& s, int ndest, const int (&d)[kStageItems],
-                                            const unsigned (&rank)[kStageItems],
-                                            const unsigned long long (&x)[kStageItems],
-                                            const unsigned (&r)[kStageItems],
-                                            unsigned long long* __restrict__ out_keys,
+template <typename K>
+__device__ __forceinline__ void stage_write(StageLds<K>& s, int ndest, const int (&d)[kStageItems],
+                                            const unsigned (&rank)[kStageItems], const K (&x)[kStageItems],
+                                            const unsigned (&r)[kStageItems], K* __restrict__ out_keys,
                                             unsigned* __restrict__ out_rows) {
 #pragma unroll
   for (int q = 0; q < kStageItems; ++q) {
@@ -477,16 +505,36 @@ __device__ __forceinline__ void stage_write(StageLds& s, int ndest, const int (&
   __syncthreads();
 }
 
+// Compact row record: bit 31 = dead (non-public / invalid partition: skipped,
+// but kept in its bucket), bits [pk_bits, pk_bits + bucket_bits + super_bits)
+// = the pid's bucket-within-super and bucket-local bits, [0, pk_bits) = pk.
+__device__ __forceinline__ uint32_t compact_key(const KP& kp, int64_t u, int64_t k, bool dead) {
+  const uint32_t mid = (uint32_t)((uint64_t)u & ((1ULL << (kp.bucket_bits + kp.super_bits)) - 1));
+  return dead ? (0x80000000u | (mid << kp.pk_bits)) : ((mid << kp.pk_bits) | (uint32_t)k);
+}
+
+// The pair key of a compact record: bit-identical to the key k_scatter_l1
+// writes in the wide format (dead records -> kEmpty, skipped).  hpid[] holds
+// pid_hash of the bucket's 2^bucket_bits privacy ids (LDS).
+__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, uint32_t v) {
+  if (v >> 31) return kEmpty;
+  const uint64_t mid = (uint64_t)(v >> kp.pk_bits);
+  const uint32_t h = hpid[mid & ((1ULL << kp.bucket_bits) - 1)];
+  return pair_key_from(h, kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask), mid << kp.pk_bits, kp.rand_shift);
+}
+
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
+template <bool COMPACT>
 __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
                                                              const uint8_t* __restrict__ allowed,
                                                              const unsigned* __restrict__ counts,
                                                              const unsigned* __restrict__ super_base,
-                                                             unsigned long long* __restrict__ keys1,
+                                                             RecKey<COMPACT>* __restrict__ keys1,
                                                              unsigned* __restrict__ rows1, unsigned* err) {
+  using K = RecKey<COMPACT>;
   extern __shared__ unsigned long long stage_raw[];
-  StageLds& s = *reinterpret_cast<StageLds*>(stage_raw);
+  StageLds<K>& s = *reinterpret_cast<StageLds<K>*>(stage_raw);
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
   for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] = 0;
@@ -520,12 +568,12 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
       } else {
         u[q] = i < t1 ? pid[i] : -1;
         k[q] = i < t1 ? pk[i] : 0;
-        u[q + 1] = -1;
-        k[q + 1] = 0;
+        u[q + 1] = i + 1 < t1 ? pid[i + 1] : -1;
+        k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
       }
     }
     int d[kStageItems];
-    unsigned long long x[kStageItems];
+    K x[kStageItems];
     unsigned r[kStageItems];
 #pragma unroll
     for (int q = 0; q < kStageItems; ++q) {
@@ -536,14 +584,18 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
         continue;
       }
       d[q] = (int)(u[q] >> mid_bits);
-      const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
+      bool is_dead = false;
       if (k[q] < 0 || k[q] >= kp.P) {
         atomicOr(err, 1u);
-        x[q] = dead | midv;
+        is_dead = true;
       } else if (allowed != nullptr && allowed[k[q]] == 0) {
-        x[q] = dead | midv;
+        is_dead = true;
+      }
+      if (COMPACT) {
+        x[q] = (K)compact_key(kp, u[q], k[q], is_dead);
       } else {
-        x[q] = pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift);
+        const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
+        x[q] = (K)(is_dead ? (dead | midv) : pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift));
       }
     }
     unsigned rank[kStageItems];
@@ -555,25 +607,28 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
 }
 
 // Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
+template <bool COMPACT>
 __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
                                                              unsigned* __restrict__ cursor,
-                                                             const unsigned long long* __restrict__ keys1,
+                                                             const RecKey<COMPACT>* __restrict__ keys1,
                                                              const unsigned* __restrict__ rows1,
-                                                             unsigned long long* __restrict__ keys2,
+                                                             RecKey<COMPACT>* __restrict__ keys2,
                                                              unsigned* __restrict__ rows2) {
+  using K = RecKey<COMPACT>;
+  constexpr int R = 16 / sizeof(K);  // records per 16-byte key load
   extern __shared__ unsigned long long stage_raw[];
-  StageLds& s = *reinterpret_cast<StageLds*>(stage_raw);
+  StageLds<K>& s = *reinterpret_cast<StageLds<K>*>(stage_raw);
   __shared__ int64_t s_first, s_base, s_r0, s_r1;
   const int nsub = 1 << kp.super_bits;
   if (threadIdx.x < 64) {
     // locate this workgroup's (super-bucket, chunk): chunks of a super-bucket
-    // are 4096-row windows aligned at its first even row (n_supers <= 64)
+    // are 4096-row windows aligned at its first R-aligned row (n_supers <= 64)
     const int lane = threadIdx.x;
     int64_t lo = 0, hi = 0, nch = 0;
     if (lane < kp.n_supers) {
       lo = super_base[lane];
       hi = super_base[lane + 1];
-      nch = hi > lo ? (hi - (lo & ~(int64_t)1) + kStageRows - 1) / kStageRows : 0;
+      nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kStageRows - 1) / kStageRows : 0;
     }
     int64_t inc = nch;
 #pragma unroll
@@ -586,7 +641,7 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
     const unsigned long long hit = __ballot(mine);
     if (lane == 0 && hit == 0) s_first = -1;  // grid is an upper bound on the chunk count
     if (mine) {
-      const int64_t base = (lo & ~(int64_t)1) + (g - (inc - nch)) * kStageRows;
+      const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kStageRows;
       s_first = (int64_t)lane << kp.super_bits;
       s_base = base;
       s_r0 = base > lo ? base : lo;
@@ -598,24 +653,29 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
   const int64_t base = s_base, r0 = s_r0, r1 = s_r1;
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
-  unsigned long long x[kStageItems];
+  K x[kStageItems];
   unsigned r[kStageItems];
   int d[kStageItems];
 #pragma unroll
-  for (int q = 0; q < kStageItems; q += 2) {  // two rows per 16-byte key load
-    const int64_t i = base + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
-    if (i >= r0 && i + 1 < r1) {
-      const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
-      const uint2 c = *reinterpret_cast<const uint2*>(rows1 + i);
-      x[q] = a.x;
-      x[q + 1] = a.y;
-      r[q] = c.x;
-      r[q + 1] = c.y;
-      d[q] = (int)((x[q] >> sub_shift) & sub_mask);
-      d[q + 1] = (int)((x[q + 1] >> sub_shift) & sub_mask);
+  for (int q = 0; q < kStageItems; q += R) {  // R records per 16-byte key load
+    const int64_t i = base + R * ((int64_t)threadIdx.x + (int64_t)(q / R) * blockDim.x);
+    if (i >= r0 && i + R - 1 < r1) {
+      if constexpr (COMPACT) {
+        const uint4 a = *reinterpret_cast<const uint4*>(keys1 + i);
+        const uint4 c = *reinterpret_cast<const uint4*>(rows1 + i);
+        x[q] = a.x; x[q + 1] = a.y; x[q + 2] = a.z; x[q + 3] = a.w;
+        r[q] = c.x; r[q + 1] = c.y; r[q + 2] = c.z; r[q + 3] = c.w;
+      } else {
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
+        const uint2 c = *reinterpret_cast<const uint2*>(rows1 + i);
+        x[q] = a.x; x[q + 1] = a.y;
+        r[q] = c.x; r[q + 1] = c.y;
+      }
+#pragma unroll
+      for (int e = 0; e < R; ++e) d[q + e] = (int)((x[q + e] >> sub_shift) & sub_mask);
     } else {
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
+      for (int e = 0; e < R; ++e) {
         const bool ok = i + e >= r0 && i + e < r1;
         x[q + e] = ok ? keys1[i + e] : 0;
         r[q + e] = ok ? rows1[i + e] : 0;
@@ -675,14 +735,18 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Streams the rows [begin, end) of one bucket: pred(key) selects candidates,
-// work(key, row) handles each candidate on compacted wavefronts.  Two rows per
-// lane per 16-byte key load (8-byte row load when ROWS), KU loads in flight per
+// Streams the rows [begin, end) of one bucket: conv(record) gives the row's
+// pair key, pred(key) selects candidates, work(key, row) handles each
+// candidate on compacted wavefronts.  R = 16 / sizeof(K) rows per lane per
+// 16-byte key load (and 4·R-byte row load when ROWS), KU loads in flight per
 // lane; every wave runs the same trip count so the queue stays convergent.
-template <int KU, bool ROWS, typename P, typename W>
-__device__ __forceinline__ void stream_bucket(const unsigned long long* __restrict__ keys,
-                                              const unsigned* __restrict__ rows, int64_t begin, int64_t end,
-                                              WaveQueue q, P&& pred, W&& work) {
+template <int KU, bool ROWS, typename K, typename CV, typename P, typename W>
+__device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const unsigned* __restrict__ rows,
+                                              int64_t begin, int64_t end, WaveQueue q, CV&& conv, P&& pred,
+                                              W&& work) {
+  constexpr int R = 16 / sizeof(K);
+  using KV = typename std::conditional<R == 4, uint4, ulonglong2>::type;
+  using RV = typename std::conditional<R == 4, uint4, uint2>::type;
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ULL << lane) - 1;
   int n = 0;  // wave-uniform queue length
@@ -714,28 +778,29 @@ __device__ __forceinline__ void stream_bucket(const unsigned long long* __restri
       work(wx, wr);
     }
   };
-  int64_t a0 = (begin + 1) & ~(int64_t)1;
+  int64_t a0 = (begin + R - 1) & ~(int64_t)(R - 1);
   if (a0 > end) a0 = end;
-  const int64_t a1 = a0 + ((end - a0) & ~(int64_t)1);
-  {  // odd head / tail row (lanes 0 / 1 of wave 0)
+  const int64_t a1 = a0 + ((end - a0) & ~(int64_t)(R - 1));
+  {  // unaligned head rows [begin, a0) on lanes 0..R-2, tail rows [a1, end) on lanes R..2R-2 of wave 0
     uint64_t x = kEmpty;
     uint32_t r = 0;
-    if (threadIdx.x == 0 && begin < a0) {
-      x = keys[begin];
-      if (ROWS) r = rows[begin];
+    const int t = threadIdx.x;
+    if (t < R - 1 && begin + t < a0) {
+      x = conv(keys[begin + t]);
+      if (ROWS) r = rows[begin + t];
     }
-    if (threadIdx.x == 1 && a1 < end) {
-      x = keys[a1];
-      if (ROWS) r = rows[a1];
+    if (t >= R && t < 2 * R - 1 && a1 + (t - R) < end) {
+      x = conv(keys[a1 + (t - R)]);
+      if (ROWS) r = rows[a1 + (t - R)];
     }
     push(x, r);
   }
-  const int64_t np = (a1 - a0) >> 1;
-  const ulonglong2* kv = reinterpret_cast<const ulonglong2*>(keys + a0);
-  const uint2* rv = reinterpret_cast<const uint2*>(rows + a0);
+  const int64_t np = (a1 - a0) / R;
+  const KV* kv = reinterpret_cast<const KV*>(keys + a0);
+  const RV* rv = reinterpret_cast<const RV*>(rows + a0);
   for (int64_t g0 = 0; g0 < np; g0 += (int64_t)blockDim.x * KU) {
-    ulonglong2 kx[KU];
-    uint2 rx[KU];
+    KV kx[KU];
+    RV rx[KU];
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int64_t g = g0 + (int64_t)u * blockDim.x + threadIdx.x;
@@ -743,14 +808,21 @@ __device__ __forceinline__ void stream_bucket(const unsigned long long* __restri
         kx[u] = kv[g];
         if (ROWS) rx[u] = rv[g];
       } else {
-        kx[u] = make_ulonglong2(kEmpty, kEmpty);
-        if (ROWS) rx[u] = make_uint2(0u, 0u);
+        if constexpr (R == 4) kx[u] = make_uint4(~0u, ~0u, ~0u, ~0u);  // dead records
+        else kx[u] = make_ulonglong2(kEmpty, kEmpty);
       }
     }
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-      push((uint64_t)kx[u].x, ROWS ? rx[u].x : 0u);
-      push((uint64_t)kx[u].y, ROWS ? rx[u].y : 0u);
+      if constexpr (R == 4) {
+        push(conv(kx[u].x), ROWS ? rx[u].x : 0u);
+        push(conv(kx[u].y), ROWS ? rx[u].y : 0u);
+        push(conv(kx[u].z), ROWS ? rx[u].z : 0u);
+        push(conv(kx[u].w), ROWS ? rx[u].w : 0u);
+      } else {
+        push(conv(kx[u].x), ROWS ? rx[u].x : 0u);
+        push(conv(kx[u].y), ROWS ? rx[u].y : 0u);
+      }
     }
   }
   if (n > 0) {  // partial wave
@@ -767,8 +839,8 @@ struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
   double* f2;                    // normalized sum of squares
 };
 
-template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES>
-__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const unsigned long long* __restrict__ keys,
+template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES, bool COMPACT>
+__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const RecKey<COMPACT>* __restrict__ keys,
                                                                  const unsigned* __restrict__ rowidx,
                                                                  const unsigned* __restrict__ offsets,
                                                                  const void* __restrict__ value,
@@ -789,6 +861,10 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
   const int wave = threadIdx.x >> 6;
   const WaveQueue wq{qbase + wave * kQueueCap,
                      (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
+  // COMPACT: pid_hash of the bucket's privacy ids, after the queues
+  uint32_t* hpid = (uint32_t*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap;
+  if (COMPACT)
+    for (int64_t t = threadIdx.x; t < S; t += blockDim.x) hpid[t] = pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t);
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
@@ -805,10 +881,14 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
   const int64_t begin = offsets[b * kp.n_tiles];
   const int64_t end = offsets[(b + 1) * kp.n_tiles];  // offsets has n_buckets*n_tiles+1 entries
   const uint64_t bmask = (uint64_t)S - 1;
+  auto conv = [&](RecKey<COMPACT> v) -> uint64_t {
+    if constexpr (COMPACT) return expand_key(kp, hpid, v);
+    else return v;
+  };
   // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys below
   // their sketch's current maximum
-  stream_bucket<kUnroll, false>(
-      keys, rowidx, begin, end, wq,
+  stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, false>(
+      keys, rowidx, begin, end, wq, conv,
       [&](uint64_t x) {
         return !dead_key(x, kp.rand_shift) && x < sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
       },
@@ -822,8 +902,8 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const un
 #endif
   // B2: rows of kept pairs
   const int flags = kp.clip.flags;
-  stream_bucket<kUnroll / 2, true>(
-      keys, rowidx, begin, end, wq,
+  stream_bucket<COMPACT ? PDP_B2_KU_COMPACT : kUnroll / 2, true>(
+      keys, rowidx, begin, end, wq, conv,
       [&](uint64_t x) {
         return !dead_key(x, kp.rand_shift) && x <= sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
       },
@@ -1117,7 +1197,11 @@ template <int VK, bool KA>
 int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w, const void* value,
                   const pdp_partition_accumulators& acc) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
-  auto kern = ranges ? k_bucket_bound<VK, KA, true> : k_bucket_bound<VK, KA, false>;
+  const bool compact = p.key_format == PDP_KEYS_COMPACT;
+  const void* kern = compact ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, true>
+                                       : (const void*)k_bucket_bound<VK, KA, false, true>)
+                             : (ranges ? (const void*)k_bucket_bound<VK, KA, true, false>
+                                       : (const void*)k_bucket_bound<VK, KA, false, false>);
   PairRecords rec{};
   if (ranges) {
     rec.runs = (unsigned*)(ws + w.runs);
@@ -1126,12 +1210,13 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
     rec.f1 = w.rec_f1 ? (double*)(ws + w.rec_f1) : nullptr;
     rec.f2 = w.rec_f2 ? (double*)(ws + w.rec_f2) : nullptr;
   }
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)p.lds_bytes));
+  PDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes));
+  const void* keys2 = ws + w.keys2;
+  const unsigned* rows2 = (const unsigned*)(ws + w.rows2);
+  const unsigned* counts = (const unsigned*)(ws + w.counts);
+  void* args[] = {(void*)&kp, (void*)&keys2, (void*)&rows2, (void*)&counts, (void*)&value, (void*)&acc, (void*)&rec};
   PDP_PROF_BEGIN("k_bucket_bound", st);
-  hipLaunchKernelGGL(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), (unsigned)p.lds_bytes, st, kp,
-                     (const unsigned long long*)(ws + w.keys2), (const unsigned*)(ws + w.rows2),
-                     (const unsigned*)(ws + w.counts), value, acc, rec);
+  PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (ranges) {
@@ -1140,6 +1225,34 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
     PDP_PROF_BEGIN("k_range_reduce", st);
     hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_ranges, (unsigned)p.n_groups), dim3(kRangeThreads),
                        kRangeLds, st, kp, rec, acc);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
+  return PDP_OK;
+}
+
+template <bool COMPACT>
+int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
+                   const uint8_t* allowed, const unsigned* counts, const unsigned* super_base, unsigned* cursor,
+                   char* ws, const Ws& w, unsigned* err) {
+  using K = RecKey<COMPACT>;
+  const size_t lds = sizeof(StageLds<K>);
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<COMPACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l2<COMPACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+  PDP_PROF_BEGIN("k_scatter_l1", st);
+  hipLaunchKernelGGL(k_scatter_l1<COMPACT>, dim3((unsigned)p.n_tiles), dim3(kPartThreads), lds, st, kp, pid, pk,
+                     allowed, counts, super_base, (K*)(ws + w.keys1), (unsigned*)(ws + w.rows1), err);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  if (p.super_bits > 0) {
+    // chunks: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
+    const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kStageRows + 2 * p.n_supers + 1;
+    PDP_PROF_BEGIN("k_scatter_l2", st);
+    hipLaunchKernelGGL(k_scatter_l2<COMPACT>, dim3((unsigned)n_l2), dim3(kPartThreads), lds, st, kp, super_base,
+                       cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1), (K*)(ws + w.keys2),
+                       (unsigned*)(ws + w.rows2));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -1217,6 +1330,7 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->merge = p.merge;
   info->n_ranges = p.n_ranges;
   info->range_group = p.range_group;
+  info->key_format = p.key_format;
   return PDP_OK;
 }
 
@@ -1292,26 +1406,11 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   hipLaunchKernelGGL(k_init_cursors, dim3(grid_for(n_init)), dim3(kBlock), 0, st, kp, counts, cursor, super_base);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_scatter_l1", st);
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(StageLds)));
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l2, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(StageLds)));
-  hipLaunchKernelGGL(k_scatter_l1, dim3((unsigned)p.n_tiles), dim3(kPartThreads), sizeof(StageLds), st, kp, privacy_id,
-                     partition_key, pk_allowed, counts, super_base, (unsigned long long*)(ws + w.keys1),
-                     (unsigned*)(ws + w.rows1), err);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  if (p.super_bits > 0) {
-    const int64_t n_l2 = (cfg->n_rows + p.n_supers) / kStageRows + p.n_supers + 1;
-    PDP_PROF_BEGIN("k_scatter_l2", st);
-    hipLaunchKernelGGL(k_scatter_l2, dim3((unsigned)n_l2), dim3(kPartThreads), sizeof(StageLds), st, kp, super_base, cursor,
-                       (const unsigned long long*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
-                       (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
-    PDP_PROF_END(st);
-    PDP_HIP_CHECK(hipGetLastError());
-  }
-  return PDP_OK;
+  if (p.key_format == PDP_KEYS_COMPACT)
+    return launch_scatter<true>(kp, p, st, privacy_id, partition_key, pk_allowed, counts, super_base, cursor, ws, w,
+                                err);
+  return launch_scatter<false>(kp, p, st, privacy_id, partition_key, pk_allowed, counts, super_base, cursor, ws, w,
+                               err);
 }
 
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,

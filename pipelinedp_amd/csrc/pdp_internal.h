@@ -64,10 +64,26 @@ __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
 // 32 random bits of the pair (pid, pk) under `seed`: a per-pid hash, then the
 // partition folded in as an odd-multiplier progression (32-bit multiplies only;
 // ties between one pid's pairs, p ~ 2^-32, break by partition).
+__host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, int64_t pid) {
+  return fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^ (uint32_t)seed);
+}
+
+__host__ __device__ __forceinline__ uint32_t pair_hash_from(uint32_t hpid, uint64_t seed, int64_t pk) {
+  return fmix32(hpid ^ ((uint32_t)pk * 0xC2B2AE3DU + (uint32_t)(seed >> 32)));
+}
+
 __host__ __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {
-  const uint32_t h = fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^
-                            (uint32_t)seed);
-  return fmix32(h ^ ((uint32_t)pk * 0xC2B2AE3DU + (uint32_t)(seed >> 32)));
+  return pair_hash_from(pid_hash(seed, pid), seed, pk);
+}
+
+// pair_key (below) with the pid's hash already computed (pid_hash)
+__host__ __device__ __forceinline__ uint64_t pair_key_from(uint32_t hpid, uint64_t seed, int64_t pk,
+                                                           uint64_t mid_bits, int rand_shift) {
+  const uint64_t h = (uint64_t)pair_hash_from(hpid, seed, pk) << 32;
+  const uint64_t low = (1ULL << rand_shift) - 1;
+  uint64_t x = (h & ~low) | mid_bits | (uint64_t)pk;
+  if ((x | low) == ~0ULL) x &= ~(1ULL << rand_shift);
+  return x;
 }
 
 // Sampling key of the pair (pid, pk): bits [rand_shift, 64) are random (the
@@ -77,11 +93,7 @@ __host__ __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, int64_t pi
 // is, so every execution path samples the same pairs.  Never equal to kEmpty.
 __host__ __device__ __forceinline__ uint64_t pair_key(uint64_t seed, int64_t pid, int64_t pk,
                                                       uint64_t mid_bits, int rand_shift) {
-  const uint64_t h = (uint64_t)pair_hash(seed, pid, pk) << 32;
-  const uint64_t low = (1ULL << rand_shift) - 1;
-  uint64_t x = (h & ~low) | mid_bits | (uint64_t)pk;
-  if ((x | low) == kEmpty) x &= ~(1ULL << rand_shift);
-  return x;
+  return pair_key_from(pid_hash(seed, pid), seed, pk, mid_bits, rand_shift);
 }
 
 __host__ __device__ __forceinline__ uint64_t derive_row_seed(uint64_t seed) {

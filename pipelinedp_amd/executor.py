@@ -182,7 +182,7 @@ def _acc_struct(acc) -> N.PartitionAccumulators:
 
 def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, seed: int,
                  row_offset: int = 0, algorithm: int = N.ALGO_AUTO,
-                 merge: int = N.MERGE_AUTO) -> N.BoundConfig:
+                 merge: int = N.MERGE_AUTO, key_format: int = N.KEYS_AUTO) -> N.BoundConfig:
     c = N.BoundConfig()
     c.n_rows = int(n_rows)
     c.n_privacy_ids = int(n_privacy_ids)
@@ -202,13 +202,15 @@ def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, se
     c.merge = int(merge)
     c.max_contributions = int(bounding.max_contributions or 0)
     c.rows_are_units = 1 if bounding.rows_are_units else 0
+    c.key_format = int(key_format)
     return c
 
 
 def bound_plan(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec,
-               algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO) -> N.BoundPlanInfo:
+               algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
+               key_format: int = N.KEYS_AUTO) -> N.BoundPlanInfo:
     """Execution plan the library resolves for this shard (no device work)."""
-    cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge)
+    cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge, key_format)
     info = N.BoundPlanInfo()
     N.check(N.lib().pdp_bound_plan(ctypes.byref(cfg), ctypes.byref(info)), "pdp_bound_plan")
     return info
@@ -231,7 +233,8 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                      bounding: BoundingSpec, seed: int, row_offset: int = 0, allowed=None,
                      acc=None, workspace: Optional[BoundWorkspace] = None, stream=None,
                      check_keys: bool = True, timer: Optional["StageTimer"] = None,
-                     algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO):
+                     algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
+                     key_format: int = N.KEYS_AUTO):
     """Bounds contributions of one shard and ADDS its per-partition accumulators.
 
     pid, pk: int64 device tensors of length n (dense keys; pid may be None
@@ -264,7 +267,8 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     if bounding.linf < 0 or bounding.linf > N.MAX_LINF:
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")
-    cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge)
+    cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
+                       key_format)
     nbytes = ctypes.c_uint64(0)
     N.check(lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)),
             "pdp_bound_workspace_bytes")

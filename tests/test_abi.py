@@ -129,9 +129,13 @@ def test_workspace_bytes(lib):
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(n_rows=1000)), ctypes.byref(small)) == 0
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg()), ctypes.byref(big)) == 0
     assert 0 < small.value < big.value
-    # bucketed: two levels of (8 B key + 4 B row) + pair records (8 B key + 8 B nsum per kept slot)
-    assert big.value >= 100_000_000 * 24 + 1_000_000 * 8 * 16
-    assert big.value < 100_000_000 * 26 + 1_000_000 * 8 * 16 + (64 << 20)
+    # bucketed, compact records: two levels of (4 B record + 4 B row) + pair records
+    # (8 B key + 8 B nsum per kept slot)
+    assert big.value >= 100_000_000 * 16 + 1_000_000 * 8 * 16
+    assert big.value < 100_000_000 * 18 + 1_000_000 * 8 * 16 + (64 << 20)
+    wide = ctypes.c_uint64(0)
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(key_format=N.KEYS_WIDE)), ctypes.byref(wide)) == 0
+    assert wide.value >= 100_000_000 * 24 + 1_000_000 * 8 * 16
     cb = ctypes.c_uint64(0)
     assert lib.pdp_compact_workspace_bytes(1 << 20, ctypes.byref(cb)) == 0 and cb.value > 0
 
@@ -141,7 +145,7 @@ def test_workspace_bytes(lib):
     ("max_contributions", 257, -4, b"max_contributions"),
     ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
     ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
-    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"),
+    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 3, -1, b"key_format"),
 ])
 def test_invalid_configs_are_rejected(lib, field, value, code, msg):
     info = N.BoundPlanInfo()

@@ -36,7 +36,8 @@ def _rand_shift(n, U, P, spec, algorithm=0):
     return X.bound_plan(n, U, P, spec, algorithm).rand_shift
 
 
-def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0, merge=0):
+def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0, merge=0,
+             key_format=0):
     import torch
     from pipelinedp_amd import executor as X
     tp = torch.as_tensor(pid).to(device)
@@ -44,7 +45,8 @@ def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0,
     tv = None if val is None else torch.as_tensor(val).to(device)
     ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
     acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
-                             allowed=ta, row_offset=row_offset, algorithm=algorithm, merge=merge)
+                             allowed=ta, row_offset=row_offset, algorithm=algorithm, merge=merge,
+                             key_format=key_format)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
@@ -94,8 +96,9 @@ CASES = [
 ]
 
 
-# name -> (PDP_ALGO_*, PDP_MERGE_*)
-ALGOS = {"global": (1, 0), "bucketed-atomic": (2, 1), "bucketed-ranges": (2, 2)}
+# name -> (PDP_ALGO_*, PDP_MERGE_*, PDP_KEYS_*)
+ALGOS = {"global": (1, 0, 0), "bucketed-atomic-wide": (2, 1, 1), "bucketed-ranges-wide": (2, 2, 1),
+         "bucketed-atomic-compact": (2, 1, 2), "bucketed-ranges-compact": (2, 2, 2)}
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
@@ -116,7 +119,7 @@ def test_bound_and_reduce_matches_oracle(device, case, skew, algo):
     except N.NativeLibraryError:
         pytest.skip(f"{algo} infeasible for l0={l0}, linf={linf}")
     got = _run_gpu(device, pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo][0],
-                   merge=ALGOS[algo][1])
+                   merge=ALGOS[algo][1], key_format=ALGOS[algo][2])
     want = _oracle(pid, pk, val, U, P, spec, seed, row_offset=77, algorithm=ALGOS[algo][0])
     _compare(got, want, _abs_scale(pid, pk, val, P, lo, hi, mid))
 
@@ -151,7 +154,7 @@ def test_public_filter(device, algo):
     allowed[::3] = True
     spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0, max_value=10)
     got = _run_gpu(device, pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo][0],
-                   merge=ALGOS[algo][1])
+                   merge=ALGOS[algo][1], key_format=ALGOS[algo][2])
     want = _oracle(pid, pk, val, U, P, spec, 99, allowed=allowed, algorithm=ALGOS[algo][0])
     _compare(got, want, _abs_scale(pid, pk, val, P, 0, 10, 0))
     assert np.all(got["count"][~allowed] == 0)
@@ -167,7 +170,7 @@ def test_out_of_range_keys_raise(device, algo, bad):
     spec = X.BoundingSpec(l0=1, linf=1, value_kind=O.VALUE_NONE, flags=0)
     with pytest.raises(ValueError):
         X.bound_and_reduce(pid, pk, None, n_privacy_ids=3, n_partitions=2, bounding=spec, seed=1,
-                           algorithm=ALGOS[algo][0], merge=ALGOS[algo][1])
+                           algorithm=ALGOS[algo][0], merge=ALGOS[algo][1], key_format=ALGOS[algo][2])
 
 
 @pytest.mark.parametrize("heavy", [False, True])
@@ -187,8 +190,8 @@ def test_algorithms_agree_at_scale(device, heavy):
                           min_value=0.0, max_value=10.0, middle=5.0)
     a = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=1)
     sc = _abs_scale(pid, pk, val, P, 0.0, 10.0, 5.0)
-    for merge in (1, 2):  # 30k partitions = 15 merge ranges
-        b = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=2, merge=merge)
+    for merge, keys in ((1, 1), (2, 1), (1, 2), (2, 2)):  # 30k partitions = 15 merge ranges
+        b = _run_gpu(device, pid, pk, val, U, P, spec, 3, algorithm=2, merge=merge, key_format=keys)
         np.testing.assert_array_equal(a["privacy_id_count"], b["privacy_id_count"])
         np.testing.assert_array_equal(a["count"], b["count"])
         assert np.all(np.abs(a["sum"] - b["sum"]) <= FLOAT_RTOL * sc)
@@ -208,6 +211,16 @@ def test_range_merge_matches_oracle_many_ranges(device, P):
     got = _run_gpu(device, pid, pk, val, U, P, spec, 21, algorithm=2, merge=2)
     want = _oracle(pid, pk, val, U, P, spec, 21, algorithm=2)
     _compare(got, want, _abs_scale(pid, pk, val, P, 0, 9, 4.5))
+
+
+def test_compact_records_chosen_when_they_fit():
+    """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records; wider key
+    spaces fall back to the 12-byte (u64 key + row) format."""
+    from pipelinedp_amd import executor as X
+    spec = X.BoundingSpec(l0=8, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_NSUM, min_value=0.0,
+                          max_value=10.0, middle=5.0)
+    assert X.bound_plan(100_000_000, 1_000_000, 100_000, spec).key_format == 2
+    assert X.bound_plan(100_000_000, 1_000_000, 10_000_000, spec).key_format == 1
 
 
 def test_empty_input(device):
