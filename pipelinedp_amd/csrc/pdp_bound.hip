@@ -39,24 +39,44 @@ namespace {
 constexpr int kPartThreads = 512;
 constexpr int64_t kTileRows = 65536;
 constexpr int kUnroll = 8;
-constexpr int kBucketThreads = 1024;
-constexpr int64_t kLdsBudget = 124 * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
+#ifndef PDP_BUCKET_THREADS
+#define PDP_BUCKET_THREADS 1024
+#endif
+#ifndef PDP_LDS_BUDGET_KB
+#define PDP_LDS_BUDGET_KB 124
+#endif
+constexpr int kBucketThreads = PDP_BUCKET_THREADS;
+constexpr int64_t kLdsBudget = PDP_LDS_BUDGET_KB * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
 constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
 constexpr int kRangeBits = 11;                // partitions per merge range = 2048
 constexpr int kRangeParts = 1 << kRangeBits;
-constexpr int kMaxRanges = 1024;              // per-bucket range histogram <= one block scan
+constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= one block scan
 constexpr int kRangeThreads = 256;
 constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
 // 16-byte key loads in flight per lane in the bucket kernel's B1 / B2 passes
 #ifndef PDP_B1_KU_COMPACT
-#define PDP_B1_KU_COMPACT 4
+#define PDP_B1_KU_COMPACT 1
+#endif
+#ifndef PDP_PIPE
+#define PDP_PIPE 1
+#endif
+// attribute of the bucket kernel's per-candidate work lambdas (A/B: noinline
+// keeps one copy of the sketch code instead of one per unrolled push)
+#ifndef PDP_WORK_ATTR
+#define PDP_WORK_ATTR
+#endif
+#ifndef PDP_BATCH_PRED
+#define PDP_BATCH_PRED 0
+#endif
+#ifndef PDP_INSERT_SKIP
+#define PDP_INSERT_SKIP 0
 #endif
 #ifndef PDP_B2_KU_COMPACT
-#define PDP_B2_KU_COMPACT 2
+#define PDP_B2_KU_COMPACT 1
 #endif
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
@@ -552,9 +572,8 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
   const int mid_bits = kp.bucket_bits + kp.super_bits;
   const uint64_t mid_mask = (1ULL << mid_bits) - 1;
   const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
-  for (int64_t c0 = t0; c0 < t1; c0 += kStageRows) {
-    // two consecutive rows per 16-byte load (tiles and chunks start even)
-    int64_t u[kStageItems], k[kStageItems];
+  // two consecutive rows per 16-byte load (tiles and chunks start even)
+  auto load = [&](int64_t c0, int64_t (&u)[kStageItems], int64_t (&k)[kStageItems]) {
 #pragma unroll
     for (int q = 0; q < kStageItems; q += 2) {
       const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
@@ -572,6 +591,10 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
         k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
       }
     }
+  };
+  int64_t u[kStageItems], k[kStageItems];
+  if (t0 < t1) load(t0, u, k);
+  for (int64_t c0 = t0; c0 < t1; c0 += kStageRows) {
     int d[kStageItems];
     K x[kStageItems];
     unsigned r[kStageItems];
@@ -598,6 +621,8 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
         x[q] = (K)(is_dead ? (dead | midv) : pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift));
       }
     }
+    // next sub-chunk's column loads go out before this one's LDS passes
+    if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
     unsigned rank[kStageItems];
     stage_count(s, nd, d, rank);
     stage_write(s, nd, d, rank, x, r, keys1, rows1);
@@ -750,8 +775,7 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ULL << lane) - 1;
   int n = 0;  // wave-uniform queue length
-  auto push = [&](uint64_t x, uint32_t r) {
-    const bool p = pred(x);
+  auto push_p = [&](uint64_t x, uint32_t r, bool p) {
     const unsigned long long m = __ballot(p);
     if (p) {
       const int pos = n + __popcll(m & below);
@@ -778,6 +802,7 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
       work(wx, wr);
     }
   };
+  auto push = [&](uint64_t x, uint32_t r) { push_p(x, r, pred(x)); };
   int64_t a0 = (begin + R - 1) & ~(int64_t)(R - 1);
   if (a0 > end) a0 = end;
   const int64_t a1 = a0 + ((end - a0) & ~(int64_t)(R - 1));
@@ -798,9 +823,8 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
   const int64_t np = (a1 - a0) / R;
   const KV* kv = reinterpret_cast<const KV*>(keys + a0);
   const RV* rv = reinterpret_cast<const RV*>(rows + a0);
-  for (int64_t g0 = 0; g0 < np; g0 += (int64_t)blockDim.x * KU) {
-    KV kx[KU];
-    RV rx[KU];
+  const int64_t step = (int64_t)blockDim.x * KU;
+  auto load = [&](int64_t g0, KV (&kx)[KU], RV (&rx)[KU]) {
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       const int64_t g = g0 + (int64_t)u * blockDim.x + threadIdx.x;
@@ -812,6 +836,53 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
         else kx[u] = make_ulonglong2(kEmpty, kEmpty);
       }
     }
+  };
+  KV kx[KU];
+  RV rx[KU];
+  if (np > 0) load(0, kx, rx);
+  for (int64_t g0 = 0; g0 < np; g0 += step) {
+#if PDP_PIPE
+    // software pipeline: the next batch's loads are in flight while this
+    // batch runs through the queue (LDS work only, no vector memory)
+    KV nk[KU];
+    RV nr[KU];
+    const bool more = g0 + step < np;  // block-uniform
+    if (more) load(g0 + step, nk, nr);
+#endif
+#if PDP_BATCH_PRED
+    // every record's key conversion and predicate first (their LDS reads issue
+    // back to back under one wait), then the wave-serial queue pushes; a
+    // predicate evaluated before earlier pushes' work ran is only weaker (the
+    // sketch maxima only decrease), and work() re-checks
+    uint64_t xs[KU * R];
+    bool ps[KU * R];
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if constexpr (R == 4) {
+        xs[u * 4 + 0] = conv(kx[u].x);
+        xs[u * 4 + 1] = conv(kx[u].y);
+        xs[u * 4 + 2] = conv(kx[u].z);
+        xs[u * 4 + 3] = conv(kx[u].w);
+      } else {
+        xs[u * 2 + 0] = conv(kx[u].x);
+        xs[u * 2 + 1] = conv(kx[u].y);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < KU * R; ++i) ps[i] = pred(xs[i]);
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if constexpr (R == 4) {
+        push_p(xs[u * 4 + 0], ROWS ? rx[u].x : 0u, ps[u * 4 + 0]);
+        push_p(xs[u * 4 + 1], ROWS ? rx[u].y : 0u, ps[u * 4 + 1]);
+        push_p(xs[u * 4 + 2], ROWS ? rx[u].z : 0u, ps[u * 4 + 2]);
+        push_p(xs[u * 4 + 3], ROWS ? rx[u].w : 0u, ps[u * 4 + 3]);
+      } else {
+        push_p(xs[u * 2 + 0], ROWS ? rx[u].x : 0u, ps[u * 2 + 0]);
+        push_p(xs[u * 2 + 1], ROWS ? rx[u].y : 0u, ps[u * 2 + 1]);
+      }
+    }
+#else
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       if constexpr (R == 4) {
@@ -824,6 +895,18 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
         push(conv(kx[u].y), ROWS ? rx[u].y : 0u);
       }
     }
+#endif
+#if PDP_PIPE
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        kx[u] = nk[u];
+        if (ROWS) rx[u] = nr[u];
+      }
+    }
+#else
+    if (g0 + step < np) load(g0 + step, kx, rx);
+#endif
   }
   if (n > 0) {  // partial wave
     wave_lds_fence();
@@ -849,15 +932,20 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
   const int64_t n_slots = S * l0;
-  unsigned long long* sk = smem;                      // [S*l0] pair sketch per pid
-  unsigned long long* rsk = sk + n_slots;             // bounded: [S*l0*linf] row sketches
+  // LDS state is structure-of-arrays: entry j of privacy id p at [j * S + p]
+  // (row-sketch entry t of slot s at [t * S*l0 + s]), so a wave's lanes, which
+  // touch random privacy ids, spread over the LDS banks
+  unsigned long long* sk = smem;                      // [l0][S] pair sketch per pid
+  unsigned long long* rsk = sk + n_slots;             // bounded: [linf][S*l0] row sketches
   double* tot = (double*)(sk + n_slots);              // keep-all: [3][S*l0] pair sums
   unsigned* cnt = KEEP_ALL_ROWS ? (unsigned*)(tot + 3 * n_slots) : (unsigned*)(rsk + n_slots * kp.linf);
   unsigned* rh = cnt + n_slots;          // RANGES: [n_ranges] kept pairs per partition range
   unsigned* rcur = rh + kp.n_ranges;     //         [n_ranges] write cursors
   unsigned* wsum = rcur + kp.n_ranges;   //         block-scan scratch
   unsigned* tail = RANGES ? wsum + kBucketThreads / 64 + 1 : rh;
-  unsigned long long* qbase = (unsigned long long*)(((uintptr_t)tail + 7) & ~(uintptr_t)7);
+  // derived from smem by offset (not through an integer round trip) so the
+  // compiler keeps the LDS address space and emits ds_* rather than flat_*
+  unsigned long long* qbase = smem + (((const char*)tail - (const char*)smem) + 7) / 8;
   const int wave = threadIdx.x >> 6;
   const WaveQueue wq{qbase + wave * kQueueCap,
                      (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
@@ -890,11 +978,18 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, false>(
       keys, rowidx, begin, end, wq, conv,
       [&](uint64_t x) {
-        return !dead_key(x, kp.rand_shift) && x < sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
+#ifdef PDP_ABL_B1_NOPRED
+        return x == 0;
+#endif
+        return !dead_key(x, kp.rand_shift) && x < sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
       },
-      [&](uint64_t x, uint32_t) {
-        unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask) * l0;
-        if (x < s[l0 - 1]) sketch_insert(s, l0, x);
+      [&](uint64_t x, uint32_t) PDP_WORK_ATTR {
+        unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask);
+#if PDP_INSERT_SKIP
+        if (x < s[(l0 - 1) * S]) sketch_insert_strided_skip(s, l0, S, x);
+#else
+        if (x < s[(l0 - 1) * S]) sketch_insert_strided(s, l0, S, x);
+#endif
       });
   __syncthreads();
 #ifdef PDP_ABL_B1_ONLY
@@ -905,19 +1000,18 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   stream_bucket<COMPACT ? PDP_B2_KU_COMPACT : kUnroll / 2, true>(
       keys, rowidx, begin, end, wq, conv,
       [&](uint64_t x) {
-        return !dead_key(x, kp.rand_shift) && x <= sk[((x >> kp.pk_bits) & bmask) * l0 + l0 - 1];
+        return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
       },
-      [&](uint64_t x, uint32_t r) {
+      [&](uint64_t x, uint32_t r) PDP_WORK_ATTR {
       const int64_t pl = (x >> kp.pk_bits) & bmask;
-      const unsigned long long* s = sk + pl * l0;
-      const int j = sketch_find(s, l0, x);
+      const int j = sketch_find_strided(sk + pl, l0, S, x);
       if (j < 0) return;
-      const int64_t slot = pl * l0 + j;
+      const int64_t slot = j * S + pl;  // entry j of pid pl (structure of arrays)
       atomicAdd(cnt + slot, 1u);
       if (!KEEP_ALL_ROWS) {
         const uint64_t y = row_key(kp.row_seed, kp.row_offset + r, r);
-        unsigned long long* rs = rsk + slot * kp.linf;
-        if (y < rs[kp.linf - 1]) sketch_insert(rs, kp.linf, y);
+        unsigned long long* rs = rsk + slot;
+        if (y < rs[(kp.linf - 1) * n_slots]) sketch_insert_strided(rs, kp.linf, n_slots, y);
       } else if (VALUE_KIND != PDP_VALUE_NONE) {
         double v;
         long long iv;
@@ -972,7 +1066,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     PairSums ps;
     if (!KEEP_ALL_ROWS) {
       const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
-      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot * kp.linf, m, value, kp.clip);
+      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot, m, value, kp.clip, n_slots);
     } else if (VALUE_KIND != PDP_VALUE_NONE) {
       ps = pair_sums_from_totals((long long)c, tot[slot], tot[n_slots + slot], tot[2 * n_slots + slot], kp.clip);
     } else {

@@ -174,6 +174,47 @@ __device__ __forceinline__ void sketch_insert(unsigned long long* s, int k, uint
   }
 }
 
+// The same on a sketch whose entries are `stride` apart (structure-of-arrays
+// LDS layout: entry j of sketch p at s[j * stride + p], so that the lanes of a
+// wave touching different sketches hit different LDS banks).
+__device__ __forceinline__ void sketch_insert_strided(unsigned long long* s, int k, int64_t stride, uint64_t x) {
+  for (int j = 0; j < k; ++j) {
+    const uint64_t old = atomicMin(s + j * stride, (unsigned long long)x);
+    if (old == x) return;
+    if (old > x) {
+      if (old == kEmpty) return;
+      x = old;
+    }
+  }
+}
+
+// As sketch_insert_strided, but the atomic chain starts at the first entry
+// not below x in a plain (non-atomic) read of the sketch: entries only ever
+// decrease, so an entry already below x stays below it and atomicMin there
+// would leave it unchanged and carry x on.  Saves the leading atomics (LDS
+// 64-bit atomics with return are the expensive part of an insert).
+__device__ __forceinline__ void sketch_insert_strided_skip(unsigned long long* s, int k, int64_t stride, uint64_t x) {
+  int j = 0;
+  while (j < k && s[j * stride] < x) ++j;
+  for (; j < k; ++j) {
+    const uint64_t old = atomicMin(s + j * stride, (unsigned long long)x);
+    if (old == x) return;
+    if (old > x) {
+      if (old == kEmpty) return;
+      x = old;
+    }
+  }
+}
+
+__device__ __forceinline__ int sketch_find_strided(const unsigned long long* s, int k, int64_t stride, uint64_t x) {
+  int lo = 0, hi = k;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (s[mid * stride] < x) lo = mid + 1; else hi = mid;
+  }
+  return (lo < k && s[lo * stride] == x) ? lo : -1;
+}
+
 // Position of x in a quiescent sorted sketch, or -1.
 __device__ __forceinline__ int sketch_find(const unsigned long long* s, int k, uint64_t x) {
   int lo = 0, hi = k;
@@ -215,7 +256,8 @@ struct ClipParams {
 // (combiners.py:749-753 with the Count/Sum/Mean/Variance children).
 template <int VALUE_KIND>
 __device__ __forceinline__ PairSums pair_sums_from_rows(const unsigned long long* rows, long long m,
-                                                        const void* value, const ClipParams& cp) {
+                                                        const void* value, const ClipParams& cp,
+                                                        int64_t stride = 1) {
   PairSums s{m, 0, 0.0, 0.0, 0.0};
   if (VALUE_KIND == PDP_VALUE_NONE) return s;
   double raw = 0.0;
@@ -223,7 +265,7 @@ __device__ __forceinline__ PairSums pair_sums_from_rows(const unsigned long long
   for (long long t = 0; t < m; ++t) {
     double v;
     long long iv;
-    load_value<VALUE_KIND>(value, (uint32_t)rows[t], &v, &iv);
+    load_value<VALUE_KIND>(value, (uint32_t)rows[t * stride], &v, &iv);
     const double cv = fmin(fmax(v, cp.lo), cp.hi);
     if (cp.flags & PDP_SUM_PER_PARTITION) {
       raw += v;
