@@ -239,6 +239,18 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
                       const double* noised_count, double* out, int64_t out_stride,
                       uint64_t seed, void* stream);
 
+/* DPEngine.add_dp_noise (dp_engine.py:551-607): out[i] = (double)values[i]
+ * + noise, the `lambda value: create_mechanism().add_noise(float(value))` of
+ * its "Add noise" map_values stage (dp_engine.py:595-599) over a column.
+ * values: n int64 (PDP_VALUE_I64) or fp64 (PDP_VALUE_F64); noise_kind
+ * PDP_NOISE_LAPLACE (scale = b = l0*linf/eps, dp_computations.py:430-477) or
+ * PDP_NOISE_GAUSSIAN (scale = sigma, :480-537).  Element i draws from the
+ * Philox4x32-10 stream (seed, index_offset + i), so shards of one column
+ * noised with their global offsets equal the unsharded result.  values and
+ * out: device, 16-byte aligned; out may alias values when both are fp64. */
+int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noise_kind,
+                  double scale, uint64_t seed, int64_t index_offset, double* out, void* stream);
+
 /* Device error word: the bounding kernels set bit 0 when a key is outside
  * [0, n_privacy_ids) x [0, n_partitions) (the row is skipped, never read out
  * of bounds).  Reads it from the workspace of pdp_bound_contributions

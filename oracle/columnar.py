@@ -361,3 +361,15 @@ def noise_metrics(ops, index, acc, sum_is_int, noised_count, seed, partition_off
         elif kind == OP_THRESHOLDED_PID:
             put(cols[0], np.asarray(noised_count)[index])
     return out
+
+
+ADD_NOISE_SLOT = 0x41444E00  # pdp_select.hip kAddNoiseSlot
+
+
+def add_noise(values, noise_kind, scale, seed, index_offset=0):
+    """DPEngine.add_dp_noise's "Add noise" map (dp_engine.py:595-599):
+    float(value) + noise, element i drawing from Philox (seed, offset + i)."""
+    x = np.asarray(values)
+    idx = np.arange(x.shape[0], dtype=np.int64) + int(index_offset)
+    r = philox_for(int(seed), idx, ADD_NOISE_SLOT)
+    return x.astype(np.float64) + draw_noise(noise_kind, float(scale), r)

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "pdp_compact_workspace_bytes",
     "pdp_compact",
     "pdp_noise_metrics",
+    "pdp_add_noise",
     "pdp_bound_error_flags",
     "pdp_profiler_enable",
     "pdp_profiler_report",
@@ -158,6 +159,7 @@ def _declare(lib):
         "pdp_compact": (ctypes.c_int, [vp, i64, vp, vp, vp, u64, vp]),
         "pdp_noise_metrics": (ctypes.c_int, [P(MetricOp), i32, vp, i64, vp, i64,
                                              P(PartitionAccumulators), i32, vp, vp, i64, u64, vp]),
+        "pdp_add_noise": (ctypes.c_int, [vp, i32, i64, i32, ctypes.c_double, u64, i64, vp, vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),

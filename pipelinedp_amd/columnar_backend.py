@@ -53,6 +53,8 @@ ST_EMPTY_ACCS = "Build empty accumulators"                           # dp_engine
 ST_SP_EXTRACT = "Extract (privacy_id, partition_key))"               # :241-244
 ST_SP_COMBINE = "Combine accumulators per partition key"             # :276-277
 ST_SP_KEYS = "Drop accumulators, keep only partition keys"           # :286-287
+# DPEngine.add_dp_noise
+ST_ADD_NOISE = "Add noise"                                           # dp_engine.py:597-599
 SELECT_PARTITIONS = {"Group by privacy_id", "Sample cross-partition contributions",
                      "Drop privacy id and add accumulator"}                          # :248-273
 
@@ -138,9 +140,72 @@ def _chain(sink):
     return nodes, node
 
 
-def recognise(sink) -> AggregatePlan:
-    """Maps a recorded chain to an AggregatePlan; NotImplementedError otherwise."""
+class NoisePlan:
+    """A recognised DPEngine.add_dp_noise chain (dp_engine.py:551-607):
+    source of (partition_key, value) -> map_values "Add noise" -> annotate."""
+
+    def __init__(self, source, noise_fn, params, budget):
+        self.source = source
+        self.noise_fn = noise_fn
+        self.params = params
+        self.budget = budget
+
+
+def _closure_objects(fn, depth=0):
+    """Objects captured by fn's closure, recursively through captured functions."""
+    out = []
+    for cell in getattr(fn, "__closure__", None) or ():
+        try:
+            obj = cell.cell_contents
+        except ValueError:
+            continue
+        out.append(obj)
+        if callable(obj) and depth < 4:
+            out.extend(_closure_objects(obj, depth + 1))
+    return out
+
+
+def noise_mechanism_of(noise_fn):
+    """(PDP_NOISE_*, b or sigma) of the add_dp_noise lambda: the
+    MechanismSpec and Sensitivities its create_mechanism() closes over
+    (dp_engine.py:580-593), recomputed with the mirror's mechanisms."""
+    spec = sens = None
+    for obj in _closure_objects(noise_fn):
+        if hasattr(obj, "mechanism_type") and hasattr(obj, "standard_deviation_is_set"):
+            spec = obj
+        elif all(hasattr(obj, a) for a in ("l0", "linf", "l1", "l2")):
+            sens = obj
+    if spec is None or sens is None:
+        raise NotImplementedError("unrecognised add_dp_noise function (no MechanismSpec / Sensitivities)")
+    if sens.l0 is not None and sens.linf is not None:
+        local = dpc.Sensitivities(l0=sens.l0, linf=sens.linf)
+    else:
+        local = dpc.Sensitivities(l1=sens.l1, l2=sens.l2)
+    return _additive(spec, local)
+
+
+def _recognise_add_noise(nodes, source) -> NoisePlan:
+    fn = params = budget = None
+    for node in nodes:
+        if node.op == "map_values" and node.stage == ST_ADD_NOISE:
+            if fn is not None:
+                raise NotImplementedError("more than one 'Add noise' stage")
+            fn = node.fn
+        elif node.op == "annotate":
+            params = node.kwargs.get("params")
+            budget = node.kwargs.get("budget")
+        else:
+            raise NotImplementedError(f"unrecognised stage {node.stage!r} in an add_dp_noise graph")
+    return NoisePlan(source, fn, params, budget)
+
+
+def recognise(sink):
+    """Maps a recorded chain to an AggregatePlan (aggregate /
+    select_partitions) or a NoisePlan (add_dp_noise); NotImplementedError
+    otherwise."""
     nodes, source = _chain(sink)
+    if any(n.op == "map_values" and n.stage == ST_ADD_NOISE for n in nodes):
+        return _recognise_add_noise(nodes, source)
     if any(n.op == "map" and n.stage == ST_SP_EXTRACT for n in nodes):
         return _recognise_select_partitions(nodes, source)
     plan = AggregatePlan()
@@ -455,6 +520,8 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
 
     def _execute(self, sink) -> List:
         plan = recognise(sink)
+        if isinstance(plan, NoisePlan):
+            return AddNoiseRun(self, plan).run()
         return AggregateRun(self, plan).run()
 
     def accumulators(self, col):
@@ -663,6 +730,41 @@ class AggregateRun:
         if not hasattr(self, "_seed_cache"):
             self._seed_cache = parallel.broadcast_seeds(self.backend._seeds())
         return self._seed_cache
+
+
+class AddNoiseRun:
+    """DPEngine.add_dp_noise on the GPU: the value column + noise in one
+    kernel (`pdp_add_noise`), keys passed through in input order.  A
+    two-column ColumnTable (keys, values) is used as columns directly (device
+    tensors stay on the device); any other source is read as (key, value)
+    tuples.  Under torch.distributed each rank noises its own rows with global
+    row indices as Philox counters."""
+
+    def __init__(self, backend: ColumnarBackend, plan: NoisePlan):
+        self.backend = backend
+        self.plan = plan
+
+    def run(self) -> List:
+        import torch
+        from pipelinedp_amd import executor as X
+        kind, scale = noise_mechanism_of(self.plan.noise_fn)
+        device = self.backend._torch_device()
+        src = self.plan.source
+        if isinstance(src, C.ColumnTable) and len(src.names) == 2:
+            keys = src.column(src.names[0])
+            vals = src.column(src.names[1])
+        else:
+            pairs = list(src)
+            keys = [k for k, _ in pairs]
+            vals = [v for _, v in pairs]
+        val_t = _value_tensor(vals, device)
+        offset = parallel.row_offset(int(val_t.numel()))
+        _, _, seed_noise = parallel.broadcast_seeds(self.backend._seeds())
+        out = X.add_noise(val_t, noise_kind=kind, scale=scale, seed=seed_noise, index_offset=offset)
+        noised = out.cpu().numpy().tolist()
+        if C._is_torch(keys):
+            keys = keys.cpu().numpy()
+        return list(zip(np.asarray(keys).tolist() if isinstance(keys, np.ndarray) else keys, noised))
 
 
 def _local_strategy(strategy):

@@ -8,6 +8,7 @@
 //   k_compact_*       ascending stream compaction of the kept partitions
 //   k_noise_metrics   CompoundCombiner.compute_metrics (combiners.py:766-788)
 //                     for Count/Sum/PrivacyIdCount/Mean/Variance children
+#include <cmath>
 #include <cstring>
 
 #include "pdp_internal.h"
@@ -127,6 +128,42 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(const uint8_t* __restr
   for (int t = 0; t < kCompactItems; ++t) {
     const int64_t i = base + t;
     if (i < n && keep[i]) out_index[pos++] = i;
+  }
+}
+
+
+// DPEngine.add_dp_noise (dp_engine.py:551-607): y[i] = float(x[i]) + noise,
+// one Philox4x32-10 draw per element keyed by (seed, index_offset + i).  One
+// 16-byte load + one 16-byte store per thread step (2 elements): HBM-bound.
+constexpr uint32_t kAddNoiseSlot = 0x41444E00u;  // "ADN"
+
+template <int VALUE_KIND>
+__global__ void __launch_bounds__(kBlock) k_add_noise(const void* __restrict__ x, int64_t n, int kind,
+                                                      double scale, uint64_t seed, int64_t index_offset,
+                                                      double* __restrict__ y) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t pairs = n >> 1;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < pairs; t += stride) {
+    const int64_t i = 2 * t;
+    double a, b;
+    if (VALUE_KIND == PDP_VALUE_I64) {
+      const longlong2 v = reinterpret_cast<const longlong2*>(x)[t];
+      a = (double)v.x;
+      b = (double)v.y;
+    } else {
+      const double2 v = reinterpret_cast<const double2*>(x)[t];
+      a = v.x;
+      b = v.y;
+    }
+    double2 o;
+    o.x = a + draw_noise(kind, scale, philox_for(seed, index_offset + i, kAddNoiseSlot));
+    o.y = b + draw_noise(kind, scale, philox_for(seed, index_offset + i + 1, kAddNoiseSlot));
+    reinterpret_cast<double2*>(y)[t] = o;
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t i = n - 1;
+    const double a = VALUE_KIND == PDP_VALUE_I64 ? (double)((const long long*)x)[i] : ((const double*)x)[i];
+    y[i] = a + draw_noise(kind, scale, philox_for(seed, index_offset + i, kAddNoiseSlot));
   }
 }
 
@@ -323,6 +360,32 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
                      n_ops, index, n_kept, n_kept_dev, partition_offset, *acc, sum_is_int, noised_count,
                      out, out_stride, seed);
   PDP_PROF_END((hipStream_t)stream);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noise_kind, double scale,
+                  uint64_t seed, int64_t index_offset, double* out, void* stream) {
+  if (n < 0) return pdp::set_error(PDP_E_INVALID, "n must be >= 0");
+  if (value_kind != PDP_VALUE_F64 && value_kind != PDP_VALUE_I64)
+    return pdp::set_error(PDP_E_INVALID, "value_kind must be PDP_VALUE_F64 or PDP_VALUE_I64");
+  if (noise_kind != PDP_NOISE_LAPLACE && noise_kind != PDP_NOISE_GAUSSIAN)
+    return pdp::set_error(PDP_E_INVALID, "bad noise_kind");
+  if (!(scale >= 0.0) || !std::isfinite(scale)) return pdp::set_error(PDP_E_INVALID, "scale must be finite and >= 0");
+  if (n == 0) return PDP_OK;
+  if (values == nullptr || out == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (((uintptr_t)values | (uintptr_t)out) & 15)
+    return pdp::set_error(PDP_E_INVALID, "values and out must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t pairs = (n + 1) >> 1;
+  PDP_PROF_BEGIN("k_add_noise", st);
+  if (value_kind == PDP_VALUE_I64)
+    hipLaunchKernelGGL(k_add_noise<PDP_VALUE_I64>, dim3(grid_for(pairs)), dim3(kBlock), 0, st, values, n,
+                       noise_kind, scale, seed, index_offset, out);
+  else
+    hipLaunchKernelGGL(k_add_noise<PDP_VALUE_F64>, dim3(grid_for(pairs)), dim3(kBlock), 0, st, values, n,
+                       noise_kind, scale, seed, index_offset, out);
+  PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
 }

@@ -356,3 +356,26 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
         n_kept = int(n_kept_dev.item())
         return index[:n_kept], out, n_kept
     return index, out, n_kept_dev
+
+
+def add_noise(values, *, noise_kind: int, scale: float, seed: int, index_offset: int = 0,
+              out=None, stream=None):
+    """DPEngine.add_dp_noise's "Add noise" stage (dp_engine.py:595-599) on a
+    device column: returns float64 values + Laplace(b)/Gaussian(sigma) noise
+    drawn from Philox stream (seed, index_offset + i) (`pdp_add_noise`)."""
+    torch = _torch()
+    lib = N.lib()
+    if not values.is_cuda:
+        raise ValueError("values must be a device tensor")
+    if values.dtype not in (torch.int64, torch.float64):
+        raise ValueError("values must be int64 or float64")
+    values = values.contiguous()
+    n = int(values.numel())
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=values.device)
+    _check_col(out, "out", (torch.float64,), n, values.device)
+    vk = N.VALUE_I64 if values.dtype == torch.int64 else N.VALUE_F64
+    N.check(lib.pdp_add_noise(_ptr(values), vk, n, int(noise_kind), float(scale),
+                              int(seed) & 0xFFFFFFFFFFFFFFFF, int(index_offset), _ptr(out), _stream(stream)),
+            "pdp_add_noise")
+    return out

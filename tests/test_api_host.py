@@ -355,3 +355,46 @@ def test_select_partitions_validation_like_reference():
         engine.select_partitions(ROWS, _params(), ext)
     with pytest.raises(ValueError):
         engine.select_partitions([], pdp.SelectPartitionsParams(max_partitions_contributed=1), ext)
+
+
+@pytest.mark.parametrize("engine_name", ["mirror", "reference"])
+@pytest.mark.parametrize("kind", ["laplace", "gaussian"])
+def test_add_dp_noise_recognised(engine_name, kind):
+    """DPEngine.add_dp_noise (dp_engine.py:551-607) maps to one noise kernel
+    over the value column with the mechanism its lambda closes over:
+    Laplace b = l0*linf/eps, Gaussian sigma = calibrate(eps, delta, sqrt(l0)*linf)."""
+    mod = pdp if engine_name == "mirror" else _import_reference()
+    acc = mod.NaiveBudgetAccountant(total_epsilon=2.0, total_delta=1e-6)
+    engine = mod.DPEngine(acc, CB.ColumnarBackend())
+    nk = mod.NoiseKind.LAPLACE if kind == "laplace" else mod.NoiseKind.GAUSSIAN
+    params = mod.AddDPNoiseParams(noise_kind=nk, l0_sensitivity=3, linf_sensitivity=1.5)
+    sink = engine.add_dp_noise([(k, float(k)) for k in range(10)], params)
+    acc.compute_budgets()
+    plan = CB.recognise(sink)
+    assert isinstance(plan, CB.NoisePlan)
+    code, scale = CB.noise_mechanism_of(plan.noise_fn)
+    if kind == "laplace":
+        assert code == N.NOISE_LAPLACE and math.isclose(scale, 3 * 1.5 / 2.0, rel_tol=1e-12)
+    else:
+        assert code == N.NOISE_GAUSSIAN
+        assert math.isclose(scale, dpc.compute_sigma(2.0, 1e-6, math.sqrt(3) * 1.5), rel_tol=1e-12)
+
+
+def test_add_dp_noise_validation_like_reference():
+    with pytest.raises(ValueError):
+        pdp.AddDPNoiseParams(noise_kind=pdp.NoiseKind.LAPLACE, l0_sensitivity=0, linf_sensitivity=1.0)
+    with pytest.raises(ValueError):
+        pdp.AddDPNoiseParams(noise_kind=pdp.NoiseKind.LAPLACE, l0_sensitivity=1, linf_sensitivity=-1.0)
+
+
+def test_add_dp_noise_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+    engine = pdp.DPEngine(acc, CB.ColumnarBackend())
+    sink = engine.add_dp_noise([(0, 1.0)], pdp.AddDPNoiseParams(noise_kind=pdp.NoiseKind.LAPLACE,
+                                                                 l0_sensitivity=1, linf_sensitivity=1.0))
+    acc.compute_budgets()
+    with pytest.raises(RuntimeError):
+        list(sink)

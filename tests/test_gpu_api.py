@@ -266,3 +266,65 @@ def test_select_partitions_matches_oracle_with_sampling(device, strategy):
                        noise_scale=sel.noise_scale, threshold=sel.threshold, seed=seed_select)
     assert got == np.flatnonzero(keep).tolist()
     assert 0 < len(got) < P
+
+
+def _add_noise(pairs_or_table, kind, eps, delta, l0, linf, seed):
+    backend = CB.ColumnarBackend(seed=seed)
+    acc = pdp.NaiveBudgetAccountant(total_epsilon=eps, total_delta=delta)
+    engine = pdp.DPEngine(acc, backend)
+    nk = pdp.NoiseKind.LAPLACE if kind == "laplace" else pdp.NoiseKind.GAUSSIAN
+    sink = engine.add_dp_noise(pairs_or_table, pdp.AddDPNoiseParams(noise_kind=nk, l0_sensitivity=l0,
+                                                                     linf_sensitivity=linf))
+    acc.compute_budgets()
+    return sink, backend
+
+
+@pytest.mark.parametrize("kind", ["laplace", "gaussian"])
+def test_add_dp_noise_matches_oracle_and_distribution(device, kind):
+    """add_dp_noise (dp_engine.py:551-607) through the HIP kernel: keys kept
+    in order, values = oracle (same Philox stream, fp64 within 1e-12), noise
+    KS-distributed as the calibrated mechanism (p > 1e-4)."""
+    from scipy.stats import laplace, norm
+    from oracle import columnar as O
+    n = 30001  # odd: exercises the tail element
+    rng = np.random.default_rng(5)
+    vals = rng.integers(-50, 50, n).astype(np.float64)
+    keys = [f"k{i}" for i in range(n)]
+    sink, backend = _add_noise(list(zip(keys, vals.tolist())), kind, 1.0, 1e-6, 2, 3.0, seed=21)
+    out = list(sink)
+    assert [k for k, _ in out] == keys
+    got = np.array([v for _, v in out])
+    code, scale = CB.noise_mechanism_of(CB.recognise(sink).noise_fn)
+    _, _, seed_noise = backend._seeds()
+    want = O.add_noise(vals, code, scale, seed_noise)
+    assert np.allclose(got, want, rtol=1e-12, atol=1e-12 * scale)
+    dist = laplace(scale=6.0 / 1.0) if kind == "laplace" else norm(scale=dpc.compute_sigma(1.0, 1e-6, math.sqrt(2) * 3.0))
+    assert math.isclose(scale, dist.std() / (math.sqrt(2) if kind == "laplace" else 1.0), rel_tol=1e-12)
+    assert _ks(got - vals, dist.cdf) > 1e-4
+
+
+def test_add_dp_noise_device_columns(device):
+    """A (keys, values) ColumnTable of device tensors is noised in place on
+    the GPU; int64 values are converted as float(value)."""
+    import torch
+    from oracle import columnar as O
+    n = 4096
+    keys = torch.arange(n, device=device)
+    vals = torch.arange(n, device=device, dtype=torch.int64) * 3
+    sink, backend = _add_noise(pdp.ColumnTable({"pk": keys, "v": vals}), "laplace", 0.5, 0.0, 1, 1.0, seed=22)
+    out = list(sink)
+    assert [k for k, _ in out] == list(range(n))
+    _, _, seed_noise = backend._seeds()
+    want = O.add_noise(np.arange(n) * 3, N.NOISE_LAPLACE, 2.0, seed_noise)
+    assert np.allclose([v for _, v in out], want, rtol=1e-12, atol=1e-11)
+
+
+def test_add_noise_kernel_sharded_offsets_equal_whole(device):
+    """Shards noised with their global offsets equal the unsharded column."""
+    import torch
+    from pipelinedp_amd import executor as X
+    x = torch.randn(10001, dtype=torch.float64, device=device)
+    whole = X.add_noise(x, noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77)
+    a = X.add_noise(x[:4000].clone(), noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77)
+    b = X.add_noise(x[4000:].clone(), noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77, index_offset=4000)
+    assert torch.equal(torch.cat([a, b]), whole)
