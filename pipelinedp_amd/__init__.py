@@ -13,7 +13,7 @@ from pipelinedp_amd.aggregate_params import (AddDPNoiseParams, AggregateParams, 
                                              SelectPartitionsParams)
 from pipelinedp_amd.budget_accounting import (BudgetAccountant, MechanismSpec, NaiveBudgetAccountant,
                                               PLDBudgetAccountant)
-from pipelinedp_amd.columnar import ColumnTable
+from pipelinedp_amd.columnar import ColumnTable, DictColumn
 from pipelinedp_amd.columnar_backend import ColumnarBackend
 from pipelinedp_amd.combiners import Combiner, CustomCombiner
 from pipelinedp_amd.data_extractors import ColumnExtractor, DataExtractors, PreAggregateExtractors

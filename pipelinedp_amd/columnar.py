@@ -9,9 +9,11 @@ the data.  Anything else is extracted row-wise on the host (ingest, not
 compute) and then encoded.
 
 Keys are dictionary-encoded to dense int64 ids: integer keys that are already
-dense-ish are used as-is (identity dictionary); other keys go through
-pandas.factorize.  The dictionary decodes output partitions back to the
-user's keys.
+dense-ish are used as-is (identity dictionary); Arrow dictionary columns
+(Parquet's own dictionary pages, `ColumnTable.from_parquet`) keep their codes;
+other keys (strings, tuples, sparse integers) go through Arrow's
+dictionary_encode or pandas.factorize.  The dictionary decodes output
+partitions back to the user's keys.
 """
 import dataclasses
 from typing import Any, Mapping, Optional, Sequence
@@ -91,6 +93,46 @@ class ColumnTable:
         self.n_partitions = n_partitions
         self.partition_keys = partition_keys
 
+    @classmethod
+    def from_arrow(cls, table, columns: Optional[Sequence[str]] = None, **meta) -> "ColumnTable":
+        """ColumnTable over a pyarrow Table / RecordBatch (the columnar ingest
+        SURVEY §8(f) ranks next to the path).  Numeric columns without nulls
+        become NumPy views of the Arrow buffers (zero-copy for single-chunk
+        columns); dictionary columns become DictColumn (codes + dictionary,
+        no re-hashing); string / binary columns are dictionary-encoded by
+        Arrow (C++ hash) into DictColumn.  Nulls raise, as a None key or value
+        would fail in the reference's extractors and combiners."""
+        import pyarrow as pa
+        import pyarrow.compute as pc
+        names = list(columns) if columns is not None else list(table.column_names)
+        cols = {}
+        for name in names:
+            col = table.column(name)
+            if isinstance(col, pa.ChunkedArray):
+                col = col.combine_chunks() if col.num_chunks != 1 else col.chunk(0)
+            if col.null_count:
+                raise ValueError(f"column {name!r} has {col.null_count} nulls")
+            t = col.type
+            if pa.types.is_dictionary(t):
+                cols[name] = DictColumn.from_arrow(col)
+            elif pa.types.is_string(t) or pa.types.is_large_string(t) or pa.types.is_binary(t):
+                cols[name] = DictColumn.from_arrow(pc.dictionary_encode(col))
+            elif pa.types.is_integer(t) or pa.types.is_floating(t) or pa.types.is_boolean(t):
+                cols[name] = col.to_numpy(zero_copy_only=False)
+            else:
+                cols[name] = np.asarray(col.to_pylist(), dtype=object)
+        return cls(cols, **meta)
+
+    @classmethod
+    def from_parquet(cls, path, columns: Optional[Sequence[str]] = None,
+                     key_columns: Sequence[str] = (), **meta) -> "ColumnTable":
+        """Reads Parquet columns; `key_columns` are read as Arrow dictionary
+        arrays straight from Parquet's dictionary pages (no host hashing)."""
+        import pyarrow.parquet as pq
+        table = pq.read_table(path, columns=list(columns) if columns is not None else None,
+                              read_dictionary=list(key_columns) or None)
+        return cls.from_arrow(table, columns, **meta)
+
     @property
     def names(self):
         return list(self._cols)
@@ -114,6 +156,28 @@ class ColumnTable:
 
     def __iter__(self):
         return (_Row(self, i) for i in range(self._n))
+
+
+class DictColumn:
+    """A dictionary-encoded column: int64 `codes` into `dictionary` (an
+    object array of the keys).  Row-wise access decodes; encode_keys uses the
+    codes as the dense ids directly."""
+    __slots__ = ("codes", "dictionary")
+
+    def __init__(self, codes, dictionary):
+        self.codes = np.asarray(codes, dtype=np.int64)
+        self.dictionary = np.asarray(dictionary, dtype=object)
+
+    @classmethod
+    def from_arrow(cls, arr):
+        return cls(arr.indices.to_numpy(zero_copy_only=False).astype(np.int64, copy=False),
+                   arr.dictionary.to_pylist())
+
+    def __len__(self):
+        return len(self.codes)
+
+    def __getitem__(self, i):
+        return self.dictionary[self.codes[i]]
 
 
 def probe_columns(extract_fn, table: ColumnTable):
@@ -160,6 +224,20 @@ def _is_torch(x) -> bool:
 
 def encode_keys(values, declared_n: Optional[int] = None) -> EncodedKeys:
     """Dense int64 ids for a key column (identity when already dense)."""
+    if isinstance(values, DictColumn):
+        # Arrow dictionaries may hold unused or repeated entries: compact to
+        # the keys that occur, first-appearance order of the dictionary
+        import pandas as pd
+        if len(values.dictionary) == 0:
+            return EncodedKeys(np.zeros(0, np.int64), 1, np.zeros(0, dtype=object), {})
+        key_codes, uniques = pd.factorize(pd.Series(list(values.dictionary), dtype=object), sort=False)
+        used = np.zeros(len(uniques), dtype=bool)
+        remapped = key_codes[values.codes] if len(values.codes) else np.zeros(0, np.int64)
+        used[remapped] = True
+        dense = np.cumsum(used) - 1
+        decode = np.asarray(uniques, dtype=object)[used]
+        return EncodedKeys(dense[remapped].astype(np.int64), max(len(decode), 1), decode,
+                           {k: i for i, k in enumerate(decode)})
     if _is_torch(values):
         import torch
         if values.dtype not in (torch.int64, torch.int32):

@@ -577,8 +577,8 @@ class AggregateRun:
             if public is not None and pk_enc.decode is not None:
                 public_codes = np.asarray([pk_enc.encode[k] for k in public], dtype=np.int64)
         pid_t = None if pid_enc is None else \
-            torch.as_tensor(pid_enc.codes).to(device=device, dtype=torch.int64).contiguous()
-        pk_t = torch.as_tensor(pk_enc.codes).to(device=device, dtype=torch.int64).contiguous()
+            _h2d(pid_enc.codes, device, torch.int64)
+        pk_t = _h2d(pk_enc.codes, device, torch.int64)
         val_t = None
         value_kind = N.VALUE_NONE
         if self.prog.needs_values:
@@ -764,6 +764,8 @@ class AddNoiseRun:
         noised = out.cpu().numpy().tolist()
         if C._is_torch(keys):
             keys = keys.cpu().numpy()
+        elif isinstance(keys, C.DictColumn):
+            keys = keys.dictionary[keys.codes]
         return list(zip(np.asarray(keys).tolist() if isinstance(keys, np.ndarray) else keys, noised))
 
 
@@ -772,8 +774,20 @@ def _local_strategy(strategy):
     return agg.PartitionSelectionStrategy(_enum_value(strategy))
 
 
-def _host_or_device(col):
+def _h2d(col, device, dtype):
+    """Host column (possibly a read-only Arrow buffer view) -> contiguous
+    device tensor; device tensors are converted in place on the device."""
+    import torch
     if C._is_torch(col):
+        return col.to(device=device, dtype=dtype).contiguous()
+    arr = np.asarray(col)
+    if not arr.flags.writeable:  # only read; torch warns on non-writable arrays
+        arr = arr.copy()
+    return torch.from_numpy(arr).to(device=device, dtype=dtype).contiguous()
+
+
+def _host_or_device(col):
+    if C._is_torch(col) or isinstance(col, C.DictColumn):
         return col
     return np.asarray(col) if not isinstance(col, np.ndarray) else col
 
