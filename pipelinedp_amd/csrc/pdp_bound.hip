@@ -72,6 +72,9 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #ifndef PDP_BATCH_PRED
 #define PDP_BATCH_PRED 0
 #endif
+#ifndef PDP_GATHER_VALUES
+#define PDP_GATHER_VALUES 1
+#endif
 #ifndef PDP_INSERT_SKIP
 #define PDP_INSERT_SKIP 0
 #endif
@@ -1036,6 +1039,37 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
 #ifdef PDP_ABL_NO_B3
   return;
 #endif
+#if PDP_GATHER_VALUES
+  if (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) {
+    // B2.5: the kept rows' values replace their row keys in the row sketches,
+    // all of a thread's gathers in flight together (B3 then reads LDS only;
+    // same rows, same order, so the sums are unchanged)
+    constexpr int G = 4;
+    for (int t = 0; t < kp.linf; ++t) {
+      for (int64_t s0 = threadIdx.x; s0 < n_slots; s0 += (int64_t)G * blockDim.x) {
+        uint32_t rr[G];
+        bool live[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) {
+          const int64_t slot = s0 + (int64_t)u * blockDim.x;
+          live[u] = slot < n_slots && sk[slot] != kEmpty && (unsigned)t < cnt[slot];
+          rr[u] = live[u] ? (uint32_t)rsk[t * n_slots + slot] : 0u;
+        }
+        long long bits[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+          bits[u] = live[u] ? ((const long long*)value)[rr[u]] : 0;
+#pragma unroll
+        for (int u = 0; u < G; ++u)
+          if (live[u]) rsk[t * n_slots + s0 + (int64_t)u * blockDim.x] = (unsigned long long)bits[u];
+      }
+    }
+    __syncthreads();
+  }
+  const void* const b3_value = (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) ? nullptr : value;
+#else
+  const void* const b3_value = value;
+#endif
   unsigned* run = nullptr;
   if (RANGES) {
     // B3a: kept pairs per partition range -> this bucket's run starts
@@ -1066,7 +1100,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     PairSums ps;
     if (!KEEP_ALL_ROWS) {
       const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
-      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot, m, value, kp.clip, n_slots);
+      ps = pair_sums_from_rows<VALUE_KIND>(rsk + slot, m, b3_value, kp.clip, n_slots);
     } else if (VALUE_KIND != PDP_VALUE_NONE) {
       ps = pair_sums_from_totals((long long)c, tot[slot], tot[n_slots + slot], tot[2 * n_slots + slot], kp.clip);
     } else {

@@ -265,7 +265,12 @@ __device__ __forceinline__ PairSums pair_sums_from_rows(const unsigned long long
   for (long long t = 0; t < m; ++t) {
     double v;
     long long iv;
-    load_value<VALUE_KIND>(value, (uint32_t)rows[t * stride], &v, &iv);
+    if (value != nullptr) {
+      load_value<VALUE_KIND>(value, (uint32_t)rows[t * stride], &v, &iv);
+    } else {  // rows[] already holds the values' bits (bucket kernel B2.5)
+      iv = (long long)rows[t * stride];
+      v = VALUE_KIND == PDP_VALUE_I64 ? (double)iv : __longlong_as_double(iv);
+    }
     const double cv = fmin(fmax(v, cp.lo), cp.hi);
     if (cp.flags & PDP_SUM_PER_PARTITION) {
       raw += v;
