@@ -72,6 +72,16 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #ifndef PDP_BATCH_PRED
 #define PDP_BATCH_PRED 0
 #endif
+// level-1 scatter: prefetch the next stage's columns during this stage's LDS
+// passes (+32 VGPRs: 2 instead of 4 workgroups per CU)
+#ifndef PDP_L1_PREFETCH
+#define PDP_L1_PREFETCH 0
+#endif
+// level-1 scatter occupancy attribute (A/B: amdgpu_waves_per_eu(8, 8) caps
+// VGPRs at 64 and spills: 0.64 -> 0.96 ms; left to the compiler)
+#ifndef PDP_L1_OCC
+#define PDP_L1_OCC
+#endif
 #ifndef PDP_GATHER_VALUES
 #define PDP_GATHER_VALUES 1
 #endif
@@ -177,7 +187,7 @@ struct Ws {
   // global path
   uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
   // bucketed path
-  uint64_t counts_tm, counts, chunk_sums, cursor, super_base, keys1, rows1, keys2, rows2;
+  uint64_t counts_tm, counts, chunk_sums, cursor, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t total;
@@ -208,6 +218,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     w.cursor = off; off = align256(off + (uint64_t)p.n_buckets * 4);
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
+    w.super_tm = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
+    w.super_off = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
     const uint64_t kb = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;
     w.keys1 = off; off = align256(off + n * kb);
     w.rows1 = off; off = align256(off + n * 4);
@@ -391,7 +403,8 @@ __device__ __forceinline__ bool dead_key(uint64_t x, int rand_shift) {
 }
 
 __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t* __restrict__ pid,
-                                                            unsigned* __restrict__ counts_tm, unsigned* err) {
+                                                            unsigned* __restrict__ counts_tm,
+                                                            unsigned* __restrict__ super_tm, unsigned* err) {
   extern __shared__ unsigned hist[];
   for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) hist[b] = 0;
   __syncthreads();
@@ -424,7 +437,16 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
   __syncthreads();
   unsigned* row = counts_tm + (int64_t)blockIdx.x * kp.n_buckets;  // tile-major: coalesced
   for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) row[b] = hist[b];
+  // this tile's rows per super-bucket (the level-1 scatter's destinations)
+  const int64_t nsub = (int64_t)1 << kp.super_bits;
+  for (int64_t B = threadIdx.x; B < kp.n_supers; B += blockDim.x) {
+    unsigned v = 0;
+    const int64_t b1 = (B + 1) * nsub < kp.n_buckets ? (B + 1) * nsub : kp.n_buckets;
+    for (int64_t b = B * nsub; b < b1; ++b) v += hist[b];
+    super_tm[(int64_t)blockIdx.x * kp.n_supers + B] = v;
+  }
 }
+
 
 // [n_tiles][n_buckets] -> [n_buckets][n_tiles]
 __global__ void __launch_bounds__(kBlock) k_transpose_counts(const unsigned* __restrict__ in, int64_t rows,
@@ -467,19 +489,23 @@ constexpr int kMaxDest = 1024;
 template <bool COMPACT>
 using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>::type;
 
-template <typename K>
+// MAXD destinations per stage; the small form (<= 64 destinations, u8 tags)
+// is 37.6 KB with compact keys, four workgroups per CU instead of three
+template <typename K, int MAXD = kMaxDest>
 struct StageLds {
-  unsigned hist[kMaxDest];
-  unsigned start[kMaxDest];
-  unsigned gcur[kMaxDest];
+  using D = typename std::conditional<(MAXD <= 256), uint8_t, unsigned short>::type;
+  unsigned hist[MAXD];
+  unsigned start[MAXD];
+  unsigned gcur[MAXD];
   K keys[kStageRows];
   unsigned rows[kStageRows];
-  unsigned short dest[kStageRows];
+  D dest[kStageRows];
 };
+constexpr int kSmallDest = 64;
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
-template <typename K>
-__device__ __forceinline__ void stage_count(StageLds<K>& s, int ndest, const int (&d)[kStageItems],
+template <typename K, int MAXD>
+__device__ __forceinline__ void stage_count(StageLds<K, MAXD>& s, int ndest, const int (&d)[kStageItems],
                                             unsigned (&rank)[kStageItems]) {
   for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
   __syncthreads();
@@ -504,8 +530,8 @@ __device__ __forceinline__ void stage_count(StageLds<K>& s, int ndest, const int
 }
 
 // phase 2: place into the LDS stage, then write every run at gcur[dest]
-template <typename K>
-__device__ __forceinline__ void stage_write(StageLds<K>& s, int ndest, const int (&d)[kStageItems],
+template <typename K, int MAXD>
+__device__ __forceinline__ void stage_write(StageLds<K, MAXD>& s, int ndest, const int (&d)[kStageItems],
                                             const unsigned (&rank)[kStageItems], const K (&x)[kStageItems],
                                             const unsigned (&r)[kStageItems], K* __restrict__ out_keys,
                                             unsigned* __restrict__ out_rows) {
@@ -515,7 +541,7 @@ __device__ __forceinline__ void stage_write(StageLds<K>& s, int ndest, const int
     const unsigned slot = s.start[d[q]] + rank[q];
     s.keys[slot] = x[q];
     s.rows[slot] = r[q];
-    s.dest[slot] = (unsigned short)d[q];
+    s.dest[slot] = (typename StageLds<K, MAXD>::D)d[q];
   }
   __syncthreads();
   const unsigned total = s.start[ndest - 1] + s.hist[ndest - 1];
@@ -548,27 +574,21 @@ __device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpi
 
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
 template <bool COMPACT>
-__global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
+__global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
                                                              const uint8_t* __restrict__ allowed,
-                                                             const unsigned* __restrict__ counts,
+                                                             const unsigned* __restrict__ super_off,
                                                              const unsigned* __restrict__ super_base,
                                                              RecKey<COMPACT>* __restrict__ keys1,
                                                              unsigned* __restrict__ rows1, unsigned* err) {
   using K = RecKey<COMPACT>;
   extern __shared__ unsigned long long stage_raw[];
-  StageLds<K>& s = *reinterpret_cast<StageLds<K>*>(stage_raw);
+  static_assert(kMaxSupers <= kSmallDest, "level-1 destinations must fit the small stage");
+  StageLds<K, kSmallDest>& s = *reinterpret_cast<StageLds<K, kSmallDest>*>(stage_raw);
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
-  for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] = 0;
-  __syncthreads();
-  // rows of super-bucket B in tiles < t = sum over its buckets of (offset[b][t] - offset[b][0])
-  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) {
-    const unsigned v = counts[b * kp.n_tiles + t] - counts[b * kp.n_tiles];
-    if (v) atomicAdd(s.gcur + (b >> kp.super_bits), v);
-  }
-  __syncthreads();
-  for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += super_base[B];
+  // this tile's first row in each super-bucket region (k_super_scan)
+  for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] = super_base[B] + super_off[t * nd + B];
   __syncthreads();
   const int64_t t0 = t * kTileRows;
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
@@ -624,28 +644,45 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l1(KP kp, const int64_
         x[q] = (K)(is_dead ? (dead | midv) : pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift));
       }
     }
+#if PDP_L1_PREFETCH
     // next sub-chunk's column loads go out before this one's LDS passes
     if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
+#endif
+#ifdef PDP_ABL_L1_NOSTAGE
+    {
+      unsigned acc = 0;
+#pragma unroll
+      for (int q = 0; q < kStageItems; ++q) acc += (unsigned)d[q] ^ (unsigned)x[q] ^ r[q];
+      if (acc == 0x9E3779B9u) rows1[threadIdx.x] = acc;  // keeps the work live
+      continue;
+    }
+#endif
     unsigned rank[kStageItems];
     stage_count(s, nd, d, rank);
     stage_write(s, nd, d, rank, x, r, keys1, rows1);
     for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += s.hist[B];
     __syncthreads();
+#if !PDP_L1_PREFETCH
+    if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
+#endif
   }
 }
 
 // Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
-template <bool COMPACT>
+template <bool COMPACT, int MAXD>
 __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
                                                              unsigned* __restrict__ cursor,
                                                              const RecKey<COMPACT>* __restrict__ keys1,
                                                              const unsigned* __restrict__ rows1,
                                                              RecKey<COMPACT>* __restrict__ keys2,
                                                              unsigned* __restrict__ rows2) {
+#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
+  return;  // ablation: only the level-1 pass is meaningful
+#endif
   using K = RecKey<COMPACT>;
   constexpr int R = 16 / sizeof(K);  // records per 16-byte key load
   extern __shared__ unsigned long long stage_raw[];
-  StageLds<K>& s = *reinterpret_cast<StageLds<K>*>(stage_raw);
+  StageLds<K, MAXD>& s = *reinterpret_cast<StageLds<K, MAXD>*>(stage_raw);
   __shared__ int64_t s_first, s_base, s_r0, s_r1;
   const int nsub = 1 << kp.super_bits;
   if (threadIdx.x < 64) {
@@ -746,6 +783,25 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned x, unsigned* wsum, 
   __syncthreads();
   *total = wsum[nw];
   return wsum[w] + inc - x;
+}
+
+// super_off[t][B] = rows of super-bucket B in tiles < t (exclusive scan over
+// tiles, one workgroup per super-bucket): the level-1 scatter's per-tile
+// write offsets, read as one contiguous row per tile
+__global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __restrict__ super_tm,
+                                                       unsigned* __restrict__ super_off) {
+  __shared__ unsigned wsum[kBlock / 64 + 1];
+  const int64_t B = blockIdx.x;
+  unsigned carry = 0;
+  for (int64_t t0 = 0; t0 < kp.n_tiles; t0 += blockDim.x) {
+    const int64_t t = t0 + threadIdx.x;
+    const unsigned x = t < kp.n_tiles ? super_tm[t * kp.n_supers + B] : 0u;
+    unsigned total;
+    const unsigned ex = block_excl_scan(x, wsum, &total);
+    if (t < kp.n_tiles) super_off[t * kp.n_supers + B] = carry + ex;
+    carry += total;
+    __syncthreads();  // wsum is reused by the next chunk
+  }
 }
 
 // Per-wave LDS queue of candidate rows (capacity 2 waves' worth): rows that
@@ -931,6 +987,9 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
                                                                  const unsigned* __restrict__ offsets,
                                                                  const void* __restrict__ value,
                                                                  pdp_partition_accumulators acc, PairRecords rec) {
+#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
+  return;  // ablation: only the level-1 pass is meaningful
+#endif
   extern __shared__ unsigned long long smem[];
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
@@ -1124,6 +1183,9 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
 // then adds the partial sums with coalesced device atomics.
 __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec,
                                                                pdp_partition_accumulators acc) {
+#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
+  return;  // ablation: only the level-1 pass is meaningful
+#endif
   extern __shared__ unsigned long long smem[];
   double* s0 = (double*)smem;               // [kRangeParts] sum
   double* s1 = s0 + kRangeParts;            // normalized sum
@@ -1361,26 +1423,33 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
 
 template <bool COMPACT>
 int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
-                   const uint8_t* allowed, const unsigned* counts, const unsigned* super_base, unsigned* cursor,
+                   const uint8_t* allowed, const unsigned* super_off, const unsigned* super_base, unsigned* cursor,
                    char* ws, const Ws& w, unsigned* err) {
   using K = RecKey<COMPACT>;
-  const size_t lds = sizeof(StageLds<K>);
+  const size_t lds = sizeof(StageLds<K, kSmallDest>);
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<COMPACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l2<COMPACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
   PDP_PROF_BEGIN("k_scatter_l1", st);
   hipLaunchKernelGGL(k_scatter_l1<COMPACT>, dim3((unsigned)p.n_tiles), dim3(kPartThreads), lds, st, kp, pid, pk,
-                     allowed, counts, super_base, (K*)(ws + w.keys1), (unsigned*)(ws + w.rows1), err);
+                     allowed, super_off, super_base, (K*)(ws + w.keys1), (unsigned*)(ws + w.rows1), err);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
     // chunks: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
     const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kStageRows + 2 * p.n_supers + 1;
+    const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
+    const void* l2 = small ? (const void*)k_scatter_l2<COMPACT, kSmallDest> : (const void*)k_scatter_l2<COMPACT, kMaxDest>;
+    const size_t lds2 = small ? sizeof(StageLds<K, kSmallDest>) : sizeof(StageLds<K, kMaxDest>);
+    PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     PDP_PROF_BEGIN("k_scatter_l2", st);
-    hipLaunchKernelGGL(k_scatter_l2<COMPACT>, dim3((unsigned)n_l2), dim3(kPartThreads), lds, st, kp, super_base,
-                       cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1), (K*)(ws + w.keys2),
-                       (unsigned*)(ws + w.rows2));
+    if (small)
+      hipLaunchKernelGGL((k_scatter_l2<COMPACT, kSmallDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
+                         super_base, cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
+                         (K*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    else
+      hipLaunchKernelGGL((k_scatter_l2<COMPACT, kMaxDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
+                         super_base, cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
+                         (K*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -1516,8 +1585,14 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)hist_lds));
   PDP_PROF_BEGIN("k_part_hist", st);
+  unsigned* super_tm = (unsigned*)(ws + w.super_tm);
+  unsigned* super_off = (unsigned*)(ws + w.super_off);
   hipLaunchKernelGGL(k_part_hist, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
-                     counts_tm, err);
+                     counts_tm, super_tm, err);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_super_scan", st);
+  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_transpose_counts", st);
@@ -1535,10 +1610,10 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.key_format == PDP_KEYS_COMPACT)
-    return launch_scatter<true>(kp, p, st, privacy_id, partition_key, pk_allowed, counts, super_base, cursor, ws, w,
-                                err);
-  return launch_scatter<false>(kp, p, st, privacy_id, partition_key, pk_allowed, counts, super_base, cursor, ws, w,
-                               err);
+    return launch_scatter<true>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor, ws,
+                                w, err);
+  return launch_scatter<false>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor, ws,
+                               w, err);
 }
 
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,
