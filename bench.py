@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
 # wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for the
 # default C2 shape only; None otherwise.
-PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "v9_pmc.json")
+PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "v10_pmc.json")
 
 
 def pmc_traffic(n_rows):
@@ -66,10 +66,18 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto, 1 wide, 2 compact)")
+    ap.add_argument("--workload", choices=("c2", "c3"), default="c2",
+                    help="c2 (default, BASELINE configs[1]); c3: configs[2], 1e9 rows in total, "
+                         "Zipf(1.1) partition keys over 1e6 partitions, 1e7 privacy ids, L0=2, "
+                         "Linf=1, values U(0, 10), strong scaling over the GPUs")
     return ap.parse_args()
 
 
-def build_plan():
+# C3: N = 1e9 in total, pk Zipf(a=1.1) over P = 1e6, U = 1e7
+C3_ROWS, C3_PRIVACY_IDS, C3_PARTITIONS, C3_L0, C3_LINF, C3_ZIPF = 1_000_000_000, 10_000_000, 1_000_000, 2, 1, 1.1
+
+
+def build_plan(l0=L0, linf=LINF):
     """Noise / selection parameters exactly as DPEngine + NaiveBudgetAccountant
     derive them for this AggregateParams (3 mechanisms of weight 1: MEAN's
     count and normalized-sum Laplace mechanisms + the GENERIC selection)."""
@@ -78,12 +86,12 @@ def build_plan():
     from pipelinedp_amd import executor as X
     eps_each = EPS / 3
     mid = dpc.compute_middle(MIN_VALUE, MAX_VALUE)
-    b_count = dpc.laplace_diversity(eps_each, L0 * LINF)
-    b_nsum = dpc.laplace_diversity(eps_each, L0 * (MAX_VALUE - MIN_VALUE) / 2 * LINF)
-    bounding = X.BoundingSpec(l0=L0, linf=LINF, value_kind=N.VALUE_F64, flags=N.ACC_NSUM,
+    b_count = dpc.laplace_diversity(eps_each, l0 * linf)
+    b_nsum = dpc.laplace_diversity(eps_each, l0 * (MAX_VALUE - MIN_VALUE) / 2 * linf)
+    bounding = X.BoundingSpec(l0=l0, linf=linf, value_kind=N.VALUE_F64, flags=N.ACC_NSUM,
                               min_value=MIN_VALUE, max_value=MAX_VALUE, middle=mid)
     selection = X.SelectionSpec(strategy=N.SELECT_TRUNCATED_GEOMETRIC,
-                                keep_prob=dpc.truncated_geometric_keep_table(eps_each, DELTA, L0))
+                                keep_prob=dpc.truncated_geometric_keep_table(eps_each, DELTA, l0))
     ops = [X.MetricOpSpec(kind=N.OP_MEAN, noise_kind=N.NOISE_LAPLACE, out_col=(0, 1, 2),
                           scale=(b_count, b_nsum), middle=mid)]
     return bounding, selection, ops
@@ -125,17 +133,34 @@ def main():
         dist.init_process_group("nccl")
     device = torch.device("cuda", local_rank)
 
-    n = args.rows
-    U = max(1, (PRIVACY_IDS_PER_GPU * n) // ROWS_PER_GPU)
-    P = PARTITIONS
-    bounding, selection, ops = build_plan()
-
+    c3 = args.workload == "c3"
     g = torch.Generator(device=device)
     g.manual_seed(1000 + rank)
-    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
-    pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
-    value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
-        MIN_VALUE, MAX_VALUE)
+    if c3:  # strong scaling: 1e9 rows and 1e7 privacy ids in total, sharded by privacy id
+        n = C3_ROWS // world
+        U = C3_PRIVACY_IDS // world
+        P = C3_PARTITIONS
+        bounding, selection, ops = build_plan(C3_L0, C3_LINF)
+        pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+        w = torch.arange(1, P + 1, device=device, dtype=torch.float64).pow_(-C3_ZIPF)
+        cdf = torch.cumsum(w, 0)
+        cdf /= cdf[-1].clone()
+        pk = torch.empty(n, device=device, dtype=torch.int64)
+        for c0 in range(0, n, 1 << 27):  # bounded temporaries
+            c1 = min(n, c0 + (1 << 27))
+            u = torch.rand(c1 - c0, generator=g, device=device, dtype=torch.float64)
+            pk[c0:c1] = torch.searchsorted(cdf, u).clamp_(max=P - 1)
+        value = torch.rand(n, generator=g, device=device, dtype=torch.float64) * MAX_VALUE
+        del w, cdf
+    else:
+        n = args.rows
+        U = max(1, (PRIVACY_IDS_PER_GPU * n) // ROWS_PER_GPU)
+        P = PARTITIONS
+        bounding, selection, ops = build_plan()
+        pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+        pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
+        value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
+            MIN_VALUE, MAX_VALUE)
     torch.cuda.synchronize()
 
     P_pad, _ = parallel.partition_slices(P, world)
@@ -201,13 +226,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c3 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device",
+        "data": ("synthetic (uniform pid, Zipf(1.1) pk, U(0,10) values), generated on device" if c3 else
+                 "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device"),
         "config": {
-            "workload": "C2: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
-                        "(truncated geometric), L0=8, Linf=2",
+            "workload": ("C3: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
+                         "(truncated geometric), L0=2, Linf=1, 1e9 rows in total" if c3 else
+                         "C2: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
+                         "(truncated geometric), L0=8, Linf=2"),
             "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
             "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
         },
@@ -237,7 +265,7 @@ def main():
         "partitions_kept": kept,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
         result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows)
     if rank == 0:
         print(json.dumps(result), flush=True)
