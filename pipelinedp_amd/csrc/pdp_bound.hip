@@ -55,6 +55,8 @@ constexpr int kRangeParts = 1 << kRangeBits;
 constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= one block scan
 constexpr int kRangeThreads = 256;
 constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
+constexpr int64_t kRangeMaxGroup = 32;        // buckets per range-reduce workgroup, at most
+constexpr unsigned kRangeDirect = 256;        // records below which a workgroup adds them directly
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
 // 16-byte key loads in flight per lane in the bucket kernel's B1 / B2 passes
@@ -171,7 +173,10 @@ Plan make_plan(const pdp_bound_config* c) {
   }
   if (p.merge == PDP_MERGE_RANGES) {
     int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
-    p.range_group = g < 1 ? 1 : (g > kRangeThreads ? kRangeThreads : g);
+    // at most kRangeMaxGroup buckets per workgroup: a skewed (Zipf) key column
+    // puts most kept pairs in the first ranges, which then still spread over
+    // n_buckets / kRangeMaxGroup workgroups; near-empty workgroups exit early
+    p.range_group = g < 1 ? 1 : (g > kRangeMaxGroup ? kRangeMaxGroup : g);
     p.n_groups = (p.n_buckets + p.range_group - 1) / p.range_group;
   } else {
     p.n_ranges = 0;
@@ -489,8 +494,8 @@ constexpr int kMaxDest = 1024;
 template <bool COMPACT>
 using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>::type;
 
-// MAXD destinations per stage; the small form (<= 64 destinations, u8 tags)
-// is 37.6 KB with compact keys, four workgroups per CU instead of three
+// MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
+// fits four workgroups per CU with compact keys instead of three
 template <typename K, int MAXD = kMaxDest>
 struct StageLds {
   using D = typename std::conditional<(MAXD <= 256), uint8_t, unsigned short>::type;
@@ -501,7 +506,7 @@ struct StageLds {
   unsigned rows[kStageRows];
   D dest[kStageRows];
 };
-constexpr int kSmallDest = 64;
+constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four workgroups per CU
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
 template <typename K, int MAXD>
@@ -1198,13 +1203,6 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
   const int flags = kp.clip.flags;
   const bool f0 = flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION), f1 = flags & PDP_ACC_NSUM,
              f2 = flags & PDP_ACC_NSUM2, sum_int = flags & PDP_SUM_INT;
-  for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
-    pc[t] = 0;
-    cn[t] = 0;
-    s0[t] = 0.0;
-    s1[t] = 0.0;
-    s2[t] = 0.0;
-  }
   const int r = blockIdx.x;
   const int64_t p0 = (int64_t)r << kRangeBits;
   const int64_t b0 = (int64_t)blockIdx.y * kp.range_group;
@@ -1221,6 +1219,37 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
   unsigned total;
   const unsigned ex = block_excl_scan(len, wsum, &total);
   pre[threadIdx.x] = ex;
+  if (total == 0) return;  // block-uniform
+  __syncthreads();
+  if (total < kRangeDirect) {  // few records: straight into the accumulators
+    for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
+      int lo = 0, hi = (int)nb - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t idx = start[lo] + (i - pre[lo]);
+      const unsigned long long key = rec.key[idx];
+      const int64_t p = (int64_t)(key >> 32);
+      atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
+      if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key);
+      if (f0) {
+        if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(rec.f0[idx]));
+        else unsafeAtomicAdd((double*)acc.sum + p, rec.f0[idx]);
+      }
+      if (f1) unsafeAtomicAdd(acc.normalized_sum + p, rec.f1[idx]);
+      if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, rec.f2[idx]);
+    }
+    return;
+  }
+  for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
+    pc[t] = 0;
+    cn[t] = 0;
+    s0[t] = 0.0;
+    s1[t] = 0.0;
+    s2[t] = 0.0;
+  }
   __syncthreads();
   for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
     int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
