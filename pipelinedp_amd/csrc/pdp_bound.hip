@@ -19,7 +19,7 @@
 //    that every partitioning pass writes to <= 64 destinations per workgroup
 //    (long coalesced runs; ~2000 direct destinations thrash L2 5x).
 //    k_part_hist       per-tile histogram of bucket = pid >> bucket_bits  (8 B/row)
-//    k_transpose_counts, k_scan_*   bucket-major exclusive offsets
+//    k_bucket_totals, k_scan_*   rows per bucket (column sums) -> bucket starts
 //    k_scatter_l1      rows -> super-bucket order (pair key u64, row u32)  (16 B in, 12 B out)
 //    k_scatter_l2      super-bucket chunks -> bucket order                 (12 B in, 12 B out)
 //    k_bucket_bound    one workgroup per bucket, all sampling state in LDS:
@@ -216,10 +216,10 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     }
   } else {
     const uint64_t n_counts = (uint64_t)p.n_buckets * (uint64_t)p.n_tiles;
-    const uint64_t n_chunks = (n_counts + kScanChunk - 1) / kScanChunk;
+    const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
-    w.counts = off; off = align256(off + (n_counts + 1) * 4);
+    w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     w.cursor = off; off = align256(off + (uint64_t)p.n_buckets * 4);
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
@@ -453,21 +453,18 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
 }
 
 
-// [n_tiles][n_buckets] -> [n_buckets][n_tiles]
-__global__ void __launch_bounds__(kBlock) k_transpose_counts(const unsigned* __restrict__ in, int64_t rows,
-                                                             int64_t cols, unsigned* __restrict__ out) {
-  __shared__ unsigned tile[64][65];
-  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  for (int k = ty; k < 64; k += 4) {
-    const int64_t r = r0 + k, c = c0 + tx;
-    tile[k][tx] = (r < rows && c < cols) ? in[r * cols + c] : 0;
-  }
-  __syncthreads();
-  for (int k = ty; k < 64; k += 4) {
-    const int64_t c = c0 + k, r = r0 + tx;
-    if (c < cols && r < rows) out[c * rows + r] = tile[tx][k];
-  }
+// total[b] += sum over a chunk of tiles of counts_tm[t][b] (2-D grid: bucket
+// columns x tile chunks; integer atomics, so the result is exact)
+constexpr int kTotalsTiles = 32;
+__global__ void __launch_bounds__(kBlock) k_bucket_totals(const unsigned* __restrict__ counts_tm, int64_t n_tiles,
+                                                          int64_t n_buckets, unsigned* __restrict__ total) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_buckets) return;
+  const int64_t t0 = (int64_t)blockIdx.y * kTotalsTiles;
+  const int64_t t1 = t0 + kTotalsTiles < n_tiles ? t0 + kTotalsTiles : n_tiles;
+  unsigned v = 0;
+  for (int64_t t = t0; t < t1; ++t) v += counts_tm[t * n_buckets + b];
+  if (v) atomicAdd(total + b, v);
 }
 
 // cursor[b] = start of bucket b; super_base[B] = start of super-bucket B
@@ -475,10 +472,10 @@ __global__ void __launch_bounds__(kBlock) k_init_cursors(KP kp, const unsigned* 
                                                          unsigned* __restrict__ cursor,
                                                          unsigned* __restrict__ super_base) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < kp.n_buckets) cursor[i] = counts[i * kp.n_tiles];
+  if (i < kp.n_buckets) cursor[i] = counts[i];
   if (i <= kp.n_supers) {
     const int64_t b = i << kp.super_bits;
-    super_base[i] = counts[(b < kp.n_buckets ? b : kp.n_buckets) * kp.n_tiles];
+    super_base[i] = counts[b < kp.n_buckets ? b : kp.n_buckets];
   }
 }
 
@@ -794,9 +791,13 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned x, unsigned* wsum, 
 // tiles, one workgroup per super-bucket): the level-1 scatter's per-tile
 // write offsets, read as one contiguous row per tile
 __global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __restrict__ super_tm,
-                                                       unsigned* __restrict__ super_off) {
+                                                       unsigned* __restrict__ super_off,
+                                                       unsigned* __restrict__ bucket_total) {
   __shared__ unsigned wsum[kBlock / 64 + 1];
   const int64_t B = blockIdx.x;
+  // also clears the bucket totals k_bucket_totals accumulates into next
+  for (int64_t b = B * blockDim.x + threadIdx.x; b <= kp.n_buckets; b += (int64_t)gridDim.x * blockDim.x)
+    bucket_total[b] = 0;
   unsigned carry = 0;
   for (int64_t t0 = 0; t0 < kp.n_tiles; t0 += blockDim.x) {
     const int64_t t = t0 + threadIdx.x;
@@ -1033,8 +1034,8 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   }
   __syncthreads();
   const int64_t b = blockIdx.x;
-  const int64_t begin = offsets[b * kp.n_tiles];
-  const int64_t end = offsets[(b + 1) * kp.n_tiles];  // offsets has n_buckets*n_tiles+1 entries
+  const int64_t begin = offsets[b];
+  const int64_t end = offsets[b + 1];  // offsets has n_buckets + 1 entries
   const uint64_t bmask = (uint64_t)S - 1;
   auto conv = [&](RecKey<COMPACT> v) -> uint64_t {
     if constexpr (COMPACT) return expand_key(kp, hpid, v);
@@ -1602,10 +1603,9 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
                                 pk_allowed, ws, w);
   }
   // bucketed: histogram -> transpose -> scan -> cursors -> scatter (1 or 2 levels)
-  const int64_t n_counts = p.n_buckets * p.n_tiles;
-  unsigned* counts = (unsigned*)(ws + w.counts);
+  unsigned* counts = (unsigned*)(ws + w.counts);  // rows per bucket -> bucket starts
   if (cfg->n_rows == 0) {
-    PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (n_counts + 1) * 4, st));
+    PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (p.n_buckets + 1) * 4, st));
     return PDP_OK;
   }
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
@@ -1621,15 +1621,16 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_super_scan", st);
-  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off);
+  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off, counts);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_transpose_counts", st);
-  hipLaunchKernelGGL(k_transpose_counts, dim3((unsigned)((p.n_buckets + 63) / 64), (unsigned)((p.n_tiles + 63) / 64)),
+  PDP_PROF_BEGIN("k_bucket_totals", st);
+  hipLaunchKernelGGL(k_bucket_totals, dim3((unsigned)((p.n_buckets + kBlock - 1) / kBlock),
+                                           (unsigned)((p.n_tiles + kTotalsTiles - 1) / kTotalsTiles)),
                      dim3(kBlock), 0, st, counts_tm, p.n_tiles, p.n_buckets, counts);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  rc = scan_u32(counts, n_counts, chunk_sums, st);
+  rc = scan_u32(counts, p.n_buckets, chunk_sums, st);
   if (rc != PDP_OK) return rc;
   unsigned* cursor = (unsigned*)(ws + w.cursor);
   unsigned* super_base = (unsigned*)(ws + w.super_base);
