@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 4
+#define PDP_ABI_VERSION 5
 
 /* error codes */
 #define PDP_OK 0
@@ -256,6 +256,46 @@ int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noi
  * of bounds).  Reads it from the workspace of pdp_bound_contributions
  * (synchronises `stream`). */
 int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
+
+/* Dataset histograms: compute_dataset_histograms
+ * (pipeline_dp/dataset_histograms/computing_histograms.py:456-513) over one
+ * shard of dense columns privacy_id in [0, n_privacy_ids), partition in
+ * [0, n_partitions) and an optional value column (PDP_VALUE_NONE: sums 0).
+ * Integer histograms (logarithmic bins, _to_bin_lower_upper_logarithmic
+ * :28-47) are indexed densely: index b < 1000 is the bin [b, b + 1); index
+ * b >= 1000 is lower = q * 10^e with e = (b - 1000) / 900 + 1,
+ * q = (b - 1000) % 900 + 100, upper = lower + 10^e.  Their order in the
+ * int_* arrays: L0, L1, LINF, COUNT_PER_PARTITION, PRIVACY_ID_PER_PARTITION
+ * (HistogramType, histograms.py:60-76).  Float histograms (LINF_SUM,
+ * SUM_PER_PARTITION) have PDP_HIST_SUM_BUCKETS bins over np.linspace(min,
+ * max, PDP_HIST_SUM_BUCKETS + 1) (_min_max_lowers :346-370); bin i is
+ * [lowers[i], lowers[i + 1]]; float_n_lowers is PDP_HIST_SUM_BUCKETS + 1, 2
+ * when min == max (one bin [min, min]), 0 when empty.  A bin with count 0 is
+ * absent from the reference's histogram.  All outputs are device arrays the
+ * library zeroes and fills on `stream`; out-of-range keys set the error word
+ * that pdp_bound_error_flags reads from this workspace.  n_rows < 2^31. */
+#define PDP_HIST_LOG_BINS 16384
+#define PDP_HIST_SUM_BUCKETS 10000
+#define PDP_HIST_N_INT 5
+#define PDP_HIST_N_FLOAT 2
+
+typedef struct pdp_histogram_bins {
+  int64_t* int_count;      /* [PDP_HIST_N_INT][PDP_HIST_LOG_BINS] */
+  int64_t* int_sum;        /* [PDP_HIST_N_INT][PDP_HIST_LOG_BINS] */
+  int64_t* int_max;        /* [PDP_HIST_N_INT][PDP_HIST_LOG_BINS] */
+  int64_t* float_count;    /* [PDP_HIST_N_FLOAT][PDP_HIST_SUM_BUCKETS] */
+  double* float_sum;       /* [PDP_HIST_N_FLOAT][PDP_HIST_SUM_BUCKETS] */
+  double* float_max;       /* [PDP_HIST_N_FLOAT][PDP_HIST_SUM_BUCKETS] */
+  double* float_lowers;    /* [PDP_HIST_N_FLOAT][PDP_HIST_SUM_BUCKETS + 1] */
+  int32_t* float_n_lowers; /* [PDP_HIST_N_FLOAT] */
+} pdp_histogram_bins;
+
+int pdp_dataset_histograms_workspace_bytes(int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                           uint64_t* bytes);
+int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, const void* value,
+                           int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                           const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
+                           void* stream);
 
 /* Kernel profiler: when enabled, every kernel launch of this library is
  * bracketed by HIP events recorded on its launch stream.  enable(1) clears

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 4
+ABI_VERSION = 5
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 SELECT_ALL_NONEMPTY = 0
@@ -47,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "pdp_compact",
     "pdp_noise_metrics",
     "pdp_add_noise",
+    "pdp_dataset_histograms_workspace_bytes",
+    "pdp_dataset_histograms",
     "pdp_bound_error_flags",
     "pdp_profiler_enable",
     "pdp_profiler_report",
@@ -140,6 +142,19 @@ class MetricOp(ctypes.Structure):
     ]
 
 
+HIST_LOG_BINS = 16384
+HIST_SUM_BUCKETS = 10000
+HIST_N_INT = 5
+HIST_N_FLOAT = 2
+
+
+class HistogramBins(ctypes.Structure):
+    """pdp_histogram_bins: device output arrays of pdp_dataset_histograms (caller-owned)."""
+    _fields_ = [(name, ctypes.c_void_p) for name in (
+        "int_count", "int_sum", "int_max", "float_count", "float_sum", "float_max",
+        "float_lowers", "float_n_lowers")]
+
+
 _lock = threading.Lock()
 _lib = None
 
@@ -160,6 +175,9 @@ def _declare(lib):
         "pdp_noise_metrics": (ctypes.c_int, [P(MetricOp), i32, vp, i64, vp, i64,
                                              P(PartitionAccumulators), i32, vp, vp, i64, u64, vp]),
         "pdp_add_noise": (ctypes.c_int, [vp, i32, i64, i32, ctypes.c_double, u64, i64, vp, vp]),
+        "pdp_dataset_histograms_workspace_bytes": (ctypes.c_int, [i64, i64, i64, P(u64)]),
+        "pdp_dataset_histograms": (ctypes.c_int, [vp, vp, vp, i32, i64, i64, i64, P(HistogramBins),
+                                                  vp, u64, vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),

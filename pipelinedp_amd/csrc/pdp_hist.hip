@@ -1,0 +1,494 @@
+// pdp_hist.hip — dataset histograms (gfx950): the contribution and partition
+// statistics of pipeline_dp/dataset_histograms/computing_histograms.py
+// (compute_dataset_histograms, :456-513) over one shard of dense columns.
+//
+// The reference builds seven histograms with five group-bys and a distinct
+// (count_per_element / sum_per_key over pids, pairs and partitions).  Here the
+// dense codes turn every group-by but the (pid, pk) one into direct indexing:
+//   k_h_rows    per row: (pid, pk) into an open-addressing pair table (HBM,
+//               1.5 slots per row, linear probing) whose 32-byte slots hold
+//               key, value sum and row count, so a row's CAS and two atomics
+//               touch one cache line; rows per pid (L1), rows and value sum
+//               per partition
+//   k_h_pairs   per live pair: distinct partitions per pid (L0), distinct pids
+//               per partition, the Linf histogram, min/max of the pair sums
+//   k_h_ids     per pid: L0 / L1 histograms; per partition: count and
+//               privacy-id-count histograms, min/max of the partition sums
+//   k_h_lowers  np.linspace(min, max, 10001) bin lowers (_min_max_lowers,
+//               :346-370), bit-exact: separate fp64 multiply and add
+//   k_h_float   Linf-sum and sum-per-partition histograms (bisect_right over
+//               the lowers, _bin_lower_index :50-59); the pair histogram's
+//               counts and sums are privatised in LDS (120 KB per workgroup),
+//               bin maxima use a read-filtered atomicMax
+//   k_h_final   derived sums / maxima of the width-1 bins, fp64 maxima decoded
+//
+// Integer histograms use the logarithmic bins of
+// _to_bin_lower_upper_logarithmic (:28-47), indexed densely: lower < 1000 ->
+// index = lower (width 1, so bin sum = count * lower and max = lower, which
+// k_h_final fills in: the hot small bins only count, privatised in LDS);
+// lower = q * 10^e (q in [100, 999], e >= 1) -> 1000 + (e - 1) * 900 + q - 100.
+#include "pdp_internal.h"
+
+namespace pdp {
+namespace {
+
+constexpr int kLogBins = PDP_HIST_LOG_BINS;
+constexpr int kSumBuckets = PDP_HIST_SUM_BUCKETS;
+constexpr int kNLowers = kSumBuckets + 1;
+constexpr int kSmallBins = 1000;  // width-1 bins, counted in LDS
+constexpr uint64_t kMinTable = 1024;
+
+enum { H_L0 = 0, H_L1 = 1, H_LINF = 2, H_COUNT = 3, H_PIDS = 4 };
+enum { F_LINF_SUM = 0, F_PART_SUM = 1 };
+
+// pair-table slot: key + 1 (0 = empty, so the table clears with a memset)
+struct alignas(32) Slot {
+  unsigned long long key;
+  double sum;
+  unsigned cnt, pad;
+};
+
+uint64_t table_capacity(int64_t n_rows) {
+  uint64_t c = (uint64_t)n_rows + (uint64_t)n_rows / 2;
+  c = (c + 255) & ~(uint64_t)255;
+  return c < kMinTable ? kMinTable : c;
+}
+
+struct HWs {
+  uint64_t err, slots, l1, l0, prow, ppid, psum, minmax, fmax, total;
+};
+
+// err first: pdp_bound_error_flags reads the error word at offset 0
+HWs hlayout(int64_t n, int64_t U, int64_t P) {
+  HWs w{};
+  uint64_t off = 0;
+  const uint64_t C = table_capacity(n);
+  w.err = off; off = align256(off + 16);
+  w.slots = off; off = align256(off + C * sizeof(Slot));
+  w.l1 = off; off = align256(off + (uint64_t)U * 4);
+  w.l0 = off; off = align256(off + (uint64_t)U * 4);
+  w.prow = off; off = align256(off + (uint64_t)P * 4);
+  w.ppid = off; off = align256(off + (uint64_t)P * 4);
+  w.psum = off; off = align256(off + (uint64_t)P * 8);
+  w.minmax = off; off = align256(off + 4 * 8);        // ordered u64: pair min, max; partition min, max
+  w.fmax = off; off = align256(off + 2 * kSumBuckets * 8);  // ordered u64 bin maxima
+  w.total = off;
+  return w;
+}
+
+struct HT {
+  int64_t n, U, P;
+  int pk_bits;
+  uint64_t cap, pk_mask;
+};
+
+// order-preserving u64 image of an fp64 (for atomicMin/atomicMax)
+__device__ __forceinline__ unsigned long long ord(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+__device__ __forceinline__ double unord(unsigned long long o) {
+  const unsigned long long b = (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFULL) : ~o;
+  return __longlong_as_double((long long)b);
+}
+
+// _to_bin_lower_upper_logarithmic's lower as a dense bin index
+__device__ __forceinline__ int log_bin_index(unsigned long long v) {
+  unsigned long long bound = 1000;
+  while (v > bound) bound *= 10;
+  const unsigned long long rb = bound / 1000;
+  unsigned long long q = v / rb * rb;
+  if (q < kSmallBins) return (int)q;
+  int e = 0;
+  while (q >= 1000) { q /= 10; ++e; }
+  return kSmallBins + (e - 1) * 900 + (int)(q - 100);
+}
+
+struct IntHists {  // [5][kLogBins] each
+  unsigned long long* count;
+  unsigned long long* sum;
+  unsigned long long* max;
+};
+
+// one element of value v into integer histogram h: small bins count in LDS
+__device__ __forceinline__ void int_hist_add(const IntHists& H, unsigned* lds_counts, int h, int slot,
+                                             unsigned long long v) {
+  const int b = log_bin_index(v);
+  if (b < kSmallBins) {
+    atomicAdd(lds_counts + slot * kSmallBins + b, 1u);
+  } else {
+    const int64_t g = (int64_t)h * kLogBins + b;
+    atomicAdd(H.count + g, 1ULL);
+    atomicAdd(H.sum + g, v);
+    atomicMax(H.max + g, v);
+  }
+}
+
+__device__ __forceinline__ void flush_small(const IntHists& H, const unsigned* lds_counts, int slot, int h) {
+  for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) {
+    const unsigned c = lds_counts[slot * kSmallBins + b];
+    if (c) atomicAdd(H.count + (int64_t)h * kLogBins + b, (unsigned long long)c);
+  }
+}
+
+// x = pair key + 1 (never 0); slot index = high half of mix64(x) * cap
+__device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_t x) {
+  uint64_t h = __umul64hi(mix64(x), cap);
+  for (;;) {
+    unsigned long long* k = &slots[h].key;
+    const unsigned long long cur = *k;
+    if (cur == x) return slots + h;
+    if (cur == 0) {
+      const unsigned long long old = atomicCAS(k, 0ULL, (unsigned long long)x);
+      if (old == 0 || old == x) return slots + h;
+    }
+    h = h + 1 == cap ? 0 : h + 1;  // capacity 1.5 * rows: a free slot always exists
+  }
+}
+
+template <int VK>
+__device__ __forceinline__ double row_value(const void* value, int64_t i) {
+  if (VK == PDP_VALUE_F64) return ((const double*)value)[i];
+  if (VK == PDP_VALUE_I64) return (double)((const long long*)value)[i];
+  return 0.0;
+}
+
+template <int VK>
+__global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restrict__ pid,
+                                                   const int64_t* __restrict__ pk, const void* __restrict__ value,
+                                                   Slot* slots, unsigned* l1, unsigned* prow, double* psum,
+                                                   unsigned* err) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
+    const int64_t u = pid[i], k = pk[i];
+    if (u < 0 || u >= t.U || k < 0 || k >= t.P) {
+      atomicOr(err, 1u);
+      continue;
+    }
+    const double v = row_value<VK>(value, i);
+    Slot* s = table_insert(slots, t.cap, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1);
+    atomicAdd(&s->cnt, 1u);
+    if (VK != PDP_VALUE_NONE) atomicAdd(&s->sum, v);
+    atomicAdd(l1 + u, 1u);
+    atomicAdd(prow + k, 1u);
+    if (VK != PDP_VALUE_NONE) atomicAdd(psum + k, v);
+  }
+}
+
+// block-wide min/max of ordered fp64 images, one atomic pair per block
+__device__ __forceinline__ void block_minmax(unsigned long long mn, unsigned long long mx, unsigned long long* out) {
+  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int j = 1; j < kBlock / 64; ++j) {
+      mn = smn[j] < mn ? smn[j] : mn;
+      mx = smx[j] > mx ? smx[j] : mx;
+    }
+    if (mn != ~0ULL) atomicMin(out, mn);
+    if (mx != 0ULL) atomicMax(out + 1, mx);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict__ slots, unsigned* l0,
+                                                    unsigned* ppid, IntHists H, unsigned long long* minmax) {
+  __shared__ unsigned lds[kSmallBins];
+  for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) lds[b] = 0;
+  __syncthreads();
+  const int64_t C = (int64_t)t.cap;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < C; s += stride) {
+    const Slot sl = slots[s];
+    if (sl.key == 0) continue;
+    const unsigned long long x = sl.key - 1;
+    atomicAdd(l0 + (x >> t.pk_bits), 1u);
+    atomicAdd(ppid + (x & t.pk_mask), 1u);
+    int_hist_add(H, lds, H_LINF, 0, sl.cnt);
+    const unsigned long long o = ord(sl.sum);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+  }
+  block_minmax(mn, mx, minmax);  // contains __syncthreads: every thread reaches it
+  __syncthreads();
+  flush_small(H, lds, 0, H_LINF);
+}
+
+__global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned* __restrict__ l0,
+                                                  const unsigned* __restrict__ l1,
+                                                  const unsigned* __restrict__ prow,
+                                                  const unsigned* __restrict__ ppid,
+                                                  const double* __restrict__ psum, IntHists H,
+                                                  unsigned long long* minmax) {
+  __shared__ unsigned lds[4 * kSmallBins];
+  for (int b = threadIdx.x; b < 4 * kSmallBins; b += blockDim.x) lds[b] = 0;
+  __syncthreads();
+  const int64_t m = t.U > t.P ? t.U : t.P;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+    if (i < t.U) {
+      const unsigned r = l1[i];
+      if (r) {
+        int_hist_add(H, lds, H_L0, 0, l0[i]);
+        int_hist_add(H, lds, H_L1, 1, r);
+      }
+    }
+    if (i < t.P) {
+      const unsigned r = prow[i];
+      if (r) {
+        int_hist_add(H, lds, H_COUNT, 2, r);
+        int_hist_add(H, lds, H_PIDS, 3, ppid[i]);
+        const unsigned long long o = ord(psum[i]);
+        mn = o < mn ? o : mn;
+        mx = o > mx ? o : mx;
+      }
+    }
+  }
+  block_minmax(mn, mx, minmax + 2);
+  __syncthreads();
+  flush_small(H, lds, 0, H_L0);
+  flush_small(H, lds, 1, H_L1);
+  flush_small(H, lds, 2, H_COUNT);
+  flush_small(H, lds, 3, H_PIDS);
+}
+
+// np.linspace(mn, mx, 10001) (numpy function_base.linspace): step = delta /
+// div, y = i * step + start with separate roundings, y[-1] = stop; [mn, mn]
+// when mn == mx; no lowers when the histogram is empty.
+__global__ void __launch_bounds__(kBlock) k_h_lowers(const unsigned long long* __restrict__ minmax,
+                                                     double* lowers, int* n_lowers) {
+  const int f = blockIdx.y;
+  const unsigned long long omn = minmax[2 * f], omx = minmax[2 * f + 1];
+  const bool empty = omn == ~0ULL;
+  const double mn = unord(omn), mx = unord(omx);
+  double* L = lowers + (int64_t)f * kNLowers;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) n_lowers[f] = empty ? 0 : (mn == mx ? 2 : kNLowers);
+  if (empty || i >= kNLowers) return;
+  if (mn == mx) {
+    if (i < 2) L[i] = mn;
+    return;
+  }
+  const double delta = __dsub_rn(mx, mn);
+  const double step = __ddiv_rn(delta, (double)kSumBuckets);
+  double y;
+  if (step == 0.0) y = __dmul_rn(__ddiv_rn((double)i, (double)kSumBuckets), delta);
+  else y = __dmul_rn((double)i, step);
+  y = __dadd_rn(y, mn);
+  L[i] = i == kNLowers - 1 ? mx : y;
+}
+
+// bisect_right(lowers, v) - 1, the maximum in the last bin (_bin_lower_index)
+__device__ __forceinline__ int float_bin(const double* __restrict__ L, int nl, double v) {
+  const int nb = nl - 1;
+  if (nb <= 1) return 0;
+  const double span = L[nb] - L[0];
+  int b = (int)((v - L[0]) / span * (double)nb);
+  b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+  while (b + 1 < nb && L[b + 1] <= v) ++b;
+  while (b > 0 && L[b] > v) --b;
+  return b;
+}
+
+struct FloatHists {
+  unsigned long long* count;  // [2][kSumBuckets]
+  double* sum;
+  unsigned long long* omax;   // ordered images (workspace)
+};
+
+__device__ __forceinline__ void max_filtered(unsigned long long* omax, unsigned long long o) {
+  if (o > __hip_atomic_load(omax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(omax, o);
+}
+
+constexpr int kFloatBlock = 1024;
+
+// pair sums: counts and sums in LDS (one workgroup per CU, 16 waves), flushed
+// once; partition sums (P elements): global atomics
+__global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
+                                                         const unsigned* __restrict__ prow,
+                                                         const double* __restrict__ psum,
+                                                         const double* __restrict__ lowers,
+                                                         const int* __restrict__ n_lowers, FloatHists F) {
+  __shared__ unsigned lcnt[kSumBuckets];
+  __shared__ double lsum[kSumBuckets];
+  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
+    lcnt[b] = 0;
+    lsum[b] = 0.0;
+  }
+  __syncthreads();
+  const int64_t C = (int64_t)t.cap;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
+  if (nl0 > 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += stride) {
+      const Slot sl = slots[i];
+      if (sl.key == 0) continue;
+      const int b = float_bin(lowers, nl0, sl.sum);
+      atomicAdd(lcnt + b, 1u);
+      atomicAdd(lsum + b, sl.sum);
+      max_filtered(F.omax + b, ord(sl.sum));
+    }
+  }
+  if (nl1 > 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
+      if (prow[i] == 0) continue;
+      const double v = psum[i];
+      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + float_bin(lowers + kNLowers, nl1, v);
+      atomicAdd(F.count + g, 1ULL);
+      atomicAdd(F.sum + g, v);
+      max_filtered(F.omax + g, ord(v));
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
+    const unsigned c = lcnt[b];
+    if (c) {
+      atomicAdd(F.count + b, (unsigned long long)c);
+      atomicAdd(F.sum + b, lsum[b]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_h_final(IntHists H, FloatHists F, double* fmax_out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 5 * kSmallBins) {
+    const int h = i / kSmallBins, b = i % kSmallBins;
+    const int64_t g = (int64_t)h * kLogBins + b;
+    const unsigned long long c = H.count[g];
+    H.sum[g] = c * (unsigned long long)b;
+    H.max[g] = c ? (unsigned long long)b : 0ULL;
+  }
+  if (i < 2 * kSumBuckets) {
+    const unsigned long long o = F.omax[i];
+    fmax_out[i] = o ? unord(o) : 0.0;
+  }
+}
+
+// min images all ones, max images zero
+__global__ void k_h_init(unsigned long long* minmax) {
+  if (threadIdx.x < 4) minmax[threadIdx.x] = (threadIdx.x & 1) ? 0ULL : ~0ULL;
+}
+
+#define PDP_HLAUNCH(name, st, ...)          \
+  do {                                      \
+    PDP_PROF_BEGIN(name, st);               \
+    hipLaunchKernelGGL(__VA_ARGS__);        \
+    PDP_PROF_END(st);                       \
+    PDP_HIP_CHECK(hipGetLastError());       \
+  } while (0)
+
+}  // namespace
+}  // namespace pdp
+
+extern "C" {
+
+int pdp_dataset_histograms_workspace_bytes(int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                           uint64_t* bytes) {
+  if (bytes == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (n_rows < 0 || n_privacy_ids < 0 || n_partitions < 0)
+    return pdp::set_error(PDP_E_INVALID, "sizes must be >= 0");
+  *bytes = pdp::hlayout(n_rows, n_privacy_ids, n_partitions).total;
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, const void* value,
+                           int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                           const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
+                           void* stream) {
+  using namespace pdp;
+  if (out == nullptr || out->int_count == nullptr || out->int_sum == nullptr || out->int_max == nullptr ||
+      out->float_count == nullptr || out->float_sum == nullptr || out->float_max == nullptr ||
+      out->float_lowers == nullptr || out->float_n_lowers == nullptr)
+    return set_error(PDP_E_INVALID, "every pdp_histogram_bins output must be set");
+  if (n_rows < 0 || n_privacy_ids < 0 || n_partitions < 0) return set_error(PDP_E_INVALID, "sizes must be >= 0");
+  if (n_rows >= (int64_t)1 << 31) return set_error(PDP_E_UNSUPPORTED, "n_rows must be < 2^31 per shard");
+  if (value_kind != PDP_VALUE_NONE && value_kind != PDP_VALUE_F64 && value_kind != PDP_VALUE_I64)
+    return set_error(PDP_E_INVALID, "bad value_kind");
+  if (bits_for(n_privacy_ids) + bits_for(n_partitions) > 63)
+    return set_error(PDP_E_UNSUPPORTED, "pair key (privacy id bits + partition bits) exceeds 63 bits");
+  const HWs w = hlayout(n_rows, n_privacy_ids, n_partitions);
+  if (workspace == nullptr || workspace_bytes < w.total)
+    return set_error(PDP_E_INVALID, "workspace smaller than pdp_dataset_histograms_workspace_bytes");
+  if (n_rows > 0 && (privacy_id == nullptr || partition == nullptr ||
+                     (value_kind != PDP_VALUE_NONE && value == nullptr)))
+    return set_error(PDP_E_INVALID, "NULL column");
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  const uint64_t C = table_capacity(n_rows);
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.err, 0, 16, st));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.minmax - w.slots, st));  // slots .. psum
+  PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.fmax, 0, 2 * kSumBuckets * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_sum, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_max, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_count, 0, 2 * kSumBuckets * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_sum, 0, 2 * kSumBuckets * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_lowers, 0, 2 * kNLowers * 8, st));
+
+  HT t;
+  t.n = n_rows;
+  t.U = n_privacy_ids;
+  t.P = n_partitions;
+  t.pk_bits = bits_for(n_partitions);
+  t.cap = C;
+  t.pk_mask = (1ULL << t.pk_bits) - 1;
+  Slot* slots = (Slot*)(ws + w.slots);
+  unsigned* l1 = (unsigned*)(ws + w.l1);
+  unsigned* l0 = (unsigned*)(ws + w.l0);
+  unsigned* prow = (unsigned*)(ws + w.prow);
+  unsigned* ppid = (unsigned*)(ws + w.ppid);
+  double* psum = (double*)(ws + w.psum);
+  unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
+  unsigned* err = (unsigned*)(ws + w.err);
+  IntHists H{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
+             (unsigned long long*)out->int_max};
+  FloatHists F{(unsigned long long*)out->float_count, out->float_sum, (unsigned long long*)(ws + w.fmax)};
+
+  if (n_rows > 0) {
+    const unsigned g = grid_for(n_rows);
+    switch (value_kind) {
+      case PDP_VALUE_F64:
+        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_F64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
+                    value, slots, l1, prow, psum, err);
+        break;
+      case PDP_VALUE_I64:
+        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_I64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
+                    value, slots, l1, prow, psum, err);
+        break;
+      default:
+        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_NONE>, dim3(g), dim3(kBlock), 0, st, t, privacy_id,
+                    partition, value, slots, l1, prow, psum, err);
+    }
+    PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)C, 4096)), dim3(kBlock), 0, st, t, slots, l0,
+                ppid, H, minmax);
+    const int64_t m = n_privacy_ids > n_partitions ? n_privacy_ids : n_partitions;
+    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t, l0, l1, prow, ppid, psum,
+                H, minmax);
+  }
+  PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
+              out->float_lowers, out->float_n_lowers);
+  if (n_rows > 0) {
+    // one 1024-thread workgroup per CU (120 KB of LDS each)
+    int dev = 0, cus = 256;
+    PDP_HIP_CHECK(hipGetDevice(&dev));
+    PDP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t m = (int64_t)C > n_partitions ? (int64_t)C : n_partitions;
+    int64_t gf = (m + kFloatBlock - 1) / kFloatBlock;
+    gf = gf < cus ? gf : cus;
+    PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, slots, prow, psum,
+                out->float_lowers, out->float_n_lowers, F);
+  }
+  PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, H, F,
+              out->float_max);
+  return PDP_OK;
+}
+
+}  // extern "C"

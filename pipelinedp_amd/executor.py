@@ -379,3 +379,49 @@ def add_noise(values, *, noise_kind: int, scale: float, seed: int, index_offset:
                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(index_offset), _ptr(out), _stream(stream)),
             "pdp_add_noise")
     return out
+
+
+def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int, stream=None,
+                       workspace: Optional[BoundWorkspace] = None) -> Dict[str, "torch.Tensor"]:
+    """compute_dataset_histograms (computing_histograms.py:456-513) on device
+    columns of dense codes (`pdp_dataset_histograms`): returns the raw device
+    bin arrays (int_count/int_sum/int_max [5, LOG_BINS], float_count/
+    float_sum/float_max [2, SUM_BUCKETS], float_lowers [2, SUM_BUCKETS + 1],
+    float_n_lowers [2]); pipelinedp_amd.dataset_histograms turns them into
+    Histogram objects."""
+    torch = _torch()
+    lib = N.lib()
+    if not pk.is_cuda:
+        raise ValueError("columns must be device tensors")
+    device = pk.device
+    n = int(pk.numel())
+    _check_col(pid, "privacy_id", (torch.int64,), n, device)
+    _check_col(pk, "partition", (torch.int64,), n, device)
+    vk = N.VALUE_NONE
+    if value is not None:
+        _check_col(value, "value", (torch.int64, torch.float64), n, device)
+        vk = N.VALUE_I64 if value.dtype == torch.int64 else N.VALUE_F64
+    nbytes = ctypes.c_uint64()
+    N.check(lib.pdp_dataset_histograms_workspace_bytes(n, int(n_privacy_ids), int(n_partitions),
+                                                      ctypes.byref(nbytes)),
+            "pdp_dataset_histograms_workspace_bytes")
+    ws = (workspace or BoundWorkspace()).get(nbytes.value, device)
+    i64 = dict(dtype=torch.int64, device=device)
+    f64 = dict(dtype=torch.float64, device=device)
+    out = {
+        "int_count": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "int_sum": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "int_max": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "float_count": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **i64),
+        "float_sum": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
+        "float_max": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
+        "float_lowers": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS + 1), **f64),
+        "float_n_lowers": torch.empty(N.HIST_N_FLOAT, dtype=torch.int32, device=device),
+    }
+    s = N.HistogramBins(**{k: _ptr(v) for k, v in out.items()})
+    N.check(lib.pdp_dataset_histograms(_ptr(pid), _ptr(pk), _ptr(value) if value is not None else None, vk, n,
+                                       int(n_privacy_ids), int(n_partitions), ctypes.byref(s), _ptr(ws),
+                                       int(ws.numel()), _stream(stream)),
+            "pdp_dataset_histograms")
+    out["workspace"] = ws
+    return out

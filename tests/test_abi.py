@@ -20,6 +20,7 @@ STRUCTS = {
     "pdp_partition_accumulators": N.PartitionAccumulators,
     "pdp_select_config": N.SelectConfig,
     "pdp_metric_op": N.MetricOp,
+    "pdp_histogram_bins": N.HistogramBins,
 }
 
 
@@ -200,3 +201,24 @@ def test_null_arguments_are_rejected_before_device_work(lib):
     rc = lib.pdp_bound_contributions(ctypes.byref(cfg), None, None, None, None, ctypes.c_void_p(256),
                                      need.value, None)
     assert rc == -1 and b"key columns" in lib.pdp_last_error()
+
+
+def test_dataset_histograms_arguments(lib):
+    need = ctypes.c_uint64(0)
+    assert lib.pdp_dataset_histograms_workspace_bytes(1000, 100, 10, ctypes.byref(need)) == 0
+    # pair table (1.5 slots of 32 bytes per row) + per-pid / per-partition arrays
+    assert need.value >= 1500 * 32 + 100 * 8 + 10 * 16
+    assert lib.pdp_dataset_histograms_workspace_bytes(-1, 100, 10, ctypes.byref(need)) == -1
+    assert lib.pdp_dataset_histograms_workspace_bytes(10, 100, 10, None) == -1
+    out = N.HistogramBins()  # every output NULL: refused before device work
+    rc = lib.pdp_dataset_histograms(None, None, None, N.VALUE_F64, 10, 100, 10, ctypes.byref(out), None, 0, None)
+    assert rc == -1 and b"output" in lib.pdp_last_error()
+    fake = N.HistogramBins(*([256] * 8))  # never dereferenced: the shape checks fail first
+    rc = lib.pdp_dataset_histograms(None, None, None, N.VALUE_F64, 1 << 31, 100, 10, ctypes.byref(fake), None, 0,
+                                    None)
+    assert rc == -4
+    rc = lib.pdp_dataset_histograms(None, None, None, N.VALUE_F64, 10, 1 << 40, 1 << 30, ctypes.byref(fake),
+                                    None, 0, None)
+    assert rc == -4 and b"63 bits" in lib.pdp_last_error()
+    rc = lib.pdp_dataset_histograms(None, None, None, N.VALUE_F64, 10, 100, 10, ctypes.byref(fake), None, 0, None)
+    assert rc == -1 and b"workspace" in lib.pdp_last_error()

@@ -1,0 +1,158 @@
+"""GPU parity of the dataset histograms (csrc/pdp_hist.hip,
+compute_dataset_histograms) against the reference's own outputs (golden
+fixtures, oracle/gen_golden_hist.py) and the NumPy oracle (oracle/histograms.py).
+
+Bin bounds, counts, integer sums and maxima are exact; fp64 sums within 1e-9
+relative (the reference sums in insertion order, the GPU in atomic order).
+With dyadic values every sum is exact in any order, so bin membership of the
+float histograms is pinned exactly too."""
+import numpy as np
+import pytest
+
+from oracle import histograms as OH
+from pipelinedp_amd import ColumnExtractor, ColumnTable, DataExtractors
+from pipelinedp_amd import executor as X
+from pipelinedp_amd.dataset_histograms import computing_histograms as CH
+from tests import hist_util as HU
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    return torch.device("cuda", 0)
+
+
+def _check_all(got, want, what, exact=False):
+    for field in OH.HIST_FIELDS:
+        HU.assert_bins_equal(getattr(got, field).bins, want[field], f"{what}/{field}", exact=exact)
+
+
+def _run_codes(pid, pk, val, U=None, P=None):
+    import torch
+    d = _dev()
+    U = int(pid.max()) + 1 if U is None else U
+    P = int(pk.max()) + 1 if P is None else P
+    vt = None if val is None else torch.as_tensor(val, device=d)
+    raw = X.dataset_histograms(torch.as_tensor(pid, device=d), torch.as_tensor(pk, device=d), vt,
+                               n_privacy_ids=U, n_partitions=P)
+    return CH.histograms_from_device(raw)
+
+
+@pytest.mark.parametrize("fx", HU.fixtures(), ids=lambda f: f["name"])
+def test_reference_golden_rows(fx):
+    rows = [tuple(r) for r in fx["rows"]]
+    ext = DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
+    (got,) = CH.compute_dataset_histograms(rows, ext)
+    for field, exp in fx["expected"].items():
+        h = getattr(got, field)
+        assert h.name.value == exp["name"]
+        HU.assert_bins_equal(h.bins, exp["bins"], f"{fx['name']}/{field}", exact=fx["name"] != "strings")
+
+
+def test_reference_golden_column_table():
+    fx = [f for f in HU.fixtures() if f["name"] == "dyadic"][0]
+    rows = fx["rows"]
+    t = ColumnTable({"pid": np.asarray([r[0] for r in rows], dtype=np.int64),
+                     "pk": np.asarray([r[1] for r in rows], dtype=np.int64),
+                     "v": np.asarray([r[2] for r in rows], dtype=np.float64)})
+    ext = DataExtractors(ColumnExtractor("pid"), ColumnExtractor("pk"), ColumnExtractor("v"))
+    (got,) = CH.compute_dataset_histograms(t, ext)
+    for field, exp in fx["expected"].items():
+        HU.assert_bins_equal(getattr(got, field).bins, exp["bins"], field, exact=True)
+
+
+@pytest.mark.parametrize("case", ["uniform_dyadic", "zipf_heavy", "int_values", "no_values", "sparse_codes"])
+def test_against_oracle(case):
+    rng = np.random.default_rng({"uniform_dyadic": 1, "zipf_heavy": 2, "int_values": 3, "no_values": 4,
+                                 "sparse_codes": 5}[case])
+    n = 400_000
+    if case == "zipf_heavy":   # partitions with 10^3..10^5 rows: logarithmic bins above 1000
+        pid = rng.integers(0, 20_000, n)
+        pk = np.minimum(rng.zipf(1.3, n) - 1, 49_999)
+        val = rng.normal(5, 3, n)
+    elif case == "sparse_codes":  # declared ranges much larger than the codes used
+        pid = rng.integers(0, 1000, n) * 997
+        pk = rng.integers(0, 50, n) * 31
+        val = np.round(rng.normal(0, 4, n) * 4) / 4
+    else:
+        pid = rng.integers(0, 30_000, n)
+        pk = rng.integers(0, 3_000, n)
+        val = np.round(rng.normal(1, 2, n) * 16) / 16
+    if case == "int_values":
+        val = rng.integers(-50, 100, n)
+    if case == "no_values":
+        got = _run_codes(pid, pk, None)
+        want = OH.dataset_histograms(pid, pk, np.zeros(n))
+    else:
+        got = _run_codes(pid, pk, val, U=int(pid.max()) + 7, P=int(pk.max()) + 3)
+        want = OH.dataset_histograms(pid, pk, val)
+    _check_all(got, want, case, exact=case != "zipf_heavy")
+
+
+def test_single_row_and_constant_sums():
+    got = _run_codes(np.array([3]), np.array([1]), np.array([2.5]), U=5, P=2)
+    _check_all(got, OH.dataset_histograms([3], [1], [2.5]), "single")
+    assert got.linf_sum_contributions_histogram.bins[0].lower == got.linf_sum_contributions_histogram.bins[0].upper
+
+
+def test_empty_input():
+    got = _run_codes(np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0), U=4, P=4)
+    for field in OH.HIST_FIELDS:
+        h = getattr(got, field)
+        assert h.bins == [] and h.lower is None and h.upper is None
+
+
+def test_out_of_range_codes_raise():
+    """device-resident dense codes are taken as declared; one outside
+    [0, n) sets the kernel's error bit and the API raises"""
+    import torch
+    d = _dev()
+    t = ColumnTable({"pid": torch.tensor([0, 1], device=d), "pk": torch.tensor([0, 5], device=d),
+                     "v": torch.tensor([1.0, 1.0], device=d, dtype=torch.float64)},
+                    n_privacy_ids=2, n_partitions=3)
+    ext = DataExtractors(ColumnExtractor("pid"), ColumnExtractor("pk"), ColumnExtractor("v"))
+    with pytest.raises(ValueError):
+        CH.compute_dataset_histograms(t, ext)
+    pid = torch.tensor([0, 1, 2], device=d)
+    pk = torch.tensor([0, 9, 1], device=d)
+    raw = X.dataset_histograms(pid, pk, None, n_privacy_ids=3, n_partitions=2)
+    flags = np.zeros(1, np.uint32)
+    import ctypes
+    from pipelinedp_amd import _native as N
+    N.check(N.lib().pdp_bound_error_flags(X._ptr(raw["workspace"]), flags.ctypes.data_as(
+        ctypes.POINTER(ctypes.c_uint32)), X._stream()), "flags")
+    assert flags[0] & 1
+    h = CH.histograms_from_device(raw)   # the bad row is skipped, never read out of bounds
+    assert h.l1_contributions_histogram.total_sum() == 2
+
+
+def test_full_size_invariants():
+    """1e8 rows (C2's shape): totals every histogram must satisfy, checked
+    against torch group-bys on the device."""
+    import torch
+    d = _dev()
+    n, U, P = 100_000_000, 1_000_000, 100_000
+    g = torch.Generator(device=d).manual_seed(5)
+    pid = torch.randint(0, U, (n,), device=d, generator=g)
+    pk = torch.randint(0, P, (n,), device=d, generator=g)
+    val = torch.randint(-8, 9, (n,), device=d, generator=g).to(torch.float64) / 4
+    raw = X.dataset_histograms(pid, pk, val, n_privacy_ids=U, n_partitions=P)
+    h = CH.histograms_from_device(raw)
+    n_pairs = int(torch.unique(pid * P + pk).numel())
+    n_pids = int(torch.unique(pid).numel())
+    total = float(val.sum().item())
+    del pid, pk, raw
+    assert h.l1_contributions_histogram.total_sum() == n
+    assert h.l1_contributions_histogram.total_count() == n_pids
+    assert h.linf_contributions_histogram.total_sum() == n
+    assert h.count_per_partition_histogram.total_sum() == n
+    assert h.count_per_partition_histogram.total_count() == P
+    assert h.l0_contributions_histogram.total_sum() == n_pairs
+    assert h.linf_contributions_histogram.total_count() == n_pairs
+    assert h.count_privacy_id_per_partition.total_sum() == n_pairs
+    assert h.linf_sum_contributions_histogram.total_count() == n_pairs
+    assert h.sum_per_partition_histogram.total_count() == P
+    assert h.sum_per_partition_histogram.total_sum() == total  # quarter-integers: exact
+    assert h.linf_sum_contributions_histogram.total_sum() == total
+    assert len(h.linf_sum_contributions_histogram.bins) <= CH.NUMBER_OF_BUCKETS_SUM_HISTOGRAM
