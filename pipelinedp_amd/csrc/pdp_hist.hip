@@ -8,10 +8,11 @@
 //   k_h_rows    per row: (pid, pk) into an open-addressing pair table (HBM,
 //               1.5 slots per row, linear probing) whose 32-byte slots hold
 //               key, value sum and row count, so a row's CAS and two atomics
-//               touch one cache line; rows per pid (L1), rows and value sum
-//               per partition
-//   k_h_pairs   per live pair: distinct partitions per pid (L0), distinct pids
-//               per partition, the Linf histogram, min/max of the pair sums
+//               touch one cache line
+//   k_h_pairs   per live pair, one packed 64-bit atomic per pid and per
+//               partition: (distinct partitions << 32 | rows) per pid (L0, L1),
+//               (distinct pids << 32 | rows) per partition, + the partition's
+//               value sum; the Linf histogram, min/max of the pair sums
 //   k_h_ids     per pid: L0 / L1 histograms; per partition: count and
 //               privacy-id-count histograms, min/max of the partition sums
 //   k_h_lowers  np.linspace(min, max, 10001) bin lowers (_min_max_lowers,
@@ -55,7 +56,7 @@ uint64_t table_capacity(int64_t n_rows) {
 }
 
 struct HWs {
-  uint64_t err, slots, l1, l0, prow, ppid, psum, minmax, fmax, total;
+  uint64_t err, slots, pidstat, pkstat, psum, minmax, fmax, total;
 };
 
 // err first: pdp_bound_error_flags reads the error word at offset 0
@@ -65,10 +66,10 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
   const uint64_t C = table_capacity(n);
   w.err = off; off = align256(off + 16);
   w.slots = off; off = align256(off + C * sizeof(Slot));
-  w.l1 = off; off = align256(off + (uint64_t)U * 4);
-  w.l0 = off; off = align256(off + (uint64_t)U * 4);
-  w.prow = off; off = align256(off + (uint64_t)P * 4);
-  w.ppid = off; off = align256(off + (uint64_t)P * 4);
+  // packed counters, one 64-bit atomic per pair: per pid (distinct
+  // partitions << 32 | rows), per partition (distinct pids << 32 | rows)
+  w.pidstat = off; off = align256(off + (uint64_t)U * 8);
+  w.pkstat = off; off = align256(off + (uint64_t)P * 8);
   w.psum = off; off = align256(off + (uint64_t)P * 8);
   w.minmax = off; off = align256(off + 4 * 8);        // ordered u64: pair min, max; partition min, max
   w.fmax = off; off = align256(off + 2 * kSumBuckets * 8);  // ordered u64 bin maxima
@@ -78,7 +79,7 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
 
 struct HT {
   int64_t n, U, P;
-  int pk_bits;
+  int pk_bits, has_value;
   uint64_t cap, pk_mask;
 };
 
@@ -156,8 +157,7 @@ __device__ __forceinline__ double row_value(const void* value, int64_t i) {
 template <int VK>
 __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restrict__ pid,
                                                    const int64_t* __restrict__ pk, const void* __restrict__ value,
-                                                   Slot* slots, unsigned* l1, unsigned* prow, double* psum,
-                                                   unsigned* err) {
+                                                   Slot* slots, unsigned* err) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
     const int64_t u = pid[i], k = pk[i];
@@ -169,9 +169,6 @@ __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restri
     Slot* s = table_insert(slots, t.cap, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1);
     atomicAdd(&s->cnt, 1u);
     if (VK != PDP_VALUE_NONE) atomicAdd(&s->sum, v);
-    atomicAdd(l1 + u, 1u);
-    atomicAdd(prow + k, 1u);
-    if (VK != PDP_VALUE_NONE) atomicAdd(psum + k, v);
   }
 }
 
@@ -196,8 +193,9 @@ __device__ __forceinline__ void block_minmax(unsigned long long mn, unsigned lon
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict__ slots, unsigned* l0,
-                                                    unsigned* ppid, IntHists H, unsigned long long* minmax) {
+__global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict__ slots,
+                                                    unsigned long long* pidstat, unsigned long long* pkstat,
+                                                    double* psum, IntHists H, unsigned long long* minmax) {
   __shared__ unsigned lds[kSmallBins];
   for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) lds[b] = 0;
   __syncthreads();
@@ -208,8 +206,10 @@ __global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict
     const Slot sl = slots[s];
     if (sl.key == 0) continue;
     const unsigned long long x = sl.key - 1;
-    atomicAdd(l0 + (x >> t.pk_bits), 1u);
-    atomicAdd(ppid + (x & t.pk_mask), 1u);
+    const unsigned long long inc = (1ULL << 32) | sl.cnt;
+    atomicAdd(pidstat + (x >> t.pk_bits), inc);
+    atomicAdd(pkstat + (x & t.pk_mask), inc);
+    if (t.has_value) atomicAdd(psum + (x & t.pk_mask), sl.sum);
     int_hist_add(H, lds, H_LINF, 0, sl.cnt);
     const unsigned long long o = ord(sl.sum);
     mn = o < mn ? o : mn;
@@ -220,10 +220,8 @@ __global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict
   flush_small(H, lds, 0, H_LINF);
 }
 
-__global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned* __restrict__ l0,
-                                                  const unsigned* __restrict__ l1,
-                                                  const unsigned* __restrict__ prow,
-                                                  const unsigned* __restrict__ ppid,
+__global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned long long* __restrict__ pidstat,
+                                                  const unsigned long long* __restrict__ pkstat,
                                                   const double* __restrict__ psum, IntHists H,
                                                   unsigned long long* minmax) {
   __shared__ unsigned lds[4 * kSmallBins];
@@ -234,17 +232,17 @@ __global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned* __restri
   unsigned long long mn = ~0ULL, mx = 0ULL;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
     if (i < t.U) {
-      const unsigned r = l1[i];
-      if (r) {
-        int_hist_add(H, lds, H_L0, 0, l0[i]);
-        int_hist_add(H, lds, H_L1, 1, r);
+      const unsigned long long st = pidstat[i];
+      if (st) {
+        int_hist_add(H, lds, H_L0, 0, st >> 32);
+        int_hist_add(H, lds, H_L1, 1, st & 0xFFFFFFFFULL);
       }
     }
     if (i < t.P) {
-      const unsigned r = prow[i];
-      if (r) {
-        int_hist_add(H, lds, H_COUNT, 2, r);
-        int_hist_add(H, lds, H_PIDS, 3, ppid[i]);
+      const unsigned long long st = pkstat[i];
+      if (st) {
+        int_hist_add(H, lds, H_COUNT, 2, st & 0xFFFFFFFFULL);
+        int_hist_add(H, lds, H_PIDS, 3, st >> 32);
         const unsigned long long o = ord(psum[i]);
         mn = o < mn ? o : mn;
         mx = o > mx ? o : mx;
@@ -312,7 +310,7 @@ constexpr int kFloatBlock = 1024;
 // pair sums: counts and sums in LDS (one workgroup per CU, 16 waves), flushed
 // once; partition sums (P elements): global atomics
 __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
-                                                         const unsigned* __restrict__ prow,
+                                                         const unsigned long long* __restrict__ pkstat,
                                                          const double* __restrict__ psum,
                                                          const double* __restrict__ lowers,
                                                          const int* __restrict__ n_lowers, FloatHists F) {
@@ -338,7 +336,7 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
   }
   if (nl1 > 0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
-      if (prow[i] == 0) continue;
+      if (pkstat[i] == 0) continue;
       const double v = psum[i];
       const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + float_bin(lowers + kNLowers, nl1, v);
       atomicAdd(F.count + g, 1ULL);
@@ -439,12 +437,11 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
   t.P = n_partitions;
   t.pk_bits = bits_for(n_partitions);
   t.cap = C;
+  t.has_value = value_kind != PDP_VALUE_NONE;
   t.pk_mask = (1ULL << t.pk_bits) - 1;
   Slot* slots = (Slot*)(ws + w.slots);
-  unsigned* l1 = (unsigned*)(ws + w.l1);
-  unsigned* l0 = (unsigned*)(ws + w.l0);
-  unsigned* prow = (unsigned*)(ws + w.prow);
-  unsigned* ppid = (unsigned*)(ws + w.ppid);
+  unsigned long long* pidstat = (unsigned long long*)(ws + w.pidstat);
+  unsigned long long* pkstat = (unsigned long long*)(ws + w.pkstat);
   double* psum = (double*)(ws + w.psum);
   unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
   unsigned* err = (unsigned*)(ws + w.err);
@@ -457,20 +454,20 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
     switch (value_kind) {
       case PDP_VALUE_F64:
         PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_F64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                    value, slots, l1, prow, psum, err);
+                    value, slots, err);
         break;
       case PDP_VALUE_I64:
         PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_I64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                    value, slots, l1, prow, psum, err);
+                    value, slots, err);
         break;
       default:
         PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_NONE>, dim3(g), dim3(kBlock), 0, st, t, privacy_id,
-                    partition, value, slots, l1, prow, psum, err);
+                    partition, value, slots, err);
     }
-    PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)C, 4096)), dim3(kBlock), 0, st, t, slots, l0,
-                ppid, H, minmax);
+    PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)C, 4096)), dim3(kBlock), 0, st, t, slots, pidstat,
+                pkstat, psum, H, minmax);
     const int64_t m = n_privacy_ids > n_partitions ? n_privacy_ids : n_partitions;
-    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t, l0, l1, prow, ppid, psum,
+    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t, pidstat, pkstat, psum,
                 H, minmax);
   }
   PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
@@ -483,7 +480,7 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
     const int64_t m = (int64_t)C > n_partitions ? (int64_t)C : n_partitions;
     int64_t gf = (m + kFloatBlock - 1) / kFloatBlock;
     gf = gf < cus ? gf : cus;
-    PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, slots, prow, psum,
+    PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, slots, pkstat, psum,
                 out->float_lowers, out->float_n_lowers, F);
   }
   PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, H, F,

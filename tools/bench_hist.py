@@ -4,7 +4,8 @@ partitions, fp64 values, inputs resident in HBM.  One step = one
 pdp_dataset_histograms call (all seven histograms, bins left on the device).
 
 Prints one JSON line: rows/s, per-kernel HIP-event times, the roofline of the
-dominant kernel (algorithmic bytes: 24 B/row of pid + pk + value for k_h_rows)
+dominant kernel (algorithmic bytes: 24 B/row of pid + pk + value for k_h_rows,
+the 32-byte pair-table slots for the table scans)
 and a CPU baseline: the NumPy oracle (oracle/histograms.py, vectorised, one
 process) on a 4e6-row sample of the same workload.
 
@@ -55,7 +56,11 @@ def main():
     N.profiler_enable(False)
     kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
     dom = max(kernel_ms, key=kernel_ms.get)
-    dom_bytes = 24.0 * n if dom == "k_h_rows" else None
+    # algorithmic bytes per launch: k_h_rows streams pid + pk + value (24 B/row);
+    # k_h_pairs / k_h_float scan the pair table (1.5 slots of 32 B per row)
+    cap = max(1024, ((n + n // 2) + 255) // 256 * 256)
+    per_kernel_bytes = {"k_h_rows": 24.0 * n, "k_h_pairs": 32.0 * cap, "k_h_float": 32.0 * cap}
+    dom_bytes = per_kernel_bytes.get(dom)
     out = {
         "metric": "dataset histogram input rows/sec (compute_dataset_histograms device pass)",
         "value": n / dt, "unit": "rows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
