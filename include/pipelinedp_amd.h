@@ -297,6 +297,30 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
                            const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
                            void* stream);
 
+/* The same computation in two phases, for rows sharded by privacy id over
+ * ranks (pipelinedp_amd.executor.dataset_histograms with torch.distributed).
+ * _pairs zeroes `out` and builds the pair table, the per-pid and
+ * per-partition statistics and the Linf histogram.  Between the phases the
+ * caller reduces across ranks, at the byte offsets that _exchange_offsets
+ * gives into the workspace: the per-partition counters (uint64[n_partitions],
+ * sum), the per-partition value sums (double[n_partitions], sum), and the
+ * pair-sum minimum / maximum (two order-preserving uint64 words at
+ * minmax + 0 / + 8: min / max as unsigned integers).  _finish then builds
+ * the remaining histograms; partition_histograms = 0 skips the three
+ * per-partition histograms (so that one rank owns them).  The bins of all
+ * ranks are then merged: counts and sums added, maxima by maximum (only
+ * over bins with a count), lowers taken from any rank (pair histogram) or
+ * from the rank with partition_histograms = 1. */
+int pdp_dataset_histograms_pairs(const int64_t* privacy_id, const int64_t* partition, const void* value,
+                                 int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                 const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
+                                 void* stream);
+int pdp_dataset_histograms_exchange_offsets(int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                            uint64_t* pkstat, uint64_t* psum, uint64_t* minmax);
+int pdp_dataset_histograms_finish(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                  int32_t partition_histograms, const pdp_histogram_bins* out, void* workspace,
+                                  uint64_t workspace_bytes, void* stream);
+
 /* Kernel profiler: when enabled, every kernel launch of this library is
  * bracketed by HIP events recorded on its launch stream.  enable(1) clears
  * previous records; report() synchronises on them and returns, per kernel

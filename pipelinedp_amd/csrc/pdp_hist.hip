@@ -79,7 +79,7 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
 
 struct HT {
   int64_t n, U, P;
-  int pk_bits, has_value;
+  int pk_bits, has_value, do_parts;  // do_parts: per-partition histograms (multi-rank: one rank)
   uint64_t cap, pk_mask;
 };
 
@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned long long
         int_hist_add(H, lds, H_L1, 1, st & 0xFFFFFFFFULL);
       }
     }
-    if (i < t.P) {
+    if (t.do_parts && i < t.P) {
       const unsigned long long st = pkstat[i];
       if (st) {
         int_hist_add(H, lds, H_COUNT, 2, st & 0xFFFFFFFFULL);
@@ -396,11 +396,22 @@ int pdp_dataset_histograms_workspace_bytes(int64_t n_rows, int64_t n_privacy_ids
   return PDP_OK;
 }
 
-int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, const void* value,
-                           int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
-                           const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
-                           void* stream) {
-  using namespace pdp;
+}  // extern "C"
+
+namespace pdp {
+namespace {
+
+struct HCall {
+  HWs w;
+  HT t;
+  char* ws;
+  hipStream_t st;
+  IntHists H;
+  FloatHists F;
+};
+
+int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+               const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes, void* stream, HCall* c) {
   if (out == nullptr || out->int_count == nullptr || out->int_sum == nullptr || out->int_max == nullptr ||
       out->float_count == nullptr || out->float_sum == nullptr || out->float_max == nullptr ||
       out->float_lowers == nullptr || out->float_n_lowers == nullptr)
@@ -411,15 +422,34 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
     return set_error(PDP_E_INVALID, "bad value_kind");
   if (bits_for(n_privacy_ids) + bits_for(n_partitions) > 63)
     return set_error(PDP_E_UNSUPPORTED, "pair key (privacy id bits + partition bits) exceeds 63 bits");
-  const HWs w = hlayout(n_rows, n_privacy_ids, n_partitions);
-  if (workspace == nullptr || workspace_bytes < w.total)
+  c->w = hlayout(n_rows, n_privacy_ids, n_partitions);
+  if (workspace == nullptr || workspace_bytes < c->w.total)
     return set_error(PDP_E_INVALID, "workspace smaller than pdp_dataset_histograms_workspace_bytes");
-  if (n_rows > 0 && (privacy_id == nullptr || partition == nullptr ||
-                     (value_kind != PDP_VALUE_NONE && value == nullptr)))
-    return set_error(PDP_E_INVALID, "NULL column");
-  hipStream_t st = (hipStream_t)stream;
-  char* ws = (char*)workspace;
-  const uint64_t C = table_capacity(n_rows);
+  c->ws = (char*)workspace;
+  c->st = (hipStream_t)stream;
+  HT& t = c->t;
+  t.n = n_rows;
+  t.U = n_privacy_ids;
+  t.P = n_partitions;
+  t.pk_bits = bits_for(n_partitions);
+  t.cap = table_capacity(n_rows);
+  t.has_value = value_kind != PDP_VALUE_NONE;
+  t.do_parts = 1;
+  t.pk_mask = (1ULL << t.pk_bits) - 1;
+  c->H = IntHists{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
+                  (unsigned long long*)out->int_max};
+  c->F = FloatHists{(unsigned long long*)out->float_count, out->float_sum, (unsigned long long*)(c->ws + c->w.fmax)};
+  return PDP_OK;
+}
+
+// zero everything; k_h_rows + k_h_pairs (pair table, per-pid / per-partition
+// statistics, Linf histogram, pair-sum min / max)
+int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partition, const void* value,
+               int32_t value_kind, const pdp_histogram_bins* out) {
+  const HWs& w = c.w;
+  const HT& t = c.t;
+  char* ws = c.ws;
+  hipStream_t st = c.st;
   PDP_HIP_CHECK(hipMemsetAsync(ws + w.err, 0, 16, st));
   PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.minmax - w.slots, st));  // slots .. psum
   PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
@@ -430,62 +460,108 @@ int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, 
   PDP_HIP_CHECK(hipMemsetAsync(out->float_count, 0, 2 * kSumBuckets * 8, st));
   PDP_HIP_CHECK(hipMemsetAsync(out->float_sum, 0, 2 * kSumBuckets * 8, st));
   PDP_HIP_CHECK(hipMemsetAsync(out->float_lowers, 0, 2 * kNLowers * 8, st));
-
-  HT t;
-  t.n = n_rows;
-  t.U = n_privacy_ids;
-  t.P = n_partitions;
-  t.pk_bits = bits_for(n_partitions);
-  t.cap = C;
-  t.has_value = value_kind != PDP_VALUE_NONE;
-  t.pk_mask = (1ULL << t.pk_bits) - 1;
+  if (t.n == 0) return PDP_OK;
+  if (privacy_id == nullptr || partition == nullptr || (value_kind != PDP_VALUE_NONE && value == nullptr))
+    return set_error(PDP_E_INVALID, "NULL column");
   Slot* slots = (Slot*)(ws + w.slots);
-  unsigned long long* pidstat = (unsigned long long*)(ws + w.pidstat);
-  unsigned long long* pkstat = (unsigned long long*)(ws + w.pkstat);
-  double* psum = (double*)(ws + w.psum);
-  unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
   unsigned* err = (unsigned*)(ws + w.err);
-  IntHists H{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
-             (unsigned long long*)out->int_max};
-  FloatHists F{(unsigned long long*)out->float_count, out->float_sum, (unsigned long long*)(ws + w.fmax)};
-
-  if (n_rows > 0) {
-    const unsigned g = grid_for(n_rows);
-    switch (value_kind) {
-      case PDP_VALUE_F64:
-        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_F64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                    value, slots, err);
-        break;
-      case PDP_VALUE_I64:
-        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_I64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                    value, slots, err);
-        break;
-      default:
-        PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_NONE>, dim3(g), dim3(kBlock), 0, st, t, privacy_id,
-                    partition, value, slots, err);
-    }
-    PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)C, 4096)), dim3(kBlock), 0, st, t, slots, pidstat,
-                pkstat, psum, H, minmax);
-    const int64_t m = n_privacy_ids > n_partitions ? n_privacy_ids : n_partitions;
-    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t, pidstat, pkstat, psum,
-                H, minmax);
+  const unsigned g = grid_for(t.n);
+  switch (value_kind) {
+    case PDP_VALUE_F64:
+      PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_F64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
+                  value, slots, err);
+      break;
+    case PDP_VALUE_I64:
+      PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_I64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
+                  value, slots, err);
+      break;
+    default:
+      PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_NONE>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
+                  value, slots, err);
   }
+  PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)t.cap, 4096)), dim3(kBlock), 0, st, t, slots,
+              (unsigned long long*)(ws + w.pidstat), (unsigned long long*)(ws + w.pkstat), (double*)(ws + w.psum),
+              c.H, (unsigned long long*)(ws + w.minmax));
+  return PDP_OK;
+}
+
+// k_h_ids (partition part only when t.do_parts), lowers, float bins, final
+int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
+  const HWs& w = c.w;
+  const HT& t = c.t;
+  char* ws = c.ws;
+  hipStream_t st = c.st;
+  unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
+  const unsigned long long* pkstat = (const unsigned long long*)(ws + w.pkstat);
+  const double* psum = (const double*)(ws + w.psum);
+  const int64_t m = t.U > t.P ? t.U : t.P;
+  if (m > 0)
+    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t,
+                (const unsigned long long*)(ws + w.pidstat), pkstat, psum, c.H, minmax);
   PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
               out->float_lowers, out->float_n_lowers);
-  if (n_rows > 0) {
-    // one 1024-thread workgroup per CU (120 KB of LDS each)
-    int dev = 0, cus = 256;
-    PDP_HIP_CHECK(hipGetDevice(&dev));
-    PDP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int64_t m = (int64_t)C > n_partitions ? (int64_t)C : n_partitions;
-    int64_t gf = (m + kFloatBlock - 1) / kFloatBlock;
-    gf = gf < cus ? gf : cus;
-    PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, slots, pkstat, psum,
-                out->float_lowers, out->float_n_lowers, F);
-  }
-  PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, H, F,
-              out->float_max);
+  // one 1024-thread workgroup per CU (120 KB of LDS each)
+  int dev = 0, cus = 256;
+  PDP_HIP_CHECK(hipGetDevice(&dev));
+  PDP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t mf = (int64_t)t.cap > t.P ? (int64_t)t.cap : t.P;
+  int64_t gf = (mf + kFloatBlock - 1) / kFloatBlock;
+  gf = gf < cus ? gf : cus;
+  PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, (const Slot*)(ws + w.slots),
+              pkstat, psum, out->float_lowers, out->float_n_lowers, c.F);
+  PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
+              c.F, out->float_max);
   return PDP_OK;
+}
+
+}  // namespace
+}  // namespace pdp
+
+extern "C" {
+
+int pdp_dataset_histograms(const int64_t* privacy_id, const int64_t* partition, const void* value,
+                           int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                           const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
+                           void* stream) {
+  pdp::HCall c;
+  int rc = pdp::hist_check(value_kind, n_rows, n_privacy_ids, n_partitions, out, workspace, workspace_bytes, stream,
+                           &c);
+  if (rc == PDP_OK) rc = pdp::hist_pairs(c, privacy_id, partition, value, value_kind, out);
+  if (rc == PDP_OK) rc = pdp::hist_finish(c, out);
+  return rc;
+}
+
+int pdp_dataset_histograms_pairs(const int64_t* privacy_id, const int64_t* partition, const void* value,
+                                 int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                 const pdp_histogram_bins* out, void* workspace, uint64_t workspace_bytes,
+                                 void* stream) {
+  pdp::HCall c;
+  int rc = pdp::hist_check(value_kind, n_rows, n_privacy_ids, n_partitions, out, workspace, workspace_bytes, stream,
+                           &c);
+  return rc == PDP_OK ? pdp::hist_pairs(c, privacy_id, partition, value, value_kind, out) : rc;
+}
+
+int pdp_dataset_histograms_exchange_offsets(int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                            uint64_t* pkstat, uint64_t* psum, uint64_t* minmax) {
+  if (pkstat == nullptr || psum == nullptr || minmax == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (n_rows < 0 || n_privacy_ids < 0 || n_partitions < 0)
+    return pdp::set_error(PDP_E_INVALID, "sizes must be >= 0");
+  const pdp::HWs w = pdp::hlayout(n_rows, n_privacy_ids, n_partitions);
+  *pkstat = w.pkstat;
+  *psum = w.psum;
+  *minmax = w.minmax;
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms_finish(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_t n_partitions,
+                                  int32_t partition_histograms, const pdp_histogram_bins* out, void* workspace,
+                                  uint64_t workspace_bytes, void* stream) {
+  pdp::HCall c;
+  int rc = pdp::hist_check(value_kind, n_rows, n_privacy_ids, n_partitions, out, workspace, workspace_bytes, stream,
+                           &c);
+  if (rc != PDP_OK) return rc;
+  c.t.do_parts = partition_histograms != 0;
+  return pdp::hist_finish(c, out);
 }
 
 }  // extern "C"

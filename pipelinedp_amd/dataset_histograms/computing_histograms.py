@@ -103,7 +103,9 @@ def compute_dataset_histograms(col, data_extractors, backend=None) -> List[hist.
     contributions per privacy id (L0: distinct partitions, L1: rows), per
     (privacy id, partition) pair (Linf: rows, Linf-sum: value sum), and per
     partition (rows, distinct privacy ids, value sum).  Returns a one-element
-    list holding a DatasetHistograms."""
+    list holding a DatasetHistograms.  Under torch.distributed each rank
+    passes its shard of rows (sharded by privacy id) and every rank gets the
+    histograms of the whole dataset."""
     from pipelinedp_amd import executor as X
     from pipelinedp_amd.columnar_backend import _h2d, _host_or_device, _value_tensor
     import torch
@@ -111,6 +113,9 @@ def compute_dataset_histograms(col, data_extractors, backend=None) -> List[hist.
     pid_raw, pk_raw, val_raw, n_pid, n_pk = _columns(col, data_extractors)
     pid_enc = C.encode_keys(_host_or_device(pid_raw), n_pid)
     pk_enc = C.encode_keys(_host_or_device(pk_raw), n_pk)
+    from pipelinedp_amd import parallel
+    if parallel.world_info()[0] > 1:  # rows sharded by privacy id: one partition dictionary for all ranks
+        pk_enc = parallel.global_partition_keys(pk_enc)
     pid_t = _h2d(pid_enc.codes, device, torch.int64)
     pk_t = _h2d(pk_enc.codes, device, torch.int64)
     val_t = _value_tensor(val_raw, device) if val_raw is not None else None

@@ -382,13 +382,14 @@ def add_noise(values, *, noise_kind: int, scale: float, seed: int, index_offset:
 
 
 def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int, stream=None,
-                       workspace: Optional[BoundWorkspace] = None) -> Dict[str, "torch.Tensor"]:
+                       workspace: Optional[BoundWorkspace] = None, group=None) -> Dict[str, "torch.Tensor"]:
     """compute_dataset_histograms (computing_histograms.py:456-513) on device
     columns of dense codes (`pdp_dataset_histograms`): returns the raw device
     bin arrays (int_count/int_sum/int_max [5, LOG_BINS], float_count/
     float_sum/float_max [2, SUM_BUCKETS], float_lowers [2, SUM_BUCKETS + 1],
     float_n_lowers [2]); pipelinedp_amd.dataset_histograms turns them into
-    Histogram objects."""
+    Histogram objects.  Under torch.distributed (rows sharded by privacy id,
+    dense codes global) every rank returns the merged, global bins."""
     torch = _torch()
     lib = N.lib()
     if not pk.is_cuda:
@@ -419,9 +420,33 @@ def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         "float_n_lowers": torch.empty(N.HIST_N_FLOAT, dtype=torch.int32, device=device),
     }
     s = N.HistogramBins(**{k: _ptr(v) for k, v in out.items()})
-    N.check(lib.pdp_dataset_histograms(_ptr(pid), _ptr(pk), _ptr(value) if value is not None else None, vk, n,
-                                       int(n_privacy_ids), int(n_partitions), ctypes.byref(s), _ptr(ws),
-                                       int(ws.numel()), _stream(stream)),
-            "pdp_dataset_histograms")
+    from pipelinedp_amd import parallel
+    world, rank = parallel.world_info(group)
+    args = (int(n_privacy_ids), int(n_partitions))
+    if world == 1:
+        N.check(lib.pdp_dataset_histograms(_ptr(pid), _ptr(pk), _ptr(value) if value is not None else None, vk, n,
+                                           *args, ctypes.byref(s), _ptr(ws), int(ws.numel()), _stream(stream)),
+                "pdp_dataset_histograms")
+    else:
+        # rows sharded by privacy id: pid- and pair-level statistics are
+        # complete per rank; partition statistics and the pair-sum range are
+        # reduced between the phases, then the bins are merged
+        vk = parallel.all_ranks_max(vk, group)  # one value kind on every rank (a value-less shard says NONE)
+        N.check(lib.pdp_dataset_histograms_pairs(_ptr(pid), _ptr(pk), _ptr(value) if value is not None else None,
+                                                 vk, n, *args, ctypes.byref(s), _ptr(ws), int(ws.numel()),
+                                                 _stream(stream)),
+                "pdp_dataset_histograms_pairs")
+        offs = [ctypes.c_uint64() for _ in range(3)]
+        N.check(lib.pdp_dataset_histograms_exchange_offsets(n, *args, *[ctypes.byref(o) for o in offs]),
+                "pdp_dataset_histograms_exchange_offsets")
+        P = int(n_partitions)
+        pkstat = ws[offs[0].value:offs[0].value + 8 * P].view(torch.int64)
+        psum = ws[offs[1].value:offs[1].value + 8 * P].view(torch.float64)
+        minmax = ws[offs[2].value:offs[2].value + 16].view(torch.int64)
+        parallel.exchange_histogram_stats(pkstat, psum, minmax, group)
+        N.check(lib.pdp_dataset_histograms_finish(vk, n, *args, 1 if rank == 0 else 0, ctypes.byref(s), _ptr(ws),
+                                                  int(ws.numel()), _stream(stream)),
+                "pdp_dataset_histograms_finish")
+        parallel.merge_histogram_bins(out, group)
     out["workspace"] = ws
     return out

@@ -139,3 +139,53 @@ def all_ranks_any(flag: bool, group=None) -> bool:
     objs = [None] * world
     dist.all_gather_object(objs, bool(flag), group=group)
     return any(objs)
+
+
+def all_ranks_max(x: int, group=None) -> int:
+    import torch
+    import torch.distributed as dist
+    if world_info(group)[0] == 1:
+        return int(x)
+    t = torch.tensor([int(x)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+_SIGN = -(1 << 63)
+
+
+def exchange_histogram_stats(pkstat, psum, minmax, group=None):
+    """Between pdp_dataset_histograms_pairs and _finish (pipelinedp_amd.h):
+    sums the per-partition packed counters and value sums over ranks, and
+    takes the global minimum / maximum of the pair sums.  The min / max words
+    are order-preserving uint64 images; flipping the top bit makes their
+    order the signed int64 order that ReduceOp.MIN / MAX use."""
+    import torch.distributed as dist
+    dist.all_reduce(pkstat, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(psum, op=dist.ReduceOp.SUM, group=group)
+    signed = minmax ^ _SIGN
+    lo, hi = signed[0:1].clone(), signed[1:2].clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    minmax[0:1] = lo ^ _SIGN
+    minmax[1:2] = hi ^ _SIGN
+
+
+def merge_histogram_bins(out, group=None):
+    """Merges the bin arrays of pdp_dataset_histograms_finish over ranks:
+    counts and sums added, maxima by maximum over the bins that hold
+    elements, per-partition lowers from the rank that built them (the others
+    hold zeros and no lowers), pair lowers identical on every rank."""
+    import torch
+    import torch.distributed as dist
+    # mask with this rank's own counts, before they are summed
+    fmax = torch.where(out["float_count"] > 0, out["float_max"], torch.full_like(out["float_max"], -float("inf")))
+    for k in ("int_count", "int_sum", "float_count", "float_sum"):
+        dist.all_reduce(out[k], op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(out["int_max"], op=dist.ReduceOp.MAX, group=group)  # counts >= 0: empty bins hold 0
+    dist.all_reduce(fmax, op=dist.ReduceOp.MAX, group=group)
+    out["float_max"].copy_(torch.where(torch.isfinite(fmax), fmax, torch.zeros_like(fmax)))
+    part = out["float_lowers"][1:2].clone()  # only the partition-histogram rank wrote it
+    dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
+    out["float_lowers"][1:2] = part
+    dist.all_reduce(out["float_n_lowers"], op=dist.ReduceOp.MAX, group=group)

@@ -156,3 +156,52 @@ def test_full_size_invariants():
     assert h.sum_per_partition_histogram.total_sum() == total  # quarter-integers: exact
     assert h.linf_sum_contributions_histogram.total_sum() == total
     assert len(h.linf_sum_contributions_histogram.bins) <= CH.NUMBER_OF_BUCKETS_SUM_HISTOGRAM
+
+
+def _two_rank_data():
+    rng = np.random.default_rng(21)
+    n = 300_000
+    pid = rng.integers(0, 50_000, n)
+    pk = np.minimum(rng.zipf(1.4, n) - 1, 1999)
+    val = np.round(rng.normal(2, 5, n) * 8) / 8
+    return pid, pk, val
+
+
+def _hist_worker(rank, port, results):
+    import os
+    import torch.distributed as dist
+    from pipelinedp_amd import parallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        pid, pk, val = _two_rank_data()
+        mine = parallel.shard_by_privacy_id(pid, 2, rank)
+        h = _run_codes(pid[mine], pk[mine], val[mine], U=50_000, P=2000)
+        results[rank] = {f: [tuple(map(float, (b.lower, b.upper, b.count, b.sum, b.max)))
+                             for b in getattr(h, f).bins] for f in OH.HIST_FIELDS}
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_match_single_process():
+    """rows sharded by privacy id over two ranks (gloo exchange, both on this
+    GPU): every rank's merged histograms equal the single-process ones
+    (dyadic values: exact)."""
+    import socket
+    import torch.multiprocessing as mp
+    pid, pk, val = _two_rank_data()
+    single = _run_codes(pid, pk, val, U=50_000, P=2000)
+    _check_all(single, OH.dataset_histograms(pid, pk, val), "single", exact=True)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.spawn(_hist_worker, args=(port, results), nprocs=2, join=True)
+    res = dict(results)
+    assert all(isinstance(res[r], dict) for r in (0, 1)), res
+    for r in (0, 1):
+        for f in OH.HIST_FIELDS:
+            HU.assert_bins_equal(res[r][f], getattr(single, f).bins, f"rank{r}/{f}", exact=True)
