@@ -136,6 +136,8 @@ __device__ __forceinline__ void flush_small(const IntHists& H, const unsigned* l
 __device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_t x) {
   uint64_t h = __umul64hi(mix64(x), cap);
   for (;;) {
+    // plain load first: a CAS on every probe measured 19.1 ms vs 12.3 ms
+    // for k_h_rows at 1e8 rows (profiles/r01/h4_bench_hist.json)
     unsigned long long* k = &slots[h].key;
     const unsigned long long cur = *k;
     if (cur == x) return slots + h;
