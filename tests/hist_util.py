@@ -56,3 +56,27 @@ def assert_bins_equal(got, want, what, rtol=1e-9, exact=False):
         else:
             assert g[0] == w[0] and g[1] == w[1] and g[4] == w[4], f"{what}: {g} vs {w}"
             assert _close(g[3], w[3], tol), f"{what}: sum {g} vs {w}"
+
+
+# Known answers from the reference's tests
+# (tests/dataset_histograms/computing_histograms_test.py): (privacy_id,
+# partition) rows -> the expected bins of one histogram.
+KAT_L0 = [  # test_compute_l0_contributions_histogram
+    ([(1, 1), (1, 2), (2, 1)], [(1, 2, 1, 1, 1), (2, 3, 1, 2, 2)]),
+    ([(i, i) for i in range(100)], [(1, 2, 100, 100, 1)]),
+    ([(0, 0)], [(1, 2, 1, 1, 1)]),
+    ([(0, i) for i in range(1234)], [(1230, 1240, 1, 1234, 1234)]),
+    ([(0, i) for i in range(15)] + [(1, i) for i in range(10, 25)], [(15, 16, 2, 30, 15)]),
+]
+KAT_L1 = [  # test_compute_l1_contributions_histogram
+    ([(1, 1), (1, 2), (2, 1)], [(1, 2, 1, 1, 1), (2, 3, 1, 2, 2)]),
+    ([(i, i) for i in range(100)], [(1, 2, 100, 100, 1)]),
+    ([(0, 0)] * 100, [(100, 101, 1, 100, 100)]),
+    ([(0, i // 2) for i in range(1235)], [(1230, 1240, 1, 1235, 1235)]),
+    ([(0, i) for i in range(15)] + [(1, i) for i in range(10, 25)], [(15, 16, 2, 30, 15)]),
+]
+
+
+def kat_cases():
+    return ([("l0_contributions_histogram", rows, exp) for rows, exp in KAT_L0] +
+            [("l1_contributions_histogram", rows, exp) for rows, exp in KAT_L1])

@@ -205,3 +205,11 @@ def test_two_ranks_match_single_process():
     for r in (0, 1):
         for f in OH.HIST_FIELDS:
             HU.assert_bins_equal(res[r][f], getattr(single, f).bins, f"rank{r}/{f}", exact=True)
+
+
+@pytest.mark.parametrize("field,rows,expected", HU.kat_cases())
+def test_reference_test_known_answers(field, rows, expected):
+    """the reference tests' expected L0 / L1 bins, through the HIP path"""
+    ext = DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: 0)
+    (got,) = CH.compute_dataset_histograms(rows, ext)
+    HU.assert_bins_equal(getattr(got, field).bins, expected, field, exact=True)

@@ -101,3 +101,10 @@ def test_compute_dataset_histograms_needs_gpu():
     ext = DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
     with pytest.raises(RuntimeError):
         CH.compute_dataset_histograms([(1, 2, 3.0)], ext)
+
+
+@pytest.mark.parametrize("field,rows,expected", HU.kat_cases())
+def test_oracle_reference_test_known_answers(field, rows, expected):
+    pid, pk, _ = HU.codes([(u, k, 0.0) for u, k in rows])
+    got = OH.dataset_histograms(pid, pk, [0.0] * len(rows))[field]
+    HU.assert_bins_equal(got, expected, field, exact=True)
