@@ -42,7 +42,9 @@ constexpr uint64_t kMinTable = 1024;
 enum { H_L0 = 0, H_L1 = 1, H_LINF = 2, H_COUNT = 3, H_PIDS = 4 };
 enum { F_LINF_SUM = 0, F_PART_SUM = 1 };
 
-// pair-table slot: key + 1 (0 = empty, so the table clears with a memset)
+// pair-table slot: key + 1 (0 = empty, so the table clears with a memset);
+// cnt holds rows - 1, so the row whose CAS creates the pair skips the count
+// atomic (most pairs have one row)
 struct alignas(32) Slot {
   unsigned long long key;
   double sum;
@@ -133,8 +135,9 @@ __device__ __forceinline__ void flush_small(const IntHists& H, const unsigned* l
 }
 
 // x = pair key + 1 (never 0); slot index = high half of mix64(x) * cap
-__device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_t x) {
+__device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_t x, bool* created) {
   uint64_t h = __umul64hi(mix64(x), cap);
+  *created = false;
   for (;;) {
     // plain load first: a CAS on every probe measured 19.1 ms vs 12.3 ms
     // for k_h_rows at 1e8 rows (profiles/r01/h4_bench_hist.json)
@@ -143,6 +146,7 @@ __device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_
     if (cur == x) return slots + h;
     if (cur == 0) {
       const unsigned long long old = atomicCAS(k, 0ULL, (unsigned long long)x);
+      *created = old == 0;
       if (old == 0 || old == x) return slots + h;
     }
     h = h + 1 == cap ? 0 : h + 1;  // capacity 1.5 * rows: a free slot always exists
@@ -168,8 +172,9 @@ __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restri
       continue;
     }
     const double v = row_value<VK>(value, i);
-    Slot* s = table_insert(slots, t.cap, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1);
-    atomicAdd(&s->cnt, 1u);
+    bool created;
+    Slot* s = table_insert(slots, t.cap, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1, &created);
+    if (!created) atomicAdd(&s->cnt, 1u);
     if (VK != PDP_VALUE_NONE) atomicAdd(&s->sum, v);
   }
 }
@@ -208,11 +213,12 @@ __global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict
     const Slot sl = slots[s];
     if (sl.key == 0) continue;
     const unsigned long long x = sl.key - 1;
-    const unsigned long long inc = (1ULL << 32) | sl.cnt;
+    const unsigned rows = sl.cnt + 1;
+    const unsigned long long inc = (1ULL << 32) | rows;
     atomicAdd(pidstat + (x >> t.pk_bits), inc);
     atomicAdd(pkstat + (x & t.pk_mask), inc);
     if (t.has_value) atomicAdd(psum + (x & t.pk_mask), sl.sum);
-    int_hist_add(H, lds, H_LINF, 0, sl.cnt);
+    int_hist_add(H, lds, H_LINF, 0, rows);
     const unsigned long long o = ord(sl.sum);
     mn = o < mn ? o : mn;
     mx = o > mx ? o : mx;
