@@ -431,7 +431,8 @@ def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         # rows sharded by privacy id: pid- and pair-level statistics are
         # complete per rank; partition statistics and the pair-sum range are
         # reduced between the phases, then the bins are merged
-        vk = parallel.all_ranks_max(vk, group)  # one value kind on every rank (a value-less shard says NONE)
+        # each rank passes its own value kind: the kernels sum int64 and fp64
+        # values alike in fp64, so the ranks' partition sums add up
         N.check(lib.pdp_dataset_histograms_pairs(_ptr(pid), _ptr(pk), _ptr(value) if value is not None else None,
                                                  vk, n, *args, ctypes.byref(s), _ptr(ws), int(ws.numel()),
                                                  _stream(stream)),

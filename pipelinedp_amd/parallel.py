@@ -141,16 +141,6 @@ def all_ranks_any(flag: bool, group=None) -> bool:
     return any(objs)
 
 
-def all_ranks_max(x: int, group=None) -> int:
-    import torch
-    import torch.distributed as dist
-    if world_info(group)[0] == 1:
-        return int(x)
-    t = torch.tensor([int(x)], dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
-    return int(t.item())
-
-
 _SIGN = -(1 << 63)
 
 
