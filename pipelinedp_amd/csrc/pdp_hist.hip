@@ -57,17 +57,36 @@ uint64_t table_capacity(int64_t n_rows) {
   return c < kMinTable ? kMinTable : c;
 }
 
+// the pair table is split into regions of kRegionW partitions (pk >> 12),
+// each sized from its row count, so that k_h_pairs can sum per-partition
+// statistics of one region in LDS and flush them with contiguous atomics
+constexpr int kRegionBits = 12;
+constexpr int kRegionW = 1 << kRegionBits;
+constexpr int kRegionLdsMax = 16384;  // region count histogram in LDS up to here
+constexpr int kPairsBlock = 512;
+constexpr int kPairsChunk = 16384;    // slots per k_h_pairs workgroup
+
+int64_t n_regions(int64_t P) { return P > 0 ? (P + kRegionW - 1) >> kRegionBits : 1; }
+
+// slots: 1.5 per row + 64 of slack per region (every region with rows gets them)
+uint64_t slots_capacity(int64_t n_rows, int64_t P) {
+  return table_capacity(n_rows) + 64 * (uint64_t)n_regions(P);
+}
+
 struct HWs {
-  uint64_t err, slots, pidstat, pkstat, psum, minmax, fmax, total;
+  uint64_t err, slots, rbase, rchunks, pidstat, pkstat, psum, minmax, fmax, total;
 };
 
 // err first: pdp_bound_error_flags reads the error word at offset 0
 HWs hlayout(int64_t n, int64_t U, int64_t P) {
   HWs w{};
   uint64_t off = 0;
-  const uint64_t C = table_capacity(n);
+  const uint64_t C = slots_capacity(n, P);
+  const int64_t R = n_regions(P);
   w.err = off; off = align256(off + 16);
   w.slots = off; off = align256(off + C * sizeof(Slot));
+  w.rbase = off; off = align256(off + (uint64_t)(R + 1) * 4);  // region rows -> slot bases (exclusive scan)
+  w.rchunks = off; off = align256(off + (uint64_t)scan_chunk_sums_len(R + 1) * 4);
   // packed counters, one 64-bit atomic per pair: per pid (distinct
   // partitions << 32 | rows), per partition (distinct pids << 32 | rows)
   w.pidstat = off; off = align256(off + (uint64_t)U * 8);
@@ -82,7 +101,8 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
 struct HT {
   int64_t n, U, P;
   int pk_bits, has_value, do_parts;  // do_parts: per-partition histograms (multi-rank: one rank)
-  uint64_t cap, pk_mask;
+  uint64_t cap, pk_mask;             // cap: allocated slots (regions use a prefix of them)
+  int64_t R;                         // regions
 };
 
 // order-preserving u64 image of an fp64 (for atomicMin/atomicMax)
@@ -134,9 +154,12 @@ __device__ __forceinline__ void flush_small(const IntHists& H, const unsigned* l
   }
 }
 
-// x = pair key + 1 (never 0); slot index = high half of mix64(x) * cap
-__device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_t x, bool* created) {
-  uint64_t h = __umul64hi(mix64(x), cap);
+// x = pair key + 1 (never 0); slot = region base + high half of mix64(x) *
+// region capacity, linear probing inside the region
+__device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t base, uint64_t cap, uint64_t x,
+                                              bool* created) {
+  uint64_t h = base + __umul64hi(mix64(x), cap);
+  const uint64_t end = base + cap;
   *created = false;
   for (;;) {
     // plain load first: a CAS on every probe measured 19.1 ms vs 12.3 ms
@@ -149,7 +172,7 @@ __device__ __forceinline__ Slot* table_insert(Slot* slots, uint64_t cap, uint64_
       *created = old == 0;
       if (old == 0 || old == x) return slots + h;
     }
-    h = h + 1 == cap ? 0 : h + 1;  // capacity 1.5 * rows: a free slot always exists
+    h = h + 1 == end ? base : h + 1;  // region capacity > its rows: a free slot always exists
   }
 }
 
@@ -160,10 +183,43 @@ __device__ __forceinline__ double row_value(const void* value, int64_t i) {
   return 0.0;
 }
 
+// rows per region (valid rows only); LDS histogram when the regions fit
+template <bool LDS>
+__global__ void __launch_bounds__(kBlock) k_h_region_count(HT t, const int64_t* __restrict__ pid,
+                                                           const int64_t* __restrict__ pk, unsigned* rcnt) {
+  __shared__ unsigned lh[LDS ? kRegionLdsMax : 1];
+  if (LDS) {
+    for (int b = threadIdx.x; b < t.R; b += blockDim.x) lh[b] = 0;
+    __syncthreads();
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
+    const int64_t u = pid[i], k = pk[i];
+    if (u < 0 || u >= t.U || k < 0 || k >= t.P) continue;
+    if (LDS) atomicAdd(lh + (k >> kRegionBits), 1u);
+    else atomicAdd(rcnt + (k >> kRegionBits), 1u);
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < t.R; b += blockDim.x)
+      if (lh[b]) atomicAdd(rcnt + b, lh[b]);
+  }
+}
+
+// region rows -> region slot capacity (1.5 per row + 64), scanned afterwards
+__global__ void __launch_bounds__(kBlock) k_h_region_caps(int64_t R, unsigned* rcnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < R) {
+    const unsigned c = rcnt[r];
+    rcnt[r] = c ? c + c / 2 + 64 : 0u;
+  }
+}
+
 template <int VK>
 __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restrict__ pid,
                                                    const int64_t* __restrict__ pk, const void* __restrict__ value,
-                                                   Slot* slots, unsigned* err) {
+                                                   const unsigned* __restrict__ rbase, Slot* slots,
+                                                   unsigned* err) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
     const int64_t u = pid[i], k = pk[i];
@@ -173,7 +229,9 @@ __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restri
     }
     const double v = row_value<VK>(value, i);
     bool created;
-    Slot* s = table_insert(slots, t.cap, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1, &created);
+    const int64_t r = k >> kRegionBits;
+    const unsigned b0 = rbase[r];
+    Slot* s = table_insert(slots, b0, rbase[r + 1] - b0, (((uint64_t)u << t.pk_bits) | (uint64_t)k) + 1, &created);
     if (!created) atomicAdd(&s->cnt, 1u);
     if (VK != PDP_VALUE_NONE) atomicAdd(&s->sum, v);
   }
@@ -181,7 +239,7 @@ __global__ void __launch_bounds__(kBlock) k_h_rows(HT t, const int64_t* __restri
 
 // block-wide min/max of ordered fp64 images, one atomic pair per block
 __device__ __forceinline__ void block_minmax(unsigned long long mn, unsigned long long mx, unsigned long long* out) {
-  __shared__ unsigned long long smn[kBlock / 64], smx[kBlock / 64];
+  __shared__ unsigned long long smn[16], smx[16];
   for (int o = 32; o > 0; o >>= 1) {
     const unsigned long long a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
     mn = a < mn ? a : mn;
@@ -191,7 +249,7 @@ __device__ __forceinline__ void block_minmax(unsigned long long mn, unsigned lon
   if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int j = 1; j < kBlock / 64; ++j) {
+    for (int j = 1; j < (int)(blockDim.x >> 6); ++j) {
       mn = smn[j] < mn ? smn[j] : mn;
       mx = smx[j] > mx ? smx[j] : mx;
     }
@@ -200,28 +258,66 @@ __device__ __forceinline__ void block_minmax(unsigned long long mn, unsigned lon
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_h_pairs(HT t, const Slot* __restrict__ slots,
-                                                    unsigned long long* pidstat, unsigned long long* pkstat,
-                                                    double* psum, IntHists H, unsigned long long* minmax) {
+// one workgroup per chunk of kPairsChunk slots; per region the chunk
+// touches, the region's per-partition statistics are summed in LDS and
+// flushed with contiguous atomics; per-pid statistics stay global atomics
+__global__ void __launch_bounds__(kPairsBlock) k_h_pairs(HT t, const Slot* __restrict__ slots,
+                                                         const unsigned* __restrict__ rbase,
+                                                         unsigned long long* pidstat, unsigned long long* pkstat,
+                                                         double* psum, IntHists H, unsigned long long* minmax) {
   __shared__ unsigned lds[kSmallBins];
+  __shared__ unsigned long long lstat[kRegionW];
+  __shared__ double lsum[kRegionW];
+  __shared__ int64_t r_first;
   for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) lds[b] = 0;
+  const int64_t used = rbase[t.R];
+  const int64_t s0 = (int64_t)blockIdx.x * kPairsChunk;
+  const int64_t s1 = s0 + kPairsChunk < used ? s0 + kPairsChunk : used;
+  if (threadIdx.x == 0) {  // last region with base <= s0
+    int64_t lo = 0, hi = t.R;  // rbase[lo] <= s0 < rbase[hi] (when s0 < used)
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)rbase[mid] <= s0) lo = mid;
+      else hi = mid;
+    }
+    r_first = lo;
+  }
   __syncthreads();
-  const int64_t C = (int64_t)t.cap;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   unsigned long long mn = ~0ULL, mx = 0ULL;
-  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < C; s += stride) {
-    const Slot sl = slots[s];
-    if (sl.key == 0) continue;
-    const unsigned long long x = sl.key - 1;
-    const unsigned rows = sl.cnt + 1;
-    const unsigned long long inc = (1ULL << 32) | rows;
-    atomicAdd(pidstat + (x >> t.pk_bits), inc);
-    atomicAdd(pkstat + (x & t.pk_mask), inc);
-    if (t.has_value) atomicAdd(psum + (x & t.pk_mask), sl.sum);
-    int_hist_add(H, lds, H_LINF, 0, rows);
-    const unsigned long long o = ord(sl.sum);
-    mn = o < mn ? o : mn;
-    mx = o > mx ? o : mx;
+  for (int64_t r = r_first; s0 < s1 && r < t.R && (int64_t)rbase[r] < s1; ++r) {
+    const int64_t a = (int64_t)rbase[r] > s0 ? (int64_t)rbase[r] : s0;
+    const int64_t e = (int64_t)rbase[r + 1] < s1 ? (int64_t)rbase[r + 1] : s1;
+    if (a >= e) continue;  // empty region (uniform across the workgroup)
+    for (int j = threadIdx.x; j < kRegionW; j += blockDim.x) {
+      lstat[j] = 0;
+      lsum[j] = 0.0;
+    }
+    __syncthreads();
+    for (int64_t s = a + threadIdx.x; s < e; s += blockDim.x) {
+      const Slot sl = slots[s];
+      if (sl.key == 0) continue;
+      const unsigned long long x = sl.key - 1;
+      const unsigned rows = sl.cnt + 1;
+      const unsigned long long inc = (1ULL << 32) | rows;
+      const int j = (int)((x & t.pk_mask) & (kRegionW - 1));
+      atomicAdd(pidstat + (x >> t.pk_bits), inc);
+      atomicAdd(lstat + j, inc);
+      if (t.has_value) atomicAdd(lsum + j, sl.sum);
+      int_hist_add(H, lds, H_LINF, 0, rows);
+      const unsigned long long o = ord(sl.sum);
+      mn = o < mn ? o : mn;
+      mx = o > mx ? o : mx;
+    }
+    __syncthreads();
+    const int64_t p0 = r << kRegionBits;
+    for (int j = threadIdx.x; j < kRegionW; j += blockDim.x) {
+      const unsigned long long st = lstat[j];
+      if (st) {
+        atomicAdd(pkstat + p0 + j, st);
+        if (t.has_value) atomicAdd(psum + p0 + j, lsum[j]);
+      }
+    }
+    __syncthreads();
   }
   block_minmax(mn, mx, minmax);  // contains __syncthreads: every thread reaches it
   __syncthreads();
@@ -440,7 +536,8 @@ int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_
   t.U = n_privacy_ids;
   t.P = n_partitions;
   t.pk_bits = bits_for(n_partitions);
-  t.cap = table_capacity(n_rows);
+  t.cap = slots_capacity(n_rows, n_partitions);
+  t.R = n_regions(n_partitions);
   t.has_value = value_kind != PDP_VALUE_NONE;
   t.do_parts = 1;
   t.pk_mask = (1ULL << t.pk_bits) - 1;
@@ -473,21 +570,34 @@ int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partiti
     return set_error(PDP_E_INVALID, "NULL column");
   Slot* slots = (Slot*)(ws + w.slots);
   unsigned* err = (unsigned*)(ws + w.err);
+  unsigned* rbase = (unsigned*)(ws + w.rbase);
   const unsigned g = grid_for(t.n);
+  if (t.R <= kRegionLdsMax)
+    PDP_HLAUNCH("k_h_region_count", st, k_h_region_count<true>, dim3(grid_for(t.n, 1024)), dim3(kBlock), 0, st, t,
+                privacy_id, partition, rbase);
+  else
+    PDP_HLAUNCH("k_h_region_count", st, k_h_region_count<false>, dim3(g), dim3(kBlock), 0, st, t, privacy_id,
+                partition, rbase);
+  PDP_HLAUNCH("k_h_region_caps", st, k_h_region_caps, dim3(grid_for(t.R)), dim3(kBlock), 0, st, t.R, rbase);
+  {
+    const int rc = scan_u32(rbase, t.R, (unsigned*)(ws + w.rchunks), st);
+    if (rc != PDP_OK) return rc;
+  }
   switch (value_kind) {
     case PDP_VALUE_F64:
       PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_F64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                  value, slots, err);
+                  value, rbase, slots, err);
       break;
     case PDP_VALUE_I64:
       PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_I64>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                  value, slots, err);
+                  value, rbase, slots, err);
       break;
     default:
       PDP_HLAUNCH("k_h_rows", st, k_h_rows<PDP_VALUE_NONE>, dim3(g), dim3(kBlock), 0, st, t, privacy_id, partition,
-                  value, slots, err);
+                  value, rbase, slots, err);
   }
-  PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3(grid_for((int64_t)t.cap, 4096)), dim3(kBlock), 0, st, t, slots,
+  const int64_t n_chunks = ((int64_t)t.cap + kPairsChunk - 1) / kPairsChunk;  // upper bound of the used slots
+  PDP_HLAUNCH("k_h_pairs", st, k_h_pairs, dim3((unsigned)n_chunks), dim3(kPairsBlock), 0, st, t, slots, rbase,
               (unsigned long long*)(ws + w.pidstat), (unsigned long long*)(ws + w.pkstat), (double*)(ws + w.psum),
               c.H, (unsigned long long*)(ws + w.minmax));
   return PDP_OK;
