@@ -5,14 +5,18 @@
 // The reference builds seven histograms with five group-bys and a distinct
 // (count_per_element / sum_per_key over pids, pairs and partitions).  Here the
 // dense codes turn every group-by but the (pid, pk) one into direct indexing:
+//   k_h_region_count, k_h_region_caps, scan
+//               rows per partition-range region (4,096 partitions each) ->
+//               region slot bases (1.5 slots per row + 64)
 //   k_h_rows    per row: (pid, pk) into an open-addressing pair table (HBM,
-//               1.5 slots per row, linear probing) whose 32-byte slots hold
-//               key, value sum and row count, so a row's CAS and two atomics
-//               touch one cache line
-//   k_h_pairs   per live pair, one packed 64-bit atomic per pid and per
-//               partition: (distinct partitions << 32 | rows) per pid (L0, L1),
-//               (distinct pids << 32 | rows) per partition, + the partition's
-//               value sum; the Linf histogram, min/max of the pair sums
+//               linear probing inside the row's region) whose 32-byte slots
+//               hold key, value sum and rows - 1, so a row's CAS and atomics
+//               touch one cache line and the creating row skips the count
+//   k_h_pairs   per live pair: one packed 64-bit atomic per pid (distinct
+//               partitions << 32 | rows: L0, L1); per partition (distinct pids
+//               << 32 | rows, value sum) summed in LDS over the region and
+//               flushed with contiguous atomics; the Linf histogram, min/max
+//               of the pair sums
 //   k_h_ids     per pid: L0 / L1 histograms; per partition: count and
 //               privacy-id-count histograms, min/max of the partition sums
 //   k_h_lowers  np.linspace(min, max, 10001) bin lowers (_min_max_lowers,

@@ -213,3 +213,16 @@ def test_reference_test_known_answers(field, rows, expected):
     ext = DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: 0)
     (got,) = CH.compute_dataset_histograms(rows, ext)
     HU.assert_bins_equal(getattr(got, field).bins, expected, field, exact=True)
+
+
+def test_many_partition_regions():
+    """P = 7e7 partitions: more regions (P / 4096) than the LDS region-count
+    histogram holds, so rows are counted per region with global atomics"""
+    rng = np.random.default_rng(31)
+    n = 200_000
+    pid = rng.integers(0, 5_000, n)
+    pk = rng.integers(0, 70_000_000, n)
+    pk[:50_000] = rng.integers(0, 40, 50_000)  # a few hot partitions in region 0 as well
+    val = np.round(rng.normal(0, 3, n) * 4) / 4
+    got = _run_codes(pid, pk, val, U=5_000, P=70_000_000)
+    _check_all(got, OH.dataset_histograms(pid, pk, val), "many_regions", exact=True)
