@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
 # wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for the
 # default C2 shape only; None otherwise.
-PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "v17_pmc.json")
+PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "v18_pmc.json")
 
 
 def pmc_traffic(n_rows):
