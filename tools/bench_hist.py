@@ -61,6 +61,12 @@ def main():
     cap = max(1024, ((n + n // 2) + 255) // 256 * 256)
     per_kernel_bytes = {"k_h_rows": 24.0 * n, "k_h_pairs": 32.0 * cap, "k_h_float": 32.0 * cap}
     dom_bytes = per_kernel_bytes.get(dom)
+    # PMC-measured HBM bytes per launch (tools/gpu_hist_pmc.sh: 2 x FETCH_SIZE + WRITE_SIZE)
+    pmc_path = os.path.join(ROOT, "profiles", "r01", "h6_pmc.json")
+    traffic = None
+    if os.path.exists(pmc_path) and n == ROWS:
+        with open(pmc_path) as f:
+            traffic = json.load(f)["kernels"].get(dom, {}).get("hbm_bytes")
     out = {
         "metric": "dataset histogram input rows/sec (compute_dataset_histograms device pass)",
         "value": n / dt, "unit": "rows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
@@ -72,7 +78,8 @@ def main():
                      "achieved": dom_bytes / (kernel_ms[dom] * 1e-3) / 1e9 if dom_bytes else None,
                      "peak": PEAK_GBS, "unit": "GB/s",
                      "frac": dom_bytes / (kernel_ms[dom] * 1e-3) / 1e9 / PEAK_GBS if dom_bytes else None,
-                     "bytes_per_launch": dom_bytes},
+                     "bytes_per_launch": dom_bytes, "traffic": traffic,
+                     "traffic_source": "profiles/r01/h6_pmc.json" if traffic else None},
         "path_roofline": {"achieved": 24.0 * n / dt / 1e9, "peak": PEAK_GBS, "unit": "GB/s",
                           "frac": 24.0 * n / dt / 1e9 / PEAK_GBS},
     }
