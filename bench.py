@@ -1,28 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark of the DPEngine.aggregate hot path on MI355X (BASELINE.json).
 
-Workload (BASELINE.json configs[1], SURVEY §8(d) "C2"): per GPU N = 1e8 rows,
-P = 1e5 partitions (pk uniform), U = 1e6 privacy ids (pid uniform, ~100 rows
-each), value fp64 ~ N(5, 3) clipped to [0, 10]; COUNT + SUM + MEAN, Laplace,
-max_partitions_contributed = 8, max_contributions_per_partition = 2,
-min/max value 0/10, eps = 1, delta = 1e-6, private partitions (truncated
-geometric).  Weak scaling: every rank holds its own 1e8 rows of its own 1e6
-privacy ids (rows sharded by privacy id), partitions are global; the one
-cross-GPU step is an RCCL reduce-scatter of the per-partition accumulators,
-after which each rank selects and noises its slice of partitions.
+Workloads:
+  c3 (default, BASELINE configs[2], the north-star target shape): 1e9 rows in
+     total, privacy ids uniform over 1e7, partition keys Zipf(1.1) folded into
+     1e6 partitions, values U(0, 10); COUNT + SUM + MEAN, Laplace,
+     max_partitions_contributed = 2 (sampling fires), max_contributions_per_
+     partition = 1, private partitions (truncated geometric), eps = 1,
+     delta = 1e-6.  Strong scaling: N GPUs share the 1e9 rows, sharded by
+     privacy id (rank r holds the privacy ids = r mod N).
+  c2 (BASELINE configs[1]): 1e8 rows per GPU, 1e6 privacy ids, 1e5 uniform
+     partitions, values N(5, 3) clipped to [0, 10], L0 = 8, Linf = 2.  Weak
+     scaling.  At N = 1 with the default workload it also runs as the
+     `secondary` object of the JSON line.
 
 A step = one full aggregate over the resident batch: contribution bounding
-(L0 + Linf sampling), per-partition reduction, [reduce-scatter], partition
-selection, compaction and noisy metrics, ending with the kept-partition count
-on the host.  Inputs are resident in HBM before timing starts.
+(L0 + Linf sampling), per-partition reduction, [RCCL reduce-scatter of the
+accumulators], partition selection, compaction and noisy metrics, ending with
+the kept-partition count on the host.  Inputs are resident in HBM before
+timing starts.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: launched by torch.distributed.run, one rank per GPU)
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+  With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
+  `python -m torch.distributed.run --nproc-per-node N` on itself as a child
+  process (before touching the GPU) and exits with its status.
 """
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,23 +43,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 # HBM bytes per launch from rocprofv3 PMC passes over this same bench command
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
-# wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for the
-# default C2 shape only; None otherwise.
-PMC_SUMMARY = os.path.join(HERE, "profiles", "r01", "v18_pmc.json")
+# wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for
+# the workload and tree named in the file; None otherwise.
+PMC_SUMMARY = {"c3": os.path.join(HERE, "profiles", "r02", "c3_pmc.json"),
+               "c2": os.path.join(HERE, "profiles", "r02", "c2_pmc.json")}
 
-
-def pmc_traffic(n_rows):
-    if n_rows != ROWS_PER_GPU or not os.path.exists(PMC_SUMMARY):
-        return {}
-    with open(PMC_SUMMARY) as f:
-        kernels = json.load(f)["kernels"]
-    return {k: v["hbm_bytes"] for k, v in kernels.items() if "hbm_bytes" in v}
-
-# workload constants (C2)
-ROWS_PER_GPU = 100_000_000
-PRIVACY_IDS_PER_GPU = 1_000_000
-PARTITIONS = 100_000
-L0, LINF = 8, 2
+# workload constants
+C2 = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000, l0=8, linf=2)
+C3 = dict(rows=1_000_000_000, privacy_ids=10_000_000, partitions=1_000_000, l0=2, linf=1, zipf=1.1)
 MIN_VALUE, MAX_VALUE = 0.0, 10.0
 EPS, DELTA = 1.0, 1e-6
 
@@ -62,22 +60,32 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=ROWS_PER_GPU, help="rows per GPU")
+    ap.add_argument("--workload", choices=("c3", "c2"), default="c3")
+    ap.add_argument("--rows", type=int, default=0, help="override: rows in total (c3) / per GPU (c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
-    ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto, 1 wide, 2 compact)")
-    ap.add_argument("--workload", choices=("c2", "c3"), default="c2",
-                    help="c2 (default, BASELINE configs[1]); c3: configs[2], 1e9 rows in total, "
-                         "Zipf(1.1) partition keys over 1e6 partitions, 1e7 privacy ids, L0=2, "
-                         "Linf=1, values U(0, 10), strong scaling over the GPUs")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
+    ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
+    ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
     return ap.parse_args()
 
 
-# C3: N = 1e9 in total, pk Zipf(a=1.1) over P = 1e6, U = 1e7
-C3_ROWS, C3_PRIVACY_IDS, C3_PARTITIONS, C3_L0, C3_LINF, C3_ZIPF = 1_000_000_000, 10_000_000, 1_000_000, 2, 1, 1.1
+def maybe_spawn(args):
+    """--gpus N > 1 without a torch.distributed environment: run N ranks of
+    this script under torch.distributed.run as a CHILD process (no exec, no
+    GPU touched in this process) and exit with its status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    sys.exit(subprocess.call(cmd, env=env))
 
 
-def build_plan(l0=L0, linf=LINF):
+def build_plan(l0, linf):
     """Noise / selection parameters exactly as DPEngine + NaiveBudgetAccountant
     derive them for this AggregateParams (3 mechanisms of weight 1: MEAN's
     count and normalized-sum Laplace mechanisms + the GENERIC selection)."""
@@ -86,81 +94,124 @@ def build_plan(l0=L0, linf=LINF):
     from pipelinedp_amd import executor as X
     eps_each = EPS / 3
     mid = dpc.compute_middle(MIN_VALUE, MAX_VALUE)
-    b_count = dpc.laplace_diversity(eps_each, l0 * linf)
-    b_nsum = dpc.laplace_diversity(eps_each, l0 * (MAX_VALUE - MIN_VALUE) / 2 * linf)
+    count_noise = dpc.laplace_noise_params(eps_each, l0 * linf)
+    nsum_noise = dpc.laplace_noise_params(eps_each, l0 * (MAX_VALUE - MIN_VALUE) / 2 * linf)
     bounding = X.BoundingSpec(l0=l0, linf=linf, value_kind=N.VALUE_F64, flags=N.ACC_NSUM,
                               min_value=MIN_VALUE, max_value=MAX_VALUE, middle=mid)
     selection = X.SelectionSpec(strategy=N.SELECT_TRUNCATED_GEOMETRIC,
                                 keep_prob=dpc.truncated_geometric_keep_table(eps_each, DELTA, l0))
-    ops = [X.MetricOpSpec(kind=N.OP_MEAN, noise_kind=N.NOISE_LAPLACE, out_col=(0, 1, 2),
-                          scale=(b_count, b_nsum), middle=mid)]
+    ops = [X.MetricOpSpec(kind=N.OP_MEAN, out_col=(0, 1, 2), noise=(count_noise, nsum_noise), middle=mid)]
     return bounding, selection, ops
 
 
-def cpu_baseline(sample_rows):
-    """Row-wise restatement of LocalBackend DPEngine.aggregate (the reference's
-    single-threaded CPU path) on a bounded sample of the same workload."""
+def cpu_baselines(workload, sample_rows):
+    """Rank 0, N = 1, before any GPU work.  `port`: the row-wise restatement
+    of LocalBackend DPEngine.aggregate (the reference's single-threaded CPU
+    path, oracle/local_backend_port.py) on a bounded sample of the workload;
+    `strong`: the vectorised NumPy oracle on up to 16 host processes
+    (oracle/strong_baseline.py)."""
     from oracle import local_backend_port as port
-    rng = np.random.default_rng(1)
+    from oracle import strong_baseline as strong
+    w = C3 if workload == "c3" else C2
     U = max(1, sample_rows // 100)
-    pid = rng.integers(0, U, sample_rows)
-    pk = rng.integers(0, PARTITIONS, sample_rows)
-    val = np.clip(rng.normal(5.0, 3.0, sample_rows), MIN_VALUE, MAX_VALUE)
+    if workload == "c3":
+        pid, pk, val = strong.c3_shard(sample_rows, U, w["partitions"], w["zipf"], 1)
+    else:
+        rng = np.random.default_rng(1)
+        pid = rng.integers(0, U, sample_rows)
+        pk = rng.integers(0, w["partitions"], sample_rows)
+        val = np.clip(rng.normal(5.0, 3.0, sample_rows), MIN_VALUE, MAX_VALUE)
     rows = list(zip(pid.tolist(), pk.tolist(), val.tolist()))
     t0 = time.perf_counter()
-    out = port.aggregate_count_sum_mean(rows, l0=L0, linf=LINF, min_value=MIN_VALUE,
+    out = port.aggregate_count_sum_mean(rows, l0=w["l0"], linf=w["linf"], min_value=MIN_VALUE,
                                         max_value=MAX_VALUE, eps=EPS, delta=DELTA)
     dt = time.perf_counter() - t0
-    return {"value": sample_rows / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{sample_rows} rows of the same workload (U={U}, P={PARTITIONS}), "
-                      f"oracle/local_backend_port.py row-wise LocalBackend restatement, "
-                      f"{dt:.1f} s, {len(out)} partitions kept"}
+    model = strong.cpu_model()
+    base = {"value": sample_rows / dt, "unit": "rows/s", "cores": 1, "kind": "port", "cpu_model": model,
+            "sample": f"{sample_rows} rows shaped like {workload.upper()} (U={U}, P={w['partitions']}, "
+                      f"L0={w['l0']}, Linf={w['linf']}); oracle/local_backend_port.py, a row-wise "
+                      f"restatement of the reference's single-threaded LocalBackend path (dict group-bys, "
+                      f"np.random.choice, np.clip per pair; no namedtuples or DPEngine generators, so it "
+                      f"runs ~2x the reference's own measured rate, BASELINE.md §2); {dt:.1f} s, "
+                      f"{len(out)} partitions kept; the full workload is a linear extrapolation"}
+    workers = max(1, min(16, os.cpu_count() or 1))
+    per = 2_000_000
+    rate, sdt, kept = strong.run(workers, per, per // 100, w["partitions"], w.get("zipf", 0.0) or 1.0001,
+                                 w["l0"], w["linf"], EPS, DELTA)
+    strong_res = {"value": rate, "unit": "rows/s", "cores": workers, "kind": "port", "cpu_model": model,
+                  "sample": f"{workers} x {per} rows (privacy-id shards, Zipf pk), vectorised NumPy oracle "
+                            f"(oracle/columnar.py) one process per shard + merge/select/noise; "
+                            f"{sdt:.2f} s, {kept} partitions kept"}
+    return base, strong_res
 
 
-def main():
-    args = parse()
+def gen_c3(n, U, P, rank, world, device, seed):
+    """This rank's shard: privacy ids r + k*world (k < U), Zipf(1.1) pk."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+    w = torch.arange(1, P + 1, device=device, dtype=torch.float64).pow_(-C3["zipf"])
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    pk = torch.empty(n, device=device, dtype=torch.int64)
+    for c0 in range(0, n, 1 << 27):  # bounded temporaries
+        c1 = min(n, c0 + (1 << 27))
+        u = torch.rand(c1 - c0, generator=g, device=device, dtype=torch.float64)
+        pk[c0:c1] = torch.searchsorted(cdf, u).clamp_(max=P - 1)
+        del u
+    value = torch.rand(n, generator=g, device=device, dtype=torch.float64) * MAX_VALUE
+    del w, cdf
+    return pid, pk, value
+
+
+def gen_c2(n, U, P, rank, device, seed):
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+    pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
+    value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
+        MIN_VALUE, MAX_VALUE)
+    return pid, pk, value
+
+
+def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields):
+    """Algorithmic bytes of each kernel of one step: every
+    input it must read once plus every output it must write once."""
+    from pipelinedp_amd import _native as N
+    kb, rb = {N.KEYS_COMPACT: (4, 4), N.KEYS_WIDE: (8, 4), N.KEYS_PACKED: (8, 0)}.get(plan.key_format, (8, 4))
+    rec = kb + rb
+    pair_rec = 8 + 8 * n_fields
+    out = {"k_part_hist": 8.0 * n,
+           "k_scatter_l1": (16.0 + rec) * n,
+           "k_scatter_l2": 2.0 * rec * n,
+           # B1 streams the keys, B2 the whole records; kept rows' values
+           # gathered; one record per kept pair out
+           "k_bucket_bound": kb * n + rec * n + 8.0 * kept_rows + pair_rec * kept_pairs,
+           "k_range_reduce": 2.0 * pair_rec * kept_pairs}
+    return out
+
+
+def run_workload(args, workload, world, rank, device, pmc_file):
     import torch
     import torch.distributed as dist
     from pipelinedp_amd import _native as N
     from pipelinedp_amd import executor as X
     from pipelinedp_amd import parallel
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    device = torch.device("cuda", local_rank)
-
-    c3 = args.workload == "c3"
-    g = torch.Generator(device=device)
-    g.manual_seed(1000 + rank)
-    if c3:  # strong scaling: 1e9 rows and 1e7 privacy ids in total, sharded by privacy id
-        n = C3_ROWS // world
-        U = C3_PRIVACY_IDS // world
-        P = C3_PARTITIONS
-        bounding, selection, ops = build_plan(C3_L0, C3_LINF)
-        pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
-        w = torch.arange(1, P + 1, device=device, dtype=torch.float64).pow_(-C3_ZIPF)
-        cdf = torch.cumsum(w, 0)
-        cdf /= cdf[-1].clone()
-        pk = torch.empty(n, device=device, dtype=torch.int64)
-        for c0 in range(0, n, 1 << 27):  # bounded temporaries
-            c1 = min(n, c0 + (1 << 27))
-            u = torch.rand(c1 - c0, generator=g, device=device, dtype=torch.float64)
-            pk[c0:c1] = torch.searchsorted(cdf, u).clamp_(max=P - 1)
-        value = torch.rand(n, generator=g, device=device, dtype=torch.float64) * MAX_VALUE
-        del w, cdf
+    if workload == "c3":
+        total = args.rows or C3["rows"]
+        n = total // world
+        U = C3["privacy_ids"] // world
+        P = C3["partitions"]
+        bounding, selection, ops = build_plan(C3["l0"], C3["linf"])
+        pid, pk, value = gen_c3(n, U, P, rank, world, device, 2000)
     else:
-        n = args.rows
-        U = max(1, (PRIVACY_IDS_PER_GPU * n) // ROWS_PER_GPU)
-        P = PARTITIONS
-        bounding, selection, ops = build_plan()
-        pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
-        pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
-        value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
-            MIN_VALUE, MAX_VALUE)
+        n = args.rows or C2["rows"]
+        U = max(1, (C2["privacy_ids"] * n) // C2["rows"])
+        P = C2["partitions"]
+        bounding, selection, ops = build_plan(C2["l0"], C2["linf"])
+        pid, pk, value = gen_c2(n, U, P, rank, device, 1000)
     torch.cuda.synchronize()
 
     P_pad, _ = parallel.partition_slices(P, world)
@@ -197,6 +248,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # key-error check of the data once (outside the timed region)
+    X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding, seed=1,
+                       row_offset=rank * n, acc=acc, workspace=ws, check_keys=True,
+                       key_format=args.key_format)
     # per-kernel times from a second, untimed pass of the same steps: the HIP
     # events the profiler records around every launch (on its launch stream)
     # would otherwise sit inside the timed region
@@ -205,73 +260,119 @@ def main():
         step(args.warmup + args.steps + i)
     kernels = N.profiler_report()
     N.profiler_enable(False)
+    kept_pairs = int(acc["privacy_id_count"].sum().item())  # last step, this rank
+    kept_rows = int(acc["count"].sum().item())
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    del pid, pk, value, acc, ws
 
     kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}  # average ms per launch
-    launches_per_step = {k: v[1] / args.steps for k, v in kernels.items()}
-    dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches_per_step[k])
-    # algorithmic bytes of the path: 24 B per input row (pid, pk,
-    # value), attributed to the dominant kernel's launch
-    alg_bytes = 24.0 * n
-    achieved = alg_bytes / (kernel_ms[dom] * 1e-3) / 1e9
+    launches = {k: v[1] / args.steps for k, v in kernels.items()}
     ms_per_step = elapsed / args.steps * 1e3
     total_rows = n * world * args.steps
-    value_rows_s = total_rows / elapsed
-    path_bytes = 24.0 * n + kept * (8 + 8 * 3 + 8 * 3)
-    traffic = pmc_traffic(n)
+    traffic, traffic_src = {}, None
+    if pmc_file and os.path.exists(pmc_file):
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+        if pmc.get("workload", "").startswith(f"{workload} n={n} ") and world == 1:
+            traffic = {k: v["hbm_bytes"] for k, v in pmc["kernels"].items() if "hbm_bytes" in v}
+            traffic_src = os.path.relpath(pmc_file, HERE)
+    alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2)
+    table = {}
+    for k, ms in kernel_ms.items():
+        e = {"ms": ms, "launches_per_step": launches[k]}
+        if k in alg:
+            e["alg_bytes"] = alg[k]
+            e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
+            e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
+        if k in traffic:
+            e["pmc_bytes"] = traffic[k]
+            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
+        table[k] = e
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
+    path_bytes = 24.0 * n + kept * (8 + 8 * 3 + 8 * 3)  # SURVEY §8(d) compulsory bytes
+    path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
+    w = C3 if workload == "c3" else C2
+    return {
+        "value": total_rows / elapsed,
+        "ms_per_step": ms_per_step,
+        "workload_name": workload,
+        "config": {
+            "workload": (f"{workload.upper()}: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
+                         f"(truncated geometric), L0={w['l0']}, Linf={w['linf']}, "
+                         + (f"{n * world:.3g} rows in total, Zipf({C3['zipf']}) partition keys"
+                            if workload == "c3" else f"{n:.3g} rows per GPU, uniform keys")),
+            "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
+            "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
+        },
+        "roofline": {  # dominant kernel, its OWN algorithmic bytes
+            "bound": "hbm", "kernel": dom,
+            "achieved": table[dom].get("achieved_gbs"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": table[dom].get("frac"), "traffic": traffic.get(dom), "traffic_source": traffic_src,
+            "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom],
+        },
+        "path_roofline": {  # the headline fraction: 24 B/row compulsory over the whole step
+            "achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": path_gbs / HBM_PEAK_GBS,
+            "bytes_per_step": path_bytes,
+            "traffic_per_step": sum(traffic.values()) if traffic else None,
+        },
+        "kernels": table,
+        "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
+                       "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
+                       "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(plan.key_format,
+                                                                               plan.key_format)},
+        "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
+    }
+
+
+def main():
+    args = parse()
+    maybe_spawn(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+
+    r = run_workload(args, args.workload, world, rank, device, PMC_SUMMARY[args.workload])
     result = {
         "metric": "input rows/sec aggregated (whole node) + achieved HBM GB/s vs peak",
-        "value": value_rows_s,
+        "value": r["value"],
         "unit": "rows/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
+        "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "strong" if c3 else "weak",
+        "scaling": "strong" if args.workload == "c3" else "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (uniform pid, Zipf(1.1) pk, U(0,10) values), generated on device" if c3 else
+        "data": ("synthetic (uniform pid, Zipf(1.1) pk, U(0,10) values), generated on device"
+                 if args.workload == "c3" else
                  "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device"),
-        "config": {
-            "workload": ("C3: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
-                         "(truncated geometric), L0=2, Linf=1, 1e9 rows in total" if c3 else
-                         "C2: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions "
-                         "(truncated geometric), L0=8, Linf=2"),
-            "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
-            "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
-        },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic.get(dom),
-            "traffic_source": os.path.relpath(PMC_SUMMARY, HERE) if dom in traffic else None,
-            "bytes_per_launch": alg_bytes,
-            "avg_ms": kernel_ms[dom],
-        },
-        "path_roofline": {
-            "achieved": path_bytes / (ms_per_step * 1e-3) / 1e9,
-            "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": path_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "bytes_per_step": path_bytes,
-            "traffic_per_step": sum(traffic.values()) if traffic else None,
-        },
-        "kernel_ms": kernel_ms,
-        "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
-                       "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
-                       "key_format": {1: "wide", 2: "compact"}.get(plan.key_format, plan.key_format)},
-        "partitions_kept": kept,
-        "cpu_baseline": None,
+        "config": r["config"],
+        "roofline": r["roofline"],
+        "path_roofline": r["path_roofline"],
+        "kernels": r["kernels"],
+        "bound_plan": r["bound_plan"],
+        "partitions_kept": r["partitions_kept"],
+        "cpu_baseline": cpu[0] if cpu else None,
+        "cpu_baseline_strong": cpu[1] if cpu else None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not c3:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows)
+    if world == 1 and args.workload == "c3" and not args.no_secondary and not args.rows:
+        torch.cuda.empty_cache()
+        s = run_workload(args, "c2", 1, 0, device, PMC_SUMMARY["c2"])
+        result["secondary"] = {k: s[k] for k in ("value", "ms_per_step", "config", "roofline",
+                                                 "path_roofline", "kernels", "bound_plan")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

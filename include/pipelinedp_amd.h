@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 5
+#define PDP_ABI_VERSION 6
 
 /* error codes */
 #define PDP_OK 0
@@ -163,6 +163,35 @@ int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value,
                           void* workspace, uint64_t workspace_bytes,
                           const pdp_partition_accumulators* acc, void* stream);
 
+/* Noise of one additive mechanism, the granularity-snapped secure samplers of
+ * Google's differential-privacy library that PyDP wraps (python-dp ~=1.1.5rc4,
+ * numerical_mechanisms.LaplaceMechanism / GaussianMechanism, called at
+ * dp_computations.py:439-440, 489-491; restated, not vendored):
+ *   out = round_to_multiple(x, granularity) + granularity * k,
+ * k a two-sided geometric sample P(k) ~ exp(-lambda |k|) (Laplace, found by an
+ * integer bisection whose every step is a Bernoulli with the exact conditional
+ * mass), or a centred Binomial(n, 1/2) sample drawn by geometric-proposal
+ * rejection (Gaussian).  Outputs lie on the power-of-two grid, so their low
+ * bits carry no information about x (the floating-point attack of Mironov
+ * 2012 on textbook samplers).  The host computes every field
+ * (pipelinedp_amd/dp_computations.py: laplace_noise_params /
+ * gaussian_noise_params); granularity = 0 means no noise. */
+#define PDP_NOISE_LAPLACE 0
+#define PDP_NOISE_GAUSSIAN 1
+
+typedef struct pdp_noise_params {
+  int32_t kind;        /* PDP_NOISE_* */
+  int32_t reserved;
+  double scale;        /* Laplace b = sensitivity / eps, Gaussian sigma (reporting) */
+  double granularity;  /* output grid, a power of two; 0 = no noise */
+  double lambda;       /* Laplace: granularity * eps / (sensitivity + granularity) */
+  int64_t step;        /* Gaussian: round(sqrt(2) * sqrt_n + 1), sqrt_n = 2 sigma / granularity */
+  double n;            /* Gaussian: sqrt_n^2 (binomial trials) */
+  double bound;        /* Gaussian: sqrt_n * sqrt(log(n) / 2), |m| above it has probability 0 */
+  double coef;         /* Gaussian: sqrt(2 / pi) / sqrt_n */
+  double corr;         /* Gaussian: 1 - 0.4 * (2 log n)^1.5 / sqrt_n */
+} pdp_noise_params;
+
 /* partition selection strategies */
 #define PDP_SELECT_ALL_NONEMPTY 0 /* keep every partition with row_count > 0 */
 #define PDP_SELECT_TRUNCATED_GEOMETRIC 1
@@ -178,7 +207,7 @@ typedef struct pdp_select_config {
   int32_t pre_threshold;         /* 0 = none */
   int32_t keep_table_len;        /* truncated geometric: keep_prob[0..len-1] */
   const double* keep_prob;       /* device; prob of keep for n; n >= len uses [len-1] */
-  double noise_scale;            /* Laplace b or Gaussian sigma (thresholding) */
+  pdp_noise_params noise;        /* thresholding strategies: the secure mechanism */
   double threshold;              /* thresholding strategies */
   const uint8_t* public_mask;    /* PDP_SELECT_PUBLIC */
   uint64_t seed;
@@ -207,23 +236,17 @@ int pdp_compact(const uint8_t* keep, int64_t n, int64_t* out_index, int64_t* out
 #define PDP_OP_VARIANCE 5         /* VarianceCombiner + compute_dp_var, dp_computations.py:306-365 */
 #define PDP_OP_THRESHOLDED_PID 6  /* PostAggregationThresholdingCombiner: copy noised_count */
 
-#define PDP_NOISE_LAPLACE 0
-#define PDP_NOISE_GAUSSIAN 1
-
 typedef struct pdp_metric_op {
   int32_t kind;        /* PDP_OP_* */
-  int32_t noise_kind;  /* PDP_NOISE_* */
+  int32_t degenerate;  /* VARIANCE: min_value == max_value */
   int32_t out_col[4];  /* output column for each produced metric, -1 = not produced.
                           COUNT/SUM/PID: [0]; MEAN: mean,count,sum;
                           VARIANCE: variance,count,sum,mean */
-  double scale[3];     /* noise parameter per mechanism (b or sigma):
-                          COUNT/SUM/PID: [0]; MEAN: count,nsum;
-                          VARIANCE: count,nsum,nsum2 */
+  pdp_noise_params noise[3]; /* per mechanism: COUNT/SUM/PID: [0]; MEAN: count,nsum;
+                                VARIANCE: count,nsum,nsum2 */
   double middle;       /* MEAN/VARIANCE: middle of [min_value, max_value] */
   double min_value;    /* VARIANCE: for min_value == max_value shortcut */
   double sq_min_value; /* VARIANCE: lower end of the squares interval */
-  int32_t degenerate;  /* VARIANCE: min_value == max_value */
-  int32_t pad;
 } pdp_metric_op;
 
 #define PDP_MAX_OPS 8
@@ -239,17 +262,18 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
                       const double* noised_count, double* out, int64_t out_stride,
                       uint64_t seed, void* stream);
 
-/* DPEngine.add_dp_noise (dp_engine.py:551-607): out[i] = (double)values[i]
- * + noise, the `lambda value: create_mechanism().add_noise(float(value))` of
- * its "Add noise" map_values stage (dp_engine.py:595-599) over a column.
- * values: n int64 (PDP_VALUE_I64) or fp64 (PDP_VALUE_F64); noise_kind
- * PDP_NOISE_LAPLACE (scale = b = l0*linf/eps, dp_computations.py:430-477) or
- * PDP_NOISE_GAUSSIAN (scale = sigma, :480-537).  Element i draws from the
- * Philox4x32-10 stream (seed, index_offset + i), so shards of one column
- * noised with their global offsets equal the unsharded result.  values and
- * out: device, 16-byte aligned; out may alias values when both are fp64. */
-int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noise_kind,
-                  double scale, uint64_t seed, int64_t index_offset, double* out, void* stream);
+/* DPEngine.add_dp_noise (dp_engine.py:551-607): out[i] = the secure
+ * mechanism `noise` applied to (double)values[i], the `lambda value:
+ * create_mechanism().add_noise(float(value))` of its "Add noise" map_values
+ * stage (dp_engine.py:595-599) over a column.  values: n int64
+ * (PDP_VALUE_I64) or fp64 (PDP_VALUE_F64); `noise` (host pointer): Laplace
+ * (l1 = l0*linf, dp_computations.py:430-477) or Gaussian (:480-537).
+ * Element i draws from the Philox4x32-10 streams (seed, index_offset + i), so
+ * shards of one column noised with their global offsets equal the unsharded
+ * result.  values and out: device, 16-byte aligned; out may alias values when
+ * both are fp64. */
+int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, const pdp_noise_params* noise,
+                  uint64_t seed, int64_t index_offset, double* out, void* stream);
 
 /* Device error word: the bounding kernels set bit 0 when a key is outside
  * [0, n_privacy_ids) x [0, n_partitions) (the row is skipped, never read out

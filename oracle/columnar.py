@@ -23,7 +23,8 @@ counter-based values the HIP kernels compute (pair keys: a MurmurHash3 fmix32
 hash of (seed, pid, pk); row keys: SplitMix64 of the global row index), so the
 sampled sets match the GPU bit-for-bit; with ``priorities="rng"`` they come
 from a NumPy Generator (the reference's np.random.choice distribution).
-Noise and selection use the same Philox4x32-10 streams as the kernels.
+Noise and selection use the same Philox4x32-10 streams and the same
+granularity-snapped secure samplers as the kernels.
 """
 import numpy as np
 
@@ -130,20 +131,135 @@ def philox_for(seed, gidx, slot):
     return philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
 
 
-def laplace_noise(b, r):
-    u = u01(r[0], r[1]) - 0.5
-    mag = -b * np.log1p(-2.0 * np.abs(u))
-    return np.where(u < 0.0, -mag, mag)
+# ------------------------------------------------------------ secure noise --
+# Restates the kernels' secure samplers (pdp_internal.h secure_*), which
+# restate the granularity-snapped samplers of Google's differential-privacy
+# library behind PyDP (python-dp ~=1.1.5rc4, not installed here):
+# out = round_to_multiple(x, g) + g * k, k two-sided geometric (Laplace) or a
+# centred binomial (Gaussian).  Philox blocks are consumed in the kernels'
+# order, so GPU and oracle agree bit for bit (up to a last-ulp difference of
+# expm1 / exp flipping one Bernoulli, probability ~1e-16 per draw).
+INT64_MAX = np.int64(0x7FFFFFFFFFFFFFFF)
 
 
-def gaussian_noise(sigma, r):
-    u1 = u01(r[0], r[1])
-    u2 = u01(r[2], r[3])
-    return sigma * np.sqrt(-2.0 * np.log(u1)) * np.cos(6.283185307179586476925286766559 * u2)
+def noise_block(seed, gidx, slot, k):
+    gidx = np.asarray(gidx, dtype=np.int64).astype(np.uint64)
+    c0 = (gidx & _U64(0xFFFFFFFF)).astype(np.uint32)
+    c1 = (gidx >> _U64(32)).astype(np.uint32)
+    c2 = np.full(c0.shape, slot & 0xFFFFFFFF, dtype=np.uint32)
+    c3 = (np.uint32(0x4E000000) + np.asarray(k, dtype=np.uint32)).astype(np.uint32)
+    return philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
 
 
-def draw_noise(kind, scale, r):
-    return gaussian_noise(scale, r) if kind == NOISE_GAUSSIAN else laplace_noise(scale, r)
+def round_to_multiple(x, base):
+    x = np.asarray(x, dtype=np.float64)
+    if base == 0.0:
+        return x
+    r = np.fmod(x, base)
+    return np.where(np.abs(r) > base / 2, x - r + np.copysign(base, r), x - r)
+
+
+def secure_geometric(lam, seed, gidx, slot, k):
+    """Bisection geometric sampler (pdp_internal.h secure_geometric); k: the
+    per-element next Philox block index (updated in place)."""
+    n = len(gidx)
+    lo = np.zeros(n, dtype=np.int64)
+    hi = np.full(n, INT64_MAX, dtype=np.int64)
+    half = np.zeros(n, dtype=bool)
+    bz = np.zeros(n, dtype=np.uint32)
+    bw = np.zeros(n, dtype=np.uint32)
+    idx = np.arange(n)
+    while len(idx):
+        l, h = lo[idx], hi[idx]
+        mid = l + ((h - l) >> 1)
+        with np.errstate(over="ignore"):
+            q = np.expm1(lam * (l - mid).astype(np.float64)) / np.expm1(lam * (l - h).astype(np.float64))
+        det = q >= 1.0
+        hi[idx[det]] = mid[det]
+        r = idx[~det]
+        if len(r):
+            qr, mr = q[~det], mid[~det]
+            fresh = r[~half[r]]
+            u = np.empty(len(r))
+            if len(fresh):
+                b = noise_block(seed, gidx[fresh], slot, k[fresh])
+                k[fresh] += 1
+                bz[fresh], bw[fresh] = b[2], b[3]
+                u[~half[r]] = u01(b[0], b[1])
+            old = half[r]
+            if old.any():
+                u[old] = u01(bz[r[old]], bw[r[old]])
+            half[r] = ~half[r]
+            low = u <= qr
+            hi[r[low]] = mr[low]
+            lo[r[~low]] = mr[~low]
+        idx = idx[lo[idx] + 1 < hi[idx]]
+    return hi - 1
+
+
+def secure_laplace(np_, seed, gidx, slot):
+    gidx = np.asarray(gidx, dtype=np.int64)
+    out = np.empty(len(gidx))
+    k = np.zeros(len(gidx), dtype=np.uint32)
+    pend = np.arange(len(gidx))
+    while len(pend):
+        a = noise_block(seed, gidx[pend], slot, k[pend])
+        k[pend] += 1
+        positive = (a[0] >> np.uint32(31)) != 0
+        kk = k[pend]
+        s = secure_geometric(np_["lambda"], seed, gidx[pend], slot, kk)
+        k[pend] = kk
+        redo = (s == 0) & ~positive
+        sf = s.astype(np.float64)
+        v = np.where(positive, sf, -sf) * np_["granularity"]
+        out[pend[~redo]] = v[~redo]
+        pend = pend[redo]
+    return out
+
+
+def _clz32(v):
+    v = np.asarray(v, dtype=np.uint32)
+    e = np.frexp(v.astype(np.float64))[1]
+    return np.where(v == 0, 32, 32 - e).astype(np.int64)
+
+
+def secure_gaussian(np_, seed, gidx, slot):
+    gidx = np.asarray(gidx, dtype=np.int64)
+    out = np.empty(len(gidx))
+    k = np.zeros(len(gidx), dtype=np.uint32)
+    step = int(np_["step"])
+    pend = np.arange(len(gidx))
+    while len(pend):
+        a = noise_block(seed, gidx[pend], slot, k[pend])
+        b = noise_block(seed, gidx[pend], slot, k[pend] + 1)
+        k[pend] += 2
+        nx, ny = ~a[0], ~a[1]
+        geom = np.where(a[0] != 0xFFFFFFFF, _clz32(nx), np.where(a[1] != 0xFFFFFFFF, 32 + _clz32(ny), 64))
+        two_sided = np.where((a[2] >> np.uint32(31)) != 0, geom, -geom - 1)
+        st = _U64(step)
+        with np.errstate(over="ignore"):
+            hi_part = b[0].astype(np.uint64) * st + ((b[1].astype(np.uint64) * st) >> _U64(32))
+        uni = (hi_part >> _U64(32)).astype(np.int64)
+        m = np.int64(step) * two_sided + uni
+        accept_u = u01(b[2], b[3])
+        md = m.astype(np.float64)
+        inb = np.abs(md) <= np_["bound"]
+        prob = np_["coef"] * np.exp(-2.0 * md * md / np_["n"]) * np_["corr"]
+        ok = inb & (prob > 0.0) & (accept_u < prob * float(step) * np.ldexp(1.0, geom) / 4.0)
+        out[pend[ok]] = md[ok] * np_["granularity"]
+        pend = pend[~ok]
+    return out
+
+
+def secure_add_noise(np_, x, seed, gidx, slot):
+    """mechanism.add_noise(x) for the elements x[i] with streams gidx[i]."""
+    x = np.asarray(x, dtype=np.float64)
+    g = float(np_["granularity"])
+    if g == 0.0:
+        return x.copy()
+    noise = secure_gaussian(np_, seed, gidx, slot) if np_["kind"] == NOISE_GAUSSIAN else \
+        secure_laplace(np_, seed, gidx, slot)
+    return round_to_multiple(x, g) + noise
 
 
 # ------------------------------------------------------------- bounding --
@@ -280,7 +396,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
 
 # --------------------------------------------------- selection + metrics --
 def select(row_count, strategy, *, max_rows_per_privacy_id=1, pre_threshold=0, keep_prob=None,
-           noise_scale=0.0, threshold=0.0, public_mask=None, seed=0, partition_offset=0):
+           noise=None, threshold=0.0, public_mask=None, seed=0, partition_offset=0):
     """Restates pdp_select_partitions: returns (keep bool[P], noised float[P])."""
     rc = np.asarray(row_count, dtype=np.int64)
     P = len(rc)
@@ -297,14 +413,15 @@ def select(row_count, strategy, *, max_rows_per_privacy_id=1, pre_threshold=0, k
         ok &= n >= pre_threshold
         shift = pre_threshold - 1
         n = n - shift
-    r = philox_for(seed, partition_offset + np.arange(P), 0x53454C00)
     if strategy == SELECT_TRUNCATED_GEOMETRIC:
+        r = philox_for(seed, partition_offset + np.arange(P), 0x53454C00)
         table = np.asarray(keep_prob, dtype=np.float64)
         t = np.minimum(np.maximum(n, 0), len(table) - 1)
         keep = ok & (u01(r[0], r[1]) < table[t])
         return keep, noised
-    noise = gaussian_noise(noise_scale, r) if strategy == SELECT_GAUSSIAN else laplace_noise(noise_scale, r)
-    v = n.astype(np.float64) + noise
+    v = np.full(P, -np.inf)
+    live = np.flatnonzero(ok)
+    v[live] = secure_add_noise(noise, n[live].astype(np.float64), seed, partition_offset + live, 0x53454C00)
     keep = ok & (v > threshold)
     noised = np.where(keep, v + shift, np.nan)
     return keep, noised
@@ -324,33 +441,34 @@ def noise_metrics(ops, index, acc, sum_is_int, noised_count, seed, partition_off
 
     for o, op in enumerate(ops):
         slot = o << 4
-        kind, nk, sc, cols = op["kind"], op["noise_kind"], op["scale"], op["out_col"]
+        kind, nz, cols = op["kind"], op["noise"], op["out_col"]
+
+        def noised(m, x, sl):
+            return secure_add_noise(nz[m], np.asarray(x, dtype=np.float64), seed, g, sl)
+
         if kind == OP_COUNT:
-            put(cols[0], acc["count"][index] + draw_noise(nk, sc[0], philox_for(seed, g, slot)))
+            put(cols[0], noised(0, acc["count"][index], slot))
         elif kind == OP_SUM:
-            s = acc["sum"][index].astype(np.float64)
-            put(cols[0], s + draw_noise(nk, sc[0], philox_for(seed, g, slot)))
+            put(cols[0], noised(0, acc["sum"][index].astype(np.float64), slot))
         elif kind == OP_PRIVACY_ID_COUNT:
-            put(cols[0], acc["privacy_id_count"][index] + draw_noise(nk, sc[0], philox_for(seed, g, slot)))
+            put(cols[0], noised(0, acc["privacy_id_count"][index], slot))
         elif kind == OP_MEAN:
-            dp_count = acc["count"][index] + draw_noise(nk, sc[0], philox_for(seed, g, slot))
+            dp_count = noised(0, acc["count"][index], slot)
             denom = np.maximum(1.0, dp_count)
-            dp_nsum = acc["normalized_sum"][index] + draw_noise(nk, sc[1], philox_for(seed, g, slot + 1))
+            dp_nsum = noised(1, acc["normalized_sum"][index], slot + 1)
             mean = op["middle"] + dp_nsum / denom
             put(cols[0], mean)
             put(cols[1], dp_count)
             put(cols[2], mean * dp_count)
         elif kind == OP_VARIANCE:
-            dp_count = acc["count"][index] + draw_noise(nk, sc[0], philox_for(seed, g, slot))
+            dp_count = noised(0, acc["count"][index], slot)
             if op.get("degenerate", 0):
                 dp_mean = np.full(len(index), op["min_value"])
                 dp_mean_sq = np.full(len(index), op["sq_min_value"])
             else:
                 denom = np.maximum(1.0, dp_count)
-                dp_mean = (acc["normalized_sum"][index] +
-                           draw_noise(nk, sc[1], philox_for(seed, g, slot + 1))) / denom
-                dp_mean_sq = (acc["normalized_sum_sq"][index] +
-                              draw_noise(nk, sc[2], philox_for(seed, g, slot + 2))) / denom
+                dp_mean = noised(1, acc["normalized_sum"][index], slot + 1) / denom
+                dp_mean_sq = noised(2, acc["normalized_sum_sq"][index], slot + 2) / denom
             dp_var = dp_mean_sq - dp_mean * dp_mean
             if not op.get("degenerate", 0):
                 dp_mean = dp_mean + op["middle"]
@@ -366,10 +484,10 @@ def noise_metrics(ops, index, acc, sum_is_int, noised_count, seed, partition_off
 ADD_NOISE_SLOT = 0x41444E00  # pdp_select.hip kAddNoiseSlot
 
 
-def add_noise(values, noise_kind, scale, seed, index_offset=0):
+def add_noise(values, noise, seed, index_offset=0):
     """DPEngine.add_dp_noise's "Add noise" map (dp_engine.py:595-599):
-    float(value) + noise, element i drawing from Philox (seed, offset + i)."""
+    mechanism.add_noise(float(value)), element i drawing from the Philox
+    streams (seed, offset + i)."""
     x = np.asarray(values)
     idx = np.arange(x.shape[0], dtype=np.int64) + int(index_offset)
-    r = philox_for(int(seed), idx, ADD_NOISE_SLOT)
-    return x.astype(np.float64) + draw_noise(noise_kind, float(scale), r)
+    return secure_add_noise(noise, x.astype(np.float64), int(seed), idx, ADD_NOISE_SLOT)

@@ -14,9 +14,15 @@ against the known answers the reference's own tests hold:
 * create_partition_strategy("truncated_geometric" | "laplace" | "gaussian",
   eps, delta, l0[, pre_threshold]) with should_keep / probability_of_keep /
   noised_value_if_should_keep / threshold.
+* The secure (granularity-snapped) samplers' parameters: laplace_params /
+  gaussian_params restate Google's LaplaceDistribution / GaussianDistribution
+  (granularity = next power of two of b / 2^40, resp. 2 sigma / 2^28.5;
+  geometric rate g eps / (sensitivity + g); binomial step, bound and
+  coefficients of ApproximateBinomialProbability); the samplers themselves
+  are restated in oracle/columnar.py (secure_*).
   Parity unpinned: per-partition delta for l0 > 1 (1-(1-delta)^(1/l0) here),
-  pre_threshold for the thresholding strategies, PyDP's secure (granular)
-  noise samplers — checked distributionally only.
+  pre_threshold for the thresholding strategies, and the samplers' output
+  (PyDP draws from an unseeded secure RNG) — checked distributionally only.
 
 Independent of pipelinedp_amd (this is the checker, not the product).
 """
@@ -51,6 +57,37 @@ def calibrate_gaussian_sigma(eps, delta, l2):
         else:
             hi = mid
     return hi
+
+
+GRANULARITY_PARAM = float(1 << 40)   # Google DP LaplaceDistribution kGranularityParam
+BINOMIAL_BOUND = float(1 << 57)      # Google DP GaussianDistribution kBinomialBound
+
+
+def next_power_of_two(x):
+    """GetNextPowerOfTwo: 2^ceil(log2 x) (0 for x <= 0, as pow(2, -inf))."""
+    return math.pow(2.0, math.ceil(math.log2(x))) if x > 0 else 0.0
+
+
+def laplace_params(epsilon, sensitivity):
+    """Secure Laplace parameters (pdp_noise_params, kind 0) for (eps, l1)."""
+    b = sensitivity / epsilon if epsilon > 0 else math.inf
+    g = next_power_of_two(b / GRANULARITY_PARAM) if math.isfinite(b) else 0.0
+    lam = g * epsilon / (sensitivity + g) if g > 0 else 0.0
+    return dict(kind=0, scale=b, granularity=g, **{"lambda": lam}, step=0, n=0.0, bound=0.0, coef=0.0, corr=0.0)
+
+
+def gaussian_params(sigma):
+    """Secure Gaussian parameters (pdp_noise_params, kind 1) for std sigma."""
+    g = next_power_of_two(2.0 * sigma / math.sqrt(BINOMIAL_BOUND))
+    if g == 0.0:
+        return dict(kind=1, scale=sigma, granularity=0.0, **{"lambda": 0.0}, step=0, n=0.0, bound=0.0,
+                    coef=0.0, corr=0.0)
+    sqrt_n = 2.0 * sigma / g
+    n = sqrt_n * sqrt_n
+    return dict(kind=1, scale=sigma, granularity=g, **{"lambda": 0.0},
+                step=int(math.floor(math.sqrt(2.0) * sqrt_n + 1 + 0.5)),  # std::round, positive
+                n=n, bound=sqrt_n * math.sqrt(math.log(n) / 2), coef=math.sqrt(2 / math.pi) / sqrt_n,
+                corr=1 - 0.4 * math.pow(2 * math.log(n), 1.5) / sqrt_n)
 
 
 class LaplaceMechanism:

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 5
+ABI_VERSION = 6
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 SELECT_ALL_NONEMPTY = 0
@@ -29,7 +29,7 @@ OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID 
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
 ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED, ALGO_PAIR_TABLE = 0, 1, 2, 3
 MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
-KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT = 0, 1, 2
+KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED = 0, 1, 2, 3
 MAX_L0 = 256
 MAX_LINF = 256
 MAX_CONTRIBUTIONS = 256
@@ -115,6 +115,22 @@ class PartitionAccumulators(ctypes.Structure):
     ]
 
 
+class NoiseParams(ctypes.Structure):
+    """pdp_noise_params: one secure (granularity-snapped) mechanism."""
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("scale", ctypes.c_double),
+        ("granularity", ctypes.c_double),
+        ("lambda_", ctypes.c_double),
+        ("step", ctypes.c_int64),
+        ("n", ctypes.c_double),
+        ("bound", ctypes.c_double),
+        ("coef", ctypes.c_double),
+        ("corr", ctypes.c_double),
+    ]
+
+
 class SelectConfig(ctypes.Structure):
     _fields_ = [
         ("n_partitions", ctypes.c_int64),
@@ -124,7 +140,7 @@ class SelectConfig(ctypes.Structure):
         ("pre_threshold", ctypes.c_int32),
         ("keep_table_len", ctypes.c_int32),
         ("keep_prob", ctypes.c_void_p),
-        ("noise_scale", ctypes.c_double),
+        ("noise", NoiseParams),
         ("threshold", ctypes.c_double),
         ("public_mask", ctypes.c_void_p),
         ("seed", ctypes.c_uint64),
@@ -134,14 +150,12 @@ class SelectConfig(ctypes.Structure):
 class MetricOp(ctypes.Structure):
     _fields_ = [
         ("kind", ctypes.c_int32),
-        ("noise_kind", ctypes.c_int32),
+        ("degenerate", ctypes.c_int32),
         ("out_col", ctypes.c_int32 * 4),
-        ("scale", ctypes.c_double * 3),
+        ("noise", NoiseParams * 3),
         ("middle", ctypes.c_double),
         ("min_value", ctypes.c_double),
         ("sq_min_value", ctypes.c_double),
-        ("degenerate", ctypes.c_int32),
-        ("pad", ctypes.c_int32),
     ]
 
 
@@ -177,7 +191,7 @@ def _declare(lib):
         "pdp_compact": (ctypes.c_int, [vp, i64, vp, vp, vp, u64, vp]),
         "pdp_noise_metrics": (ctypes.c_int, [P(MetricOp), i32, vp, i64, vp, i64,
                                              P(PartitionAccumulators), i32, vp, vp, i64, u64, vp]),
-        "pdp_add_noise": (ctypes.c_int, [vp, i32, i64, i32, ctypes.c_double, u64, i64, vp, vp]),
+        "pdp_add_noise": (ctypes.c_int, [vp, i32, i64, P(NoiseParams), u64, i64, vp, vp]),
         "pdp_dataset_histograms_workspace_bytes": (ctypes.c_int, [i64, i64, i64, P(u64)]),
         "pdp_dataset_histograms": (ctypes.c_int, [vp, vp, vp, i32, i64, i64, i64, P(HistogramBins),
                                                   vp, u64, vp]),

@@ -166,7 +166,7 @@ def _closure_objects(fn, depth=0):
 
 
 def noise_mechanism_of(noise_fn):
-    """(PDP_NOISE_*, b or sigma) of the add_dp_noise lambda: the
+    """Secure sampler (dpc.NoiseParams) of the add_dp_noise lambda: the
     MechanismSpec and Sensitivities its create_mechanism() closes over
     (dp_engine.py:580-593), recomputed with the mirror's mechanisms."""
     spec = sens = None
@@ -328,10 +328,9 @@ def _noise_kind_code(kind) -> int:
     return N.NOISE_GAUSSIAN if _enum_value(kind) == "gaussian" else N.NOISE_LAPLACE
 
 
-def _additive(spec, sens):
-    mech = dpc.create_additive_mechanism(spec, sens)
-    return (N.NOISE_GAUSSIAN if isinstance(mech, dpc.GaussianMechanism) else N.NOISE_LAPLACE,
-            float(mech.noise_parameter))
+def _additive(spec, sens) -> dpc.NoiseParams:
+    """The secure sampler of create_additive_mechanism(spec, sens)."""
+    return dpc.create_additive_mechanism(spec, sens).secure_params()
 
 
 def build_metrics_program(compound, params) -> MetricsProgram:
@@ -353,10 +352,10 @@ def build_metrics_program(compound, params) -> MetricsProgram:
     for c in compound._combiners:
         name = type(c).__name__
         if name == "CountCombiner":
-            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
-            prog.ops.append(MetricOpSpec(kind=N.OP_COUNT, noise_kind=nk, out_col=(out("count"),), scale=(sc,)))
+            prog.ops.append(MetricOpSpec(kind=N.OP_COUNT, out_col=(out("count"),),
+                                         noise=(_additive(c._mechanism_spec, c._sensitivities),)))
         elif name == "SumCombiner":
-            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
+            nz = _additive(c._mechanism_spec, c._sensitivities)
             prog.needs_values = True
             if c._bounding_per_partition:
                 prog.flags |= N.SUM_PER_PARTITION
@@ -365,11 +364,10 @@ def build_metrics_program(compound, params) -> MetricsProgram:
             else:
                 prog.flags |= N.ACC_SUM
                 set_bounds(c._min_bound, c._max_bound)
-            prog.ops.append(MetricOpSpec(kind=N.OP_SUM, noise_kind=nk, out_col=(out("sum"),), scale=(sc,)))
+            prog.ops.append(MetricOpSpec(kind=N.OP_SUM, out_col=(out("sum"),), noise=(nz,)))
         elif name == "PrivacyIdCountCombiner":
-            nk, sc = _additive(c._mechanism_spec, c._sensitivities)
-            prog.ops.append(MetricOpSpec(kind=N.OP_PRIVACY_ID_COUNT, noise_kind=nk,
-                                         out_col=(out("privacy_id_count"),), scale=(sc,)))
+            prog.ops.append(MetricOpSpec(kind=N.OP_PRIVACY_ID_COUNT, out_col=(out("privacy_id_count"),),
+                                         noise=(_additive(c._mechanism_spec, c._sensitivities),)))
         elif name == "PostAggregationThresholdingCombiner":
             prog.threshold_combiner = c
             prog.ops.append(MetricOpSpec(kind=N.OP_THRESHOLDED_PID, out_col=(out("privacy_id_count"),)))
@@ -377,13 +375,12 @@ def build_metrics_program(compound, params) -> MetricsProgram:
             prog.needs_values = True
             prog.flags |= N.ACC_NSUM
             set_bounds(c._min_value, c._max_value)
-            ck, cs = _additive(c._count_spec, c._count_sensitivities)
-            _, ss = _additive(c._sum_spec, c._sum_sensitivities)
+            cn = _additive(c._count_spec, c._count_sensitivities)
+            sn = _additive(c._sum_spec, c._sum_sensitivities)
             names = c._metrics_to_compute
             cols = (out("mean"), out("count") if "count" in names else -1,
                     out("sum") if "sum" in names else -1)
-            prog.ops.append(MetricOpSpec(kind=N.OP_MEAN, noise_kind=ck, out_col=cols, scale=(cs, ss),
-                                         middle=prog.middle))
+            prog.ops.append(MetricOpSpec(kind=N.OP_MEAN, out_col=cols, noise=(cn, sn), middle=prog.middle))
         elif name == "VarianceCombiner":
             prog.needs_values = True
             prog.flags |= N.ACC_NSUM | N.ACC_NSUM2
@@ -393,13 +390,12 @@ def build_metrics_program(compound, params) -> MetricsProgram:
                 c._params.eps, c._params.delta, p.min_value, p.max_value, p.min_sum_per_partition,
                 p.max_sum_per_partition, p.max_partitions_contributed,
                 p.max_contributions_per_partition, _to_local_noise_kind(p.noise_kind))
-            scales = pdc.variance_noise_scales(noise_params)
+            noise = pdc.variance_noise_params(noise_params)
             names = c._metrics_to_compute
             cols = (out("variance"), out("count") if "count" in names else -1,
                     out("sum") if "sum" in names else -1, out("mean") if "mean" in names else -1)
             lo, hi = p.min_value, p.max_value
-            prog.ops.append(MetricOpSpec(kind=N.OP_VARIANCE, noise_kind=_noise_kind_code(p.noise_kind),
-                                         out_col=cols, scale=scales, middle=prog.middle,
+            prog.ops.append(MetricOpSpec(kind=N.OP_VARIANCE, out_col=cols, noise=noise, middle=prog.middle,
                                          min_value=float(lo),
                                          sq_min_value=float(dpc.compute_squares_interval(lo, hi)[0]),
                                          degenerate=int(lo == hi)))
@@ -747,7 +743,7 @@ class AddNoiseRun:
     def run(self) -> List:
         import torch
         from pipelinedp_amd import executor as X
-        kind, scale = noise_mechanism_of(self.plan.noise_fn)
+        noise = noise_mechanism_of(self.plan.noise_fn)
         device = self.backend._torch_device()
         src = self.plan.source
         if isinstance(src, C.ColumnTable) and len(src.names) == 2:
@@ -760,7 +756,7 @@ class AddNoiseRun:
         val_t = _value_tensor(vals, device)
         offset = parallel.row_offset(int(val_t.numel()))
         _, _, seed_noise = parallel.broadcast_seeds(self.backend._seeds())
-        out = X.add_noise(val_t, noise_kind=kind, scale=scale, seed=seed_noise, index_offset=offset)
+        out = X.add_noise(val_t, noise=noise, seed=seed_noise, index_offset=offset)
         noised = out.cpu().numpy().tolist()
         if C._is_torch(keys):
             keys = keys.cpu().numpy()

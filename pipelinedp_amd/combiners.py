@@ -383,24 +383,37 @@ def variance_noise_scales(dp_params: dpc.ScalarNoiseParams):
             dpc.noise_scale(kind, qe, qd, l0, linf * abs(sq_mid - sq_lo)))
 
 
+def variance_noise_params(dp_params: dpc.ScalarNoiseParams):
+    """Secure samplers of compute_dp_var's three mechanisms (the scales of
+    variance_noise_scales); the sums' samplers are absent (no noise) when
+    min_value == max_value."""
+    (ce, cd), (se, sd), (qe, qd) = dpc.equally_split_budget(dp_params.eps, dp_params.delta, 3)
+    l0 = dp_params.l0_sensitivity()
+    linf = dp_params.max_contributions_per_partition
+    kind = dp_params.noise_kind
+    lo, hi = dp_params.min_value, dp_params.max_value
+    mid = dpc.compute_middle(lo, hi)
+    sq_lo, sq_hi = dpc.compute_squares_interval(lo, hi)
+    sq_mid = dpc.compute_middle(sq_lo, sq_hi)
+    count = dpc.noise_params(kind, ce, cd, l0, linf)
+    if lo == hi:
+        return count, dpc.NO_NOISE, dpc.NO_NOISE
+    return (count, dpc.noise_params(kind, se, sd, l0, linf * abs(mid - lo)),
+            dpc.noise_params(kind, qe, qd, l0, linf * abs(sq_mid - sq_lo)))
+
+
 def compute_dp_var(count, normalized_sum, normalized_sum_squares, dp_params):
     """Host restatement of dp_computations.compute_dp_var (single partition)."""
-    cs, ss, qs = variance_noise_scales(dp_params)
-    rng = np.random.default_rng()
-
-    def noise(scale):
-        if dp_params.noise_kind == agg.NoiseKind.LAPLACE:
-            return rng.laplace(0.0, scale)
-        return rng.normal(0.0, scale)
-
+    cn, sn, qn = variance_noise_params(dp_params)
+    smp = dpc.secure_sampler()
     lo, hi = dp_params.min_value, dp_params.max_value
-    dp_count = count + noise(cs)
+    dp_count = smp.add_noise(cn, count)
     if lo == hi:
         dp_mean, dp_mean_sq = lo, dpc.compute_squares_interval(lo, hi)[0]
     else:
         denom = max(1.0, dp_count)
-        dp_mean = (normalized_sum + noise(ss)) / denom
-        dp_mean_sq = (normalized_sum_squares + noise(qs)) / denom
+        dp_mean = smp.add_noise(sn, normalized_sum) / denom
+        dp_mean_sq = smp.add_noise(qn, normalized_sum_squares) / denom
     dp_var = dp_mean_sq - dp_mean**2
     if lo != hi:
         dp_mean += dpc.compute_middle(lo, hi)

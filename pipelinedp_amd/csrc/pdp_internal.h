@@ -138,20 +138,107 @@ __device__ __forceinline__ U4 philox_for(uint64_t seed, int64_t gidx, uint32_t s
   return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-__device__ __forceinline__ double laplace_noise(double b, U4 r) {
-  const double u = u01(r.x, r.y) - 0.5;  // (-0.5, 0.5)
-  const double mag = -b * log1p(-2.0 * fabs(u));
-  return u < 0.0 ? -mag : mag;
+// ------------------------------------------------------- secure noise --
+// Granularity-snapped samplers of Google's differential-privacy library
+// (what PyDP's numerical_mechanisms call; restated from its published
+// algorithm, see pdp_noise_params in pipelinedp_amd.h).  Every draw reads the
+// Philox blocks k = 0, 1, ... of the stream (seed, gidx, slot); the oracle
+// (oracle/columnar.py secure_noise) consumes them in the same order.
+__device__ __forceinline__ U4 noise_block(uint64_t seed, int64_t gidx, uint32_t slot, uint32_t k) {
+  U4 c{(uint32_t)((uint64_t)gidx), (uint32_t)((uint64_t)gidx >> 32), slot, 0x4E000000u + k};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-__device__ __forceinline__ double gaussian_noise(double sigma, U4 r) {
-  const double u1 = u01(r.x, r.y);
-  const double u2 = u01(r.z, r.w);
-  return sigma * sqrt(-2.0 * log(u1)) * cos(6.283185307179586476925286766559 * u2);
+// RoundToNearestDoubleMultiple: exact for a power-of-two base; ties go toward
+// zero (|remainder| == base / 2 keeps n - remainder)
+__device__ __forceinline__ double round_to_multiple(double x, double base) {
+  if (base == 0.0) return x;
+  const double r = fmod(x, base);
+  if (fabs(r) > base / 2) return x - r + copysign(base, r);
+  return x - r;
 }
 
-__device__ __forceinline__ double draw_noise(int kind, double scale, U4 r) {
-  return kind == PDP_NOISE_GAUSSIAN ? gaussian_noise(scale, r) : laplace_noise(scale, r);
+// Geometric sample P(X = j) = (1 - e^-lambda) e^(-lambda j), j >= 0: bisection
+// of (lo, hi] over the integers; each step keeps the lower half with its exact
+// conditional mass q = expm1(-lambda (mid - lo)) / expm1(-lambda (hi - lo)).
+// Steps with q == 1 (the far tail has no mass at fp64) draw nothing; the
+// others each read one uniform (two per Philox block).
+__device__ __forceinline__ int64_t secure_geometric(double lambda, uint64_t seed, int64_t gidx, uint32_t slot,
+                                                    uint32_t& k) {
+  int64_t lo = 0, hi = INT64_MAX;
+  U4 blk{0, 0, 0, 0};
+  int half = 0;  // 0: next uniform from a fresh block's (x, y); 1: from (z, w)
+  while (lo + 1 < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    const double q = expm1(lambda * (double)(lo - mid)) / expm1(lambda * (double)(lo - hi));
+    if (q >= 1.0) {
+      hi = mid;
+      continue;
+    }
+    double u;
+    if (half == 0) {
+      blk = noise_block(seed, gidx, slot, k++);
+      u = u01(blk.x, blk.y);
+    } else {
+      u = u01(blk.z, blk.w);
+    }
+    half ^= 1;
+    if (u <= q) hi = mid;
+    else lo = mid;
+  }
+  return hi - 1;
+}
+
+// LaplaceDistribution::Sample: g * two-sided geometric (a zero with a
+// negative sign is redrawn, so 0 is not counted twice)
+__device__ __forceinline__ double secure_laplace(const pdp_noise_params& np, uint64_t seed, int64_t gidx,
+                                                 uint32_t slot) {
+  uint32_t k = 0;
+  for (;;) {
+    const U4 a = noise_block(seed, gidx, slot, k++);
+    const bool positive = (a.x >> 31) != 0;
+    const int64_t s = secure_geometric(np.lambda, seed, gidx, slot, k);
+    if (s == 0 && !positive) continue;
+    return (positive ? (double)s : -(double)s) * np.granularity;
+  }
+}
+
+// GaussianDistribution::Sample: g * (Binomial(n, 1/2) - n/2) by rejection from
+// a two-sided geometric(1/2) over blocks of `step` integers; acceptance
+// uses Google's approximate binomial probability (Secure Noise Generation,
+// Lemma 7).  Two Philox blocks per attempt: (x, y) geometric bits, z sign;
+// then (x, y) the uniform offset in [0, step), (z, w) the acceptance uniform.
+__device__ __forceinline__ double secure_gaussian(const pdp_noise_params& np, uint64_t seed, int64_t gidx,
+                                                  uint32_t slot) {
+  uint32_t k = 0;
+  const uint64_t step = (uint64_t)np.step;
+  for (;;) {
+    const U4 a = noise_block(seed, gidx, slot, k++);
+    const U4 b = noise_block(seed, gidx, slot, k++);
+    int geom;
+    if (a.x != 0xFFFFFFFFu) geom = __clz(~a.x);
+    else if (a.y != 0xFFFFFFFFu) geom = 32 + __clz(~a.y);
+    else geom = 64;  // probability 2^-64: capped
+    const int64_t two_sided = (a.z >> 31) ? (int64_t)geom : -(int64_t)geom - 1;
+    // floor(r * step / 2^64) for the 64 random bits r = (b.x, b.y); step < 2^32
+    const uint64_t hi_part = (uint64_t)b.x * step + (((uint64_t)b.y * step) >> 32);
+    const int64_t uni = (int64_t)(hi_part >> 32);
+    const int64_t m = (int64_t)step * two_sided + uni;
+    const double accept_u = u01(b.z, b.w);
+    const double md = (double)m;
+    if (fabs(md) > np.bound) continue;
+    const double prob = np.coef * exp(-2.0 * md * md / np.n) * np.corr;
+    if (prob > 0.0 && accept_u < prob * (double)np.step * ldexp(1.0, geom) / 4.0) return md * np.granularity;
+  }
+}
+
+// mechanism.add_noise(x): x snapped to the grid plus a grid-valued sample
+__device__ __forceinline__ double secure_add_noise(const pdp_noise_params& np, double x, uint64_t seed,
+                                                   int64_t gidx, uint32_t slot) {
+  if (np.granularity == 0.0) return x;
+  const double noise = np.kind == PDP_NOISE_GAUSSIAN ? secure_gaussian(np, seed, gidx, slot)
+                                                     : secure_laplace(np, seed, gidx, slot);
+  return round_to_multiple(x, np.granularity) + noise;
 }
 
 // ------------------------------------------------- sorted-sketch insertion --

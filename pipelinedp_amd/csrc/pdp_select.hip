@@ -14,6 +14,22 @@
 #include "pdp_internal.h"
 
 namespace pdp {
+
+// host-side validation of one mechanism's parameters (pdp_noise_params)
+int check_noise(const pdp_noise_params* np) {
+  if (np == nullptr) return set_error(PDP_E_INVALID, "noise params are NULL");
+  if (np->kind != PDP_NOISE_LAPLACE && np->kind != PDP_NOISE_GAUSSIAN) return set_error(PDP_E_INVALID, "bad noise kind");
+  if (!(np->granularity >= 0.0) || !std::isfinite(np->granularity))
+    return set_error(PDP_E_INVALID, "noise granularity must be finite and >= 0");
+  if (np->granularity == 0.0) return PDP_OK;  // no noise
+  if (np->kind == PDP_NOISE_LAPLACE && !(np->lambda > 0.0 && std::isfinite(np->lambda)))
+    return set_error(PDP_E_INVALID, "Laplace noise needs a finite lambda > 0");
+  if (np->kind == PDP_NOISE_GAUSSIAN &&
+      (np->step < 1 || np->step >= ((int64_t)1 << 32) || !(np->n > 1.0) || !(np->bound > 0.0) || !(np->coef > 0.0)))
+    return set_error(PDP_E_INVALID, "Gaussian noise needs 1 <= step < 2^32, n > 1, bound > 0, coef > 0");
+  return PDP_OK;
+}
+
 namespace {
 
 __global__ void __launch_bounds__(kBlock) k_select(pdp_select_config cfg, const int64_t* __restrict__ row_count,
@@ -38,14 +54,12 @@ __global__ void __launch_bounds__(kBlock) k_select(pdp_select_config cfg, const 
         n -= shift;
       }
       if (pre_ok) {
-        const U4 r = philox_for(cfg.seed, cfg.partition_offset + p, 0x53454C00u);
         if (cfg.strategy == PDP_SELECT_TRUNCATED_GEOMETRIC) {
+          const U4 r = philox_for(cfg.seed, cfg.partition_offset + p, 0x53454C00u);
           const int64_t t = n < cfg.keep_table_len ? n : (int64_t)cfg.keep_table_len - 1;
           kp = u01(r.x, r.y) < cfg.keep_prob[t];
-        } else {
-          const double v = (double)n + (cfg.strategy == PDP_SELECT_GAUSSIAN_THRESHOLDING
-                                            ? gaussian_noise(cfg.noise_scale, r)
-                                            : laplace_noise(cfg.noise_scale, r));
+        } else {  // PyDP Laplace/GaussianPartitionSelection: mechanism.AddNoise(n) > threshold
+          const double v = secure_add_noise(cfg.noise, (double)n, cfg.seed, cfg.partition_offset + p, 0x53454C00u);
           kp = v > cfg.threshold;
           if (kp) nz = v + (double)shift;
         }
@@ -132,14 +146,15 @@ __global__ void __launch_bounds__(kBlock) k_compact_write(const uint8_t* __restr
 }
 
 
-// DPEngine.add_dp_noise (dp_engine.py:551-607): y[i] = float(x[i]) + noise,
-// one Philox4x32-10 draw per element keyed by (seed, index_offset + i).  One
-// 16-byte load + one 16-byte store per thread step (2 elements): HBM-bound.
+// DPEngine.add_dp_noise (dp_engine.py:551-607): y[i] = mechanism.add_noise(
+// float(x[i])), the secure sampler reading the Philox streams (seed,
+// index_offset + i).  One 16-byte load + one 16-byte store per thread step (2
+// elements); the samplers' fp64 transcendentals, not HBM, set its rate.
 constexpr uint32_t kAddNoiseSlot = 0x41444E00u;  // "ADN"
 
 template <int VALUE_KIND>
-__global__ void __launch_bounds__(kBlock) k_add_noise(const void* __restrict__ x, int64_t n, int kind,
-                                                      double scale, uint64_t seed, int64_t index_offset,
+__global__ void __launch_bounds__(kBlock) k_add_noise(const void* __restrict__ x, int64_t n,
+                                                      pdp_noise_params np, uint64_t seed, int64_t index_offset,
                                                       double* __restrict__ y) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t pairs = n >> 1;
@@ -156,14 +171,14 @@ __global__ void __launch_bounds__(kBlock) k_add_noise(const void* __restrict__ x
       b = v.y;
     }
     double2 o;
-    o.x = a + draw_noise(kind, scale, philox_for(seed, index_offset + i, kAddNoiseSlot));
-    o.y = b + draw_noise(kind, scale, philox_for(seed, index_offset + i + 1, kAddNoiseSlot));
+    o.x = secure_add_noise(np, a, seed, index_offset + i, kAddNoiseSlot);
+    o.y = secure_add_noise(np, b, seed, index_offset + i + 1, kAddNoiseSlot);
     reinterpret_cast<double2*>(y)[t] = o;
   }
   if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     const int64_t i = n - 1;
     const double a = VALUE_KIND == PDP_VALUE_I64 ? (double)((const long long*)x)[i] : ((const double*)x)[i];
-    y[i] = a + draw_noise(kind, scale, philox_for(seed, index_offset + i, kAddNoiseSlot));
+    y[i] = secure_add_noise(np, a, seed, index_offset + i, kAddNoiseSlot);
   }
 }
 
@@ -197,25 +212,24 @@ __global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops
       const uint32_t slot = (uint32_t)o << 4;
       switch (op.kind) {
         case PDP_OP_COUNT: {
-          const double v = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          const double v = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
           put(out, out_stride, op.out_col[0], i, v);
           break;
         }
         case PDP_OP_SUM: {
           const double s = sum_is_int ? (double)((const long long*)acc.sum)[p] : ((const double*)acc.sum)[p];
-          put(out, out_stride, op.out_col[0], i, s + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot)));
+          put(out, out_stride, op.out_col[0], i, secure_add_noise(op.noise[0], s, seed, g, slot));
           break;
         }
         case PDP_OP_PRIVACY_ID_COUNT: {
-          const double v = (double)acc.privacy_id_count[p] +
-                           draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          const double v = secure_add_noise(op.noise[0], (double)acc.privacy_id_count[p], seed, g, slot);
           put(out, out_stride, op.out_col[0], i, v);
           break;
         }
         case PDP_OP_MEAN: {
-          const double dp_count = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          const double dp_count = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
           const double denom = fmax(1.0, dp_count);
-          const double dp_nsum = acc.normalized_sum[p] + draw_noise(op.noise_kind, op.scale[1], philox_for(seed, g, slot + 1));
+          const double dp_nsum = secure_add_noise(op.noise[1], acc.normalized_sum[p], seed, g, slot + 1);
           const double mean = op.middle + dp_nsum / denom;
           put(out, out_stride, op.out_col[0], i, mean);
           put(out, out_stride, op.out_col[1], i, dp_count);
@@ -223,15 +237,15 @@ __global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops
           break;
         }
         case PDP_OP_VARIANCE: {
-          const double dp_count = (double)acc.count[p] + draw_noise(op.noise_kind, op.scale[0], philox_for(seed, g, slot));
+          const double dp_count = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
           double dp_mean, dp_mean_sq;
           if (op.degenerate) {
             dp_mean = op.min_value;
             dp_mean_sq = op.sq_min_value;
           } else {
             const double denom = fmax(1.0, dp_count);
-            dp_mean = (acc.normalized_sum[p] + draw_noise(op.noise_kind, op.scale[1], philox_for(seed, g, slot + 1))) / denom;
-            dp_mean_sq = (acc.normalized_sum_sq[p] + draw_noise(op.noise_kind, op.scale[2], philox_for(seed, g, slot + 2))) / denom;
+            dp_mean = secure_add_noise(op.noise[1], acc.normalized_sum[p], seed, g, slot + 1) / denom;
+            dp_mean_sq = secure_add_noise(op.noise[2], acc.normalized_sum_sq[p], seed, g, slot + 2) / denom;
           }
           const double dp_var = dp_mean_sq - dp_mean * dp_mean;
           if (!op.degenerate) dp_mean += op.middle;
@@ -271,6 +285,10 @@ int pdp_select_partitions(const pdp_select_config* cfg, const int64_t* row_count
     return pdp::set_error(PDP_E_INVALID, "keep_prob table is required");
   if (cfg->strategy != PDP_SELECT_PUBLIC && row_count == nullptr)
     return pdp::set_error(PDP_E_INVALID, "row_count is required");
+  if (cfg->strategy == PDP_SELECT_LAPLACE_THRESHOLDING || cfg->strategy == PDP_SELECT_GAUSSIAN_THRESHOLDING) {
+    const int rc = pdp::check_noise(&cfg->noise);
+    if (rc != PDP_OK) return rc;
+  }
   if (cfg->n_partitions == 0) return PDP_OK;
   PDP_PROF_BEGIN("k_select", (hipStream_t)stream);
   hipLaunchKernelGGL(k_select, dim3(grid_for(cfg->n_partitions)), dim3(kBlock), 0, (hipStream_t)stream,
@@ -353,6 +371,11 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
       default:
         return pdp::set_error(PDP_E_INVALID, "unknown op kind");
     }
+    const int nmech = o.kind == PDP_OP_MEAN ? 2 : (o.kind == PDP_OP_VARIANCE ? 3 : (o.kind == PDP_OP_THRESHOLDED_PID ? 0 : 1));
+    for (int m = 0; m < nmech; ++m) {
+      const int rc = pdp::check_noise(&o.noise[m]);
+      if (rc != PDP_OK) return rc;
+    }
     pack.op[i] = o;
   }
   PDP_PROF_BEGIN("k_noise_metrics", (hipStream_t)stream);
@@ -364,14 +387,13 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
   return PDP_OK;
 }
 
-int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noise_kind, double scale,
+int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, const pdp_noise_params* noise,
                   uint64_t seed, int64_t index_offset, double* out, void* stream) {
   if (n < 0) return pdp::set_error(PDP_E_INVALID, "n must be >= 0");
   if (value_kind != PDP_VALUE_F64 && value_kind != PDP_VALUE_I64)
     return pdp::set_error(PDP_E_INVALID, "value_kind must be PDP_VALUE_F64 or PDP_VALUE_I64");
-  if (noise_kind != PDP_NOISE_LAPLACE && noise_kind != PDP_NOISE_GAUSSIAN)
-    return pdp::set_error(PDP_E_INVALID, "bad noise_kind");
-  if (!(scale >= 0.0) || !std::isfinite(scale)) return pdp::set_error(PDP_E_INVALID, "scale must be finite and >= 0");
+  const int rc = pdp::check_noise(noise);
+  if (rc != PDP_OK) return rc;
   if (n == 0) return PDP_OK;
   if (values == nullptr || out == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
   if (((uintptr_t)values | (uintptr_t)out) & 15)
@@ -381,10 +403,10 @@ int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, int32_t noi
   PDP_PROF_BEGIN("k_add_noise", st);
   if (value_kind == PDP_VALUE_I64)
     hipLaunchKernelGGL(k_add_noise<PDP_VALUE_I64>, dim3(grid_for(pairs)), dim3(kBlock), 0, st, values, n,
-                       noise_kind, scale, seed, index_offset, out);
+                       *noise, seed, index_offset, out);
   else
     hipLaunchKernelGGL(k_add_noise<PDP_VALUE_F64>, dim3(grid_for(pairs)), dim3(kBlock), 0, st, values, n,
-                       noise_kind, scale, seed, index_offset, out);
+                       *noise, seed, index_offset, out);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;

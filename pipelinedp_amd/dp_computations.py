@@ -12,6 +12,10 @@ python-dp (PyDP ~=1.1.5rc4, Google differential-privacy C++):
 * Partition selection (partition_selection.py:29-44 -> PyDP
   create_partition_strategy): truncated-geometric keep probability,
   Laplace / Gaussian thresholding thresholds.
+* The secure noise of those mechanisms (PyDP add_noise, dp_computations.py:
+  456-457, 508-509): Google's granularity-snapped samplers.  NoiseParams
+  holds one mechanism's grid and sampler constants (pdp_noise_params); the
+  kernels draw with them, SecureSampler draws single host values.
 
 These are scalars computed once per aggregation on the host; the per-partition
 work (noise draws, keep decisions) runs in the HIP kernels.
@@ -129,6 +133,145 @@ def laplace_diversity(eps: float, l1_sensitivity: float) -> float:
     if eps <= 0:
         raise ValueError(f"epsilon must be positive, but {eps} given")
     return l1_sensitivity / eps
+
+
+# --------------------------------------------------------------- secure noise --
+_GRANULARITY_PARAM = float(1 << 40)  # Laplace: b / 2^40 -> the grid
+_BINOMIAL_BOUND = float(1 << 57)     # Gaussian: about 2^57 binomial trials
+
+
+def _next_power_of_two(x: float) -> float:
+    return math.pow(2.0, math.ceil(math.log2(x))) if x > 0 else 0.0
+
+
+@dataclasses.dataclass(frozen=True)
+class NoiseParams:
+    """One additive mechanism's secure sampler (pdp_noise_params).
+
+    Laplace(eps, l1): granularity g = 2^ceil(log2(b / 2^40)), b = l1 / eps;
+    noise = g * k with P(k) ~ exp(-lambda |k|), lambda = g eps / (l1 + g).
+    Gaussian(sigma): g = 2^ceil(log2(2 sigma / 2^28.5)), sqrt_n = 2 sigma / g;
+    noise = g * (Binomial(sqrt_n^2, 1/2) - sqrt_n^2 / 2) by rejection.
+    add_noise(x) = round_to_multiple(x, g) + noise; g = 0: no noise."""
+    kind: int                 # 0 Laplace, 1 Gaussian (N.NOISE_*)
+    scale: float              # b or sigma
+    granularity: float
+    lam: float = 0.0
+    step: int = 0
+    n: float = 0.0
+    bound: float = 0.0
+    coef: float = 0.0
+    corr: float = 0.0
+
+    def to_c(self):
+        from pipelinedp_amd import _native as N
+        c = N.NoiseParams()
+        c.kind, c.scale, c.granularity, c.lambda_ = self.kind, self.scale, self.granularity, self.lam
+        c.step, c.n, c.bound, c.coef, c.corr = self.step, self.n, self.bound, self.coef, self.corr
+        return c
+
+    def as_dict(self) -> dict:
+        return {"kind": self.kind, "scale": self.scale, "granularity": self.granularity,
+                "lambda": self.lam, "step": self.step, "n": self.n, "bound": self.bound,
+                "coef": self.coef, "corr": self.corr}
+
+
+NO_NOISE = NoiseParams(kind=0, scale=0.0, granularity=0.0)
+
+
+def laplace_noise_params(eps: float, l1_sensitivity: float) -> NoiseParams:
+    """Google LaplaceDistribution(epsilon, sensitivity) constants."""
+    b = laplace_diversity(eps, l1_sensitivity)
+    if not math.isfinite(b) or b <= 0:
+        return NoiseParams(kind=0, scale=max(b, 0.0) if math.isfinite(b) else b, granularity=0.0)
+    g = _next_power_of_two(b / _GRANULARITY_PARAM)
+    return NoiseParams(kind=0, scale=b, granularity=g, lam=g * eps / (l1_sensitivity + g))
+
+
+def gaussian_noise_params(sigma: float) -> NoiseParams:
+    """Google GaussianDistribution(stddev) constants (binomial sampler)."""
+    g = _next_power_of_two(2.0 * sigma / math.sqrt(_BINOMIAL_BOUND))
+    if g == 0.0 or not math.isfinite(g):
+        return NoiseParams(kind=1, scale=sigma, granularity=0.0)
+    sqrt_n = 2.0 * sigma / g
+    n = sqrt_n * sqrt_n
+    return NoiseParams(kind=1, scale=sigma, granularity=g,
+                       step=int(math.floor(math.sqrt(2.0) * sqrt_n + 1.0 + 0.5)), n=n,
+                       bound=sqrt_n * math.sqrt(math.log(n) / 2), coef=math.sqrt(2 / math.pi) / sqrt_n,
+                       corr=1 - 0.4 * math.pow(2 * math.log(n), 1.5) / sqrt_n)
+
+
+def round_to_multiple(x: float, base: float) -> float:
+    """RoundToNearestDoubleMultiple (ties toward zero)."""
+    if base == 0.0:
+        return x
+    r = math.fmod(x, base)
+    if abs(r) > base / 2:
+        return x - r + math.copysign(base, r)
+    return x - r
+
+
+class SecureSampler:
+    """Host draw of the same samplers for single values (API parity: the
+    reference's mechanism.add_noise outside a pipeline).  Randomness comes
+    from the OS CSPRNG; the pipelines' noise is drawn on the GPU."""
+
+    def __init__(self):
+        import secrets
+        self._bits = secrets.randbits
+
+    def _u01(self) -> float:
+        return ((self._bits(53)) + 0.5) / 9007199254740992.0
+
+    def _geometric(self, lam: float) -> int:
+        lo, hi = 0, (1 << 63) - 1
+        while lo + 1 < hi:
+            mid = lo + ((hi - lo) >> 1)
+            q = math.expm1(lam * float(lo - mid)) / math.expm1(lam * float(lo - hi))
+            if q >= 1.0 or self._u01() <= q:
+                hi = mid
+            else:
+                lo = mid
+        return hi - 1
+
+    def sample(self, p: NoiseParams) -> float:
+        if p.granularity == 0.0:
+            return 0.0
+        if p.kind == 0:
+            while True:
+                positive = self._bits(1) == 1
+                s = self._geometric(p.lam)
+                if s == 0 and not positive:
+                    continue
+                return (float(s) if positive else -float(s)) * p.granularity
+        while True:
+            geom = 0
+            while self._bits(1) == 1 and geom < 64:
+                geom += 1
+            two_sided = geom if self._bits(1) == 1 else -geom - 1
+            m = p.step * two_sided + ((self._bits(64) * p.step) >> 64)
+            u = self._u01()
+            md = float(m)
+            if abs(md) > p.bound:
+                continue
+            prob = p.coef * math.exp(-2.0 * md * md / p.n) * p.corr
+            if prob > 0.0 and u < prob * float(p.step) * math.ldexp(1.0, geom) / 4.0:
+                return md * p.granularity
+
+    def add_noise(self, p: NoiseParams, x: float) -> float:
+        if p.granularity == 0.0:
+            return float(x)
+        return round_to_multiple(float(x), p.granularity) + self.sample(p)
+
+
+_SAMPLER = None
+
+
+def secure_sampler() -> SecureSampler:
+    global _SAMPLER
+    if _SAMPLER is None:
+        _SAMPLER = SecureSampler()
+    return _SAMPLER
 
 
 def equally_split_budget(eps: float, delta: float, no_mechanisms: int):
@@ -254,8 +397,11 @@ class LaplaceMechanism(AdditiveMechanism):
         b = normalized_stddev / math.sqrt(2)
         return LaplaceMechanism(1 / b, l1_sensitivity)
 
+    def secure_params(self) -> NoiseParams:
+        return laplace_noise_params(self._epsilon, self._sensitivity)
+
     def add_noise(self, value) -> float:
-        return float(value) + float(np.random.default_rng().laplace(0.0, self._diversity))
+        return secure_sampler().add_noise(self.secure_params(), value)
 
     @property
     def noise_kind(self) -> agg.NoiseKind:
@@ -296,8 +442,11 @@ class GaussianMechanism(AdditiveMechanism):
     def create_from_std_deviation(cls, normalized_stddev: float, l2_sensitivity: float):
         return GaussianMechanism(normalized_stddev * l2_sensitivity, l2_sensitivity)
 
+    def secure_params(self) -> NoiseParams:
+        return gaussian_noise_params(self._sigma)
+
     def add_noise(self, value) -> float:
-        return float(value) + float(np.random.default_rng().normal(0.0, self._sigma))
+        return secure_sampler().add_noise(self.secure_params(), value)
 
     @property
     def noise_kind(self) -> agg.NoiseKind:
@@ -384,6 +533,16 @@ def create_mean_mechanism(range_middle, count_spec, count_sensitivities, normali
                           normalized_sum_sensitivities) -> MeanMechanism:
     return MeanMechanism(range_middle, create_additive_mechanism(count_spec, count_sensitivities),
                          create_additive_mechanism(normalized_sum_spec, normalized_sum_sensitivities))
+
+
+def noise_params(noise_kind: agg.NoiseKind, eps: float, delta: float, l0: float, linf: float) -> NoiseParams:
+    """Secure sampler of _add_random_noise (dp_computations.py:154-183) for
+    (eps, delta, l0, linf)."""
+    if noise_kind == agg.NoiseKind.LAPLACE:
+        return laplace_noise_params(eps, compute_l1_sensitivity(l0, linf))
+    if noise_kind == agg.NoiseKind.GAUSSIAN:
+        return gaussian_noise_params(compute_sigma(eps, delta, compute_l2_sensitivity(l0, linf)))
+    raise ValueError("Noise kind must be either Laplace or Gaussian.")
 
 
 def noise_scale(noise_kind: agg.NoiseKind, eps: float, delta: float, l0: float, linf: float) -> float:

@@ -18,6 +18,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from pipelinedp_amd import _native as N
+from pipelinedp_amd.dp_computations import NO_NOISE, NoiseParams
 
 
 @dataclasses.dataclass
@@ -51,32 +52,46 @@ class SelectionSpec:
     max_rows_per_privacy_id: int = 1
     pre_threshold: int = 0
     keep_prob: Optional[np.ndarray] = None
-    noise_scale: float = 0.0
+    noise: Optional[NoiseParams] = None  # thresholding strategies: the secure mechanism
     threshold: float = 0.0
     want_noised_count: bool = False
+
+    @property
+    def noise_scale(self) -> float:
+        return 0.0 if self.noise is None else self.noise.scale
 
 
 @dataclasses.dataclass
 class MetricOpSpec:
+    """One CompoundCombiner child's metric op (pdp_metric_op); `noise` holds
+    its mechanisms' secure samplers (COUNT/SUM/PID: 1, MEAN: 2, VARIANCE: 3)."""
     kind: int
-    noise_kind: int = N.NOISE_LAPLACE
     out_col: Sequence[int] = (-1, -1, -1, -1)
-    scale: Sequence[float] = (0.0, 0.0, 0.0)
+    noise: Sequence[NoiseParams] = ()
     middle: float = 0.0
     min_value: float = 0.0
     sq_min_value: float = 0.0
     degenerate: int = 0
 
+    @property
+    def scale(self):
+        return tuple(p.scale for p in self.noise)
+
+    @property
+    def noise_kind(self) -> int:
+        return self.noise[0].kind if self.noise else N.NOISE_LAPLACE
+
+    def _noise3(self):
+        return list(self.noise) + [NO_NOISE] * (3 - len(self.noise))
+
     def to_c(self) -> N.MetricOp:
         op = N.MetricOp()
         op.kind = self.kind
-        op.noise_kind = self.noise_kind
         cols = list(self.out_col) + [-1] * (4 - len(self.out_col))
         for i in range(4):
             op.out_col[i] = int(cols[i])
-        sc = list(self.scale) + [0.0] * (3 - len(self.scale))
-        for i in range(3):
-            op.scale[i] = float(sc[i])
+        for i, p in enumerate(self._noise3()):
+            op.noise[i] = p.to_c()
         op.middle = float(self.middle)
         op.min_value = float(self.min_value)
         op.sq_min_value = float(self.sq_min_value)
@@ -85,8 +100,7 @@ class MetricOpSpec:
 
     def as_dict(self) -> dict:
         cols = list(self.out_col) + [-1] * (4 - len(self.out_col))
-        return dict(kind=self.kind, noise_kind=self.noise_kind, out_col=cols,
-                    scale=list(self.scale) + [0.0] * (3 - len(self.scale)),
+        return dict(kind=self.kind, out_col=cols, noise=[p.as_dict() for p in self._noise3()],
                     middle=self.middle, min_value=self.min_value,
                     sq_min_value=self.sq_min_value, degenerate=self.degenerate)
 
@@ -323,7 +337,7 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
         table = torch.as_tensor(np.ascontiguousarray(selection.keep_prob, dtype=np.float64)).to(device)
         sc.keep_table_len = int(table.numel())
         sc.keep_prob = _ptr(table)
-    sc.noise_scale = float(selection.noise_scale)
+    sc.noise = (selection.noise or NO_NOISE).to_c()
     sc.threshold = float(selection.threshold)
     if selection.strategy == N.SELECT_PUBLIC:
         if public_mask is None:
@@ -358,11 +372,11 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
     return index, out, n_kept_dev
 
 
-def add_noise(values, *, noise_kind: int, scale: float, seed: int, index_offset: int = 0,
-              out=None, stream=None):
+def add_noise(values, *, noise: NoiseParams, seed: int, index_offset: int = 0, out=None, stream=None):
     """DPEngine.add_dp_noise's "Add noise" stage (dp_engine.py:595-599) on a
-    device column: returns float64 values + Laplace(b)/Gaussian(sigma) noise
-    drawn from Philox stream (seed, index_offset + i) (`pdp_add_noise`)."""
+    device column: returns the float64 values through the secure mechanism
+    `noise` (Laplace / Gaussian, granularity-snapped), element i drawing from
+    the Philox streams (seed, index_offset + i) (`pdp_add_noise`)."""
     torch = _torch()
     lib = N.lib()
     if not values.is_cuda:
@@ -375,7 +389,8 @@ def add_noise(values, *, noise_kind: int, scale: float, seed: int, index_offset:
         out = torch.empty(n, dtype=torch.float64, device=values.device)
     _check_col(out, "out", (torch.float64,), n, values.device)
     vk = N.VALUE_I64 if values.dtype == torch.int64 else N.VALUE_F64
-    N.check(lib.pdp_add_noise(_ptr(values), vk, n, int(noise_kind), float(scale),
+    c_noise = noise.to_c()
+    N.check(lib.pdp_add_noise(_ptr(values), vk, n, ctypes.byref(c_noise),
                               int(seed) & 0xFFFFFFFFFFFFFFFF, int(index_offset), _ptr(out), _stream(stream)),
             "pdp_add_noise")
     return out

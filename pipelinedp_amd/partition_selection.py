@@ -68,18 +68,19 @@ class TruncatedGeometricPartitionSelection(PartitionSelectionStrategy):
 
 
 class _ThresholdingPartitionSelection(PartitionSelectionStrategy):
+    """PyDP Laplace / GaussianPartitionSelection: keep iff the secure
+    mechanism's AddNoise(n) exceeds the threshold (noise = `noise`, the
+    mechanism with sensitivity l0 / sqrt(l0) and linf 1)."""
     _kernel_strategy = None
     noise_scale = 0.0
     threshold = 0.0
-
-    def _draw(self) -> float:
-        raise NotImplementedError
+    noise: dpc.NoiseParams = dpc.NO_NOISE
 
     def noised_value_if_should_keep(self, n: int) -> Optional[float]:
         m = self._shifted(n)
         if m is None:
             return None
-        v = m + self._draw()
+        v = dpc.secure_sampler().add_noise(self.noise, float(m))
         return v + (n - m) if v > self.threshold else None
 
     def should_keep(self, n: int) -> bool:
@@ -89,7 +90,7 @@ class _ThresholdingPartitionSelection(PartitionSelectionStrategy):
         from pipelinedp_amd.executor import SelectionSpec
         return SelectionSpec(strategy=self._kernel_strategy,
                              max_rows_per_privacy_id=max_rows_per_privacy_id,
-                             pre_threshold=self.pre_threshold or 0, noise_scale=self.noise_scale,
+                             pre_threshold=self.pre_threshold or 0, noise=self.noise,
                              threshold=self.threshold, want_noised_count=True)
 
 
@@ -100,9 +101,7 @@ class LaplacePartitionSelection(_ThresholdingPartitionSelection):
         super().__init__(*args, **kwargs)
         self.noise_scale, self.threshold = dpc.laplace_thresholding_params(
             self.epsilon, self.delta, self.max_partitions_contributed)
-
-    def _draw(self) -> float:
-        return float(np.random.default_rng().laplace(0.0, self.noise_scale))
+        self.noise = dpc.laplace_noise_params(self.epsilon, self.max_partitions_contributed)
 
 
 class GaussianPartitionSelection(_ThresholdingPartitionSelection):
@@ -112,9 +111,7 @@ class GaussianPartitionSelection(_ThresholdingPartitionSelection):
         super().__init__(*args, **kwargs)
         self.noise_scale, self.threshold = dpc.gaussian_thresholding_params(
             self.epsilon, self.delta, self.max_partitions_contributed)
-
-    def _draw(self) -> float:
-        return float(np.random.default_rng().normal(0.0, self.noise_scale))
+        self.noise = dpc.gaussian_noise_params(self.noise_scale)
 
 
 _CLASSES = {

@@ -372,12 +372,15 @@ def test_add_dp_noise_recognised(engine_name, kind):
     acc.compute_budgets()
     plan = CB.recognise(sink)
     assert isinstance(plan, CB.NoisePlan)
-    code, scale = CB.noise_mechanism_of(plan.noise_fn)
+    noise = CB.noise_mechanism_of(plan.noise_fn)
+    code, scale = noise.kind, noise.scale
     if kind == "laplace":
         assert code == N.NOISE_LAPLACE and math.isclose(scale, 3 * 1.5 / 2.0, rel_tol=1e-12)
+        assert noise == dpc.laplace_noise_params(2.0, 3 * 1.5)
     else:
         assert code == N.NOISE_GAUSSIAN
         assert math.isclose(scale, dpc.compute_sigma(2.0, 1e-6, math.sqrt(3) * 1.5), rel_tol=1e-12)
+        assert noise == dpc.gaussian_noise_params(scale)
 
 
 def test_add_dp_noise_validation_like_reference():

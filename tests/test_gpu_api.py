@@ -263,7 +263,8 @@ def test_select_partitions_matches_oracle_with_sampling(device, strategy):
                               rand_shift=__import__("pipelinedp_amd.executor", fromlist=["x"]).bound_plan(
                                   n, U, P, spec).rand_shift)
     keep, _ = O.select(oacc["privacy_id_count"], sel.strategy, keep_prob=sel.keep_prob,
-                       noise_scale=sel.noise_scale, threshold=sel.threshold, seed=seed_select)
+                       noise=None if sel.noise is None else sel.noise.as_dict(), threshold=sel.threshold,
+                       seed=seed_select)
     assert got == np.flatnonzero(keep).tolist()
     assert 0 < len(got) < P
 
@@ -294,10 +295,15 @@ def test_add_dp_noise_matches_oracle_and_distribution(device, kind):
     out = list(sink)
     assert [k for k, _ in out] == keys
     got = np.array([v for _, v in out])
-    code, scale = CB.noise_mechanism_of(CB.recognise(sink).noise_fn)
+    noise = CB.noise_mechanism_of(CB.recognise(sink).noise_fn)
+    scale = noise.scale
     _, _, seed_noise = backend._seeds()
-    want = O.add_noise(vals, code, scale, seed_noise)
-    assert np.allclose(got, want, rtol=1e-12, atol=1e-12 * scale)
+    want = O.add_noise(vals, noise.as_dict(), seed_noise)
+    np.testing.assert_array_equal(got, want)  # grid-valued draws: bit-exact
+    # every output lies on the mechanism's power-of-two grid
+    g = noise.granularity
+    assert g > 0 and math.log2(g).is_integer()
+    assert np.all(np.fmod(got, g) == 0.0)
     dist = laplace(scale=6.0 / 1.0) if kind == "laplace" else norm(scale=dpc.compute_sigma(1.0, 1e-6, math.sqrt(2) * 3.0))
     assert math.isclose(scale, dist.std() / (math.sqrt(2) if kind == "laplace" else 1.0), rel_tol=1e-12)
     assert _ks(got - vals, dist.cdf) > 1e-4
@@ -315,8 +321,8 @@ def test_add_dp_noise_device_columns(device):
     out = list(sink)
     assert [k for k, _ in out] == list(range(n))
     _, _, seed_noise = backend._seeds()
-    want = O.add_noise(np.arange(n) * 3, N.NOISE_LAPLACE, 2.0, seed_noise)
-    assert np.allclose([v for _, v in out], want, rtol=1e-12, atol=1e-11)
+    want = O.add_noise(np.arange(n) * 3, dpc.laplace_noise_params(0.5, 1.0).as_dict(), seed_noise)
+    np.testing.assert_array_equal(np.array([v for _, v in out]), want)
 
 
 def test_add_noise_kernel_sharded_offsets_equal_whole(device):
@@ -324,9 +330,10 @@ def test_add_noise_kernel_sharded_offsets_equal_whole(device):
     import torch
     from pipelinedp_amd import executor as X
     x = torch.randn(10001, dtype=torch.float64, device=device)
-    whole = X.add_noise(x, noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77)
-    a = X.add_noise(x[:4000].clone(), noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77)
-    b = X.add_noise(x[4000:].clone(), noise_kind=N.NOISE_GAUSSIAN, scale=2.5, seed=77, index_offset=4000)
+    nz = dpc.gaussian_noise_params(2.5)
+    whole = X.add_noise(x, noise=nz, seed=77)
+    a = X.add_noise(x[:4000].clone(), noise=nz, seed=77)
+    b = X.add_noise(x[4000:].clone(), noise=nz, seed=77, index_offset=4000)
     assert torch.equal(torch.cat([a, b]), whole)
 
 

@@ -254,17 +254,19 @@ def test_select_and_noise_matches_oracle(device, strategy, pre_threshold):
     table = np.minimum(1.0, 1e-3 * (np.exp(0.3 * np.arange(40)) - 1))
     table[0] = 0.0
     pub = (rng.random(P) < 0.5).astype(np.uint8)
+    from pipelinedp_amd import dp_computations as dpc
+    lap, gau = dpc.laplace_noise_params, dpc.gaussian_noise_params
+    sel_noise = gau(2.5) if strategy == O.SELECT_GAUSSIAN else lap(0.4, 1.0)
     sel = X.SelectionSpec(strategy=strategy, max_rows_per_privacy_id=1, pre_threshold=pre_threshold,
-                          keep_prob=table, noise_scale=2.5, threshold=12.0,
+                          keep_prob=table, noise=sel_noise, threshold=12.0,
                           want_noised_count=True)
     ops = [
-        X.MetricOpSpec(kind=O.OP_COUNT, noise_kind=O.NOISE_LAPLACE, out_col=(0,), scale=(1.5,)),
-        X.MetricOpSpec(kind=O.OP_SUM, noise_kind=O.NOISE_GAUSSIAN, out_col=(1,), scale=(3.0,)),
-        X.MetricOpSpec(kind=O.OP_MEAN, noise_kind=O.NOISE_LAPLACE, out_col=(2, 3, 4), scale=(1.0, 2.0),
+        X.MetricOpSpec(kind=O.OP_COUNT, out_col=(0,), noise=(lap(2.0, 3.0),)),
+        X.MetricOpSpec(kind=O.OP_SUM, out_col=(1,), noise=(gau(3.0),)),
+        X.MetricOpSpec(kind=O.OP_MEAN, out_col=(2, 3, 4), noise=(lap(1.0, 1.0), lap(0.5, 1.0)), middle=5.0),
+        X.MetricOpSpec(kind=O.OP_VARIANCE, out_col=(5, 6, 7, 8), noise=(gau(1.0), gau(2.0), gau(3.0)),
                        middle=5.0),
-        X.MetricOpSpec(kind=O.OP_VARIANCE, noise_kind=O.NOISE_GAUSSIAN, out_col=(5, 6, 7, 8),
-                       scale=(1.0, 2.0, 3.0), middle=5.0),
-        X.MetricOpSpec(kind=O.OP_PRIVACY_ID_COUNT, noise_kind=O.NOISE_GAUSSIAN, out_col=(9,), scale=(0.7,)),
+        X.MetricOpSpec(kind=O.OP_PRIVACY_ID_COUNT, out_col=(9,), noise=(gau(0.7),)),
     ]
     if strategy in (O.SELECT_LAPLACE, O.SELECT_GAUSSIAN):
         ops.append(X.MetricOpSpec(kind=O.OP_THRESHOLDED_PID, out_col=(10,)))
@@ -273,15 +275,16 @@ def test_select_and_noise_matches_oracle(device, strategy, pre_threshold):
                                             seed_noise=4242, partition_offset=1000,
                                             public_mask=torch.as_tensor(pub).to(device))
     keep, noised = O.select(rc, strategy, max_rows_per_privacy_id=1, pre_threshold=pre_threshold,
-                            keep_prob=table, noise_scale=2.5, threshold=12.0, public_mask=pub, seed=42,
+                            keep_prob=table, noise=sel_noise.as_dict(), threshold=12.0, public_mask=pub, seed=42,
                             partition_offset=1000)
     want_index = np.flatnonzero(keep)
     np.testing.assert_array_equal(index.cpu().numpy(), want_index)
     want = O.noise_metrics([o.as_dict() for o in ops], want_index, acc_np, False, noised, 4242,
                            partition_offset=1000, n_cols=n_cols)
     got = out.cpu().numpy()[:, :n_kept]
-    # transcendental noise: device libm vs numpy differ by a few ulp
-    np.testing.assert_allclose(got, want, rtol=1e-9, atol=1e-9)
+    # the secure samplers' draws are grid integers (bit-exact); the metrics
+    # built from them (mean, variance) divide in fp64 the same way
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
 
 
 def test_single_hip_runtime_loaded(device):
