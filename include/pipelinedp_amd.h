@@ -92,6 +92,11 @@ typedef struct pdp_bound_config {
 #define PDP_KEYS_WIDE 1    /* u64 pair key + u32 row: 12 B per row and pass */
 #define PDP_KEYS_COMPACT 2 /* u32 (bucket-local pid, partition) + u32 row: 8 B per row and pass;
                               needs super/bucket/partition bits <= 31 (AUTO picks it then) */
+#define PDP_KEYS_PACKED 3  /* level 1: one u64 (row within its 65,536-row tile | bucket-local pid |
+                              partition), the tile recovered from the record's position; level 2
+                              on: the COMPACT pair.  8 B per row and pass where COMPACT does not
+                              fit: needs bucket + partition bits <= 31 and super + bucket +
+                              partition bits <= 47 (AUTO's second choice) */
 
 /* per-partition merge of the kept pairs (BUCKETED; identical sums up to fp
  * summation order) */

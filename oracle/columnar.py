@@ -283,12 +283,16 @@ def derive_pid_row_seed(seed):
 def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, value_kind,
                      flags, min_value=0.0, max_value=0.0, middle=0.0, min_sum=0.0,
                      max_sum=0.0, seed=0, row_offset=0, allowed=None, priorities="hash",
-                     rng=None, rand_shift=None, max_contributions=0, rows_are_units=False):
+                     rng=None, rand_shift=None, max_contributions=0, rows_are_units=False,
+                     row_index=None):
     """Returns dense per-partition accumulators (dict of numpy arrays, length P).
 
     l0 = 0: no cross-partition sampling (every pair kept).  max_contributions:
     per pid keep the rows of the max_contributions smallest row priorities
-    first.  rows_are_units: every row is its own pair (pid is ignored)."""
+    first.  rows_are_units: every row is its own pair (pid is ignored).
+    row_index: the rows' indices in the kernels' input (default 0..n-1), for
+    a privacy-id subset of a larger input (oracle/parallel_oracle.py); the
+    value column is then the whole input's, indexed by row_index."""
     pk = np.asarray(pk, dtype=np.int64)
     if rows_are_units:  # one privacy unit per row: the row index is the pid
         pid = np.arange(len(pk), dtype=np.int64)
@@ -303,7 +307,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids, n_partitions, l0, linf, v
         "normalized_sum": np.zeros(P, np.float64),
         "normalized_sum_sq": np.zeros(P, np.float64),
     }
-    local = np.arange(n, dtype=np.int64)
+    local = np.arange(n, dtype=np.int64) if row_index is None else np.asarray(row_index, dtype=np.int64)
     valid = (pid >= 0) & (pid < n_privacy_ids) & (pk >= 0) & (pk < P)
     if allowed is not None:
         valid &= np.asarray(allowed, dtype=bool)[np.clip(pk, 0, P - 1)]

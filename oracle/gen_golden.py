@@ -227,6 +227,54 @@ def select_partitions_fixture(pdp, seed=300):
             "eps": 1e4, "delta": 1e-12, "expected_keys": keys}
 
 
+def post_threshold_fixture(pdp, noise_kind, eps, seed=400):
+    """DPEngine.aggregate(COUNT, PRIVACY_ID_COUNT, post_aggregation_thresholding
+    = True) on LocalBackend, real noise path (no patching): the
+    PostAggregationThresholdingCombiner (combiners.py:328-382) replaces the
+    PRIVACY_ID_COUNT combiner and DPEngine drops partitions whose thresholded
+    value is None (dp_engine.py:184-185, 544-549).  A huge eps (1e4 Laplace,
+    1300 Gaussian: the stand-in's calibration needs eps < 700 per mechanism)
+    and delta = 1e-10 make the outcome deterministic up to O(e^-20):
+    partitions with >= 2 privacy ids are kept, those with 1 dropped, and every
+    released value is within 1 of its exact count (12 sigma)."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for u in range(300):
+        for k in rng.choice(80, size=int(rng.integers(1, 3)), replace=False):
+            rows.extend([[u, int(k), 1]] * int(rng.integers(1, 3)))
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.PRIVACY_ID_COUNT],
+                                 noise_kind=getattr(pdp.NoiseKind, noise_kind), max_partitions_contributed=2,
+                                 max_contributions_per_partition=2, post_aggregation_thresholding=True)
+    accountant = pdp.NaiveBudgetAccountant(total_epsilon=eps, total_delta=1e-10)
+    engine = pdp.DPEngine(accountant, pdp.LocalBackend())
+    ext = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                             value_extractor=lambda r: r[2])
+    out = engine.aggregate(rows, params, ext)
+    accountant.compute_budgets()
+    got = sorted([int(pk), m._asdict()] for pk, m in out)
+    pids, cnt = {}, {}
+    for u, k, _ in rows:
+        pids.setdefault(k, set()).add(u)
+        cnt[k] = cnt.get(k, 0) + 1
+    assert [k for k, _ in got] == sorted(k for k, s in pids.items() if len(s) >= 2)
+    for k, m in got:
+        assert abs(m["privacy_id_count"] - len(pids[k])) < 1.0 and abs(m["count"] - cnt[k]) < 1.0
+    budgets = [[m.mechanism_spec.mechanism_type.value, m.mechanism_spec.eps, m.mechanism_spec.delta]
+               for m in accountant._mechanisms]
+    return {"name": f"post_aggregation_thresholding_{noise_kind.lower()}", "rows": rows, "eps": eps,
+            "delta": 1e-10, "noise_kind": noise_kind, "l0": 2, "linf": 2,
+            "field_order": list(got[0][1]) if got else [], "expected": got, "budgets": budgets}
+
+
+def main_post_threshold():
+    pdp = _import_reference()
+    for kind, eps in (("LAPLACE", 1e4), ("GAUSSIAN", 1300.0)):
+        fx = post_threshold_fixture(pdp, kind, eps)
+        with open(os.path.join(OUT, f"{fx['name']}.json"), "w") as f:
+            json.dump(fx, f)
+        print(fx["name"], len(fx["rows"]), "rows", len(fx["expected"]), "partitions", fx["field_order"])
+
+
 def main():
     pdp = _import_reference()
     os.makedirs(OUT, exist_ok=True)
@@ -241,7 +289,11 @@ def main():
     with open(os.path.join(OUT, "sampling_inclusion.json"), "w") as f:
         json.dump(sampling_fixture(pdp), f)
     print("sampling_inclusion written")
+    main_post_threshold()
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "post_threshold":
+        main_post_threshold()  # only the post-aggregation-thresholding fixtures
+    else:
+        main()

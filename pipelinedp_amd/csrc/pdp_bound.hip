@@ -37,7 +37,10 @@ namespace pdp {
 namespace {
 
 constexpr int kPartThreads = 512;
-constexpr int64_t kTileRows = 65536;
+constexpr int kStageItems = 8;
+constexpr int kStageRows = kPartThreads * kStageItems;  // 4096 rows per LDS stage / level-2 window
+constexpr int kTileRowBits = 16;
+constexpr int64_t kTileRows = (int64_t)1 << kTileRowBits;
 constexpr int kUnroll = 8;
 #ifndef PDP_BUCKET_THREADS
 #define PDP_BUCKET_THREADS 1024
@@ -160,16 +163,27 @@ Plan make_plan(const pdp_bound_config* c) {
     p.lds_bytes += (2 * (int64_t)p.n_ranges + kBucketThreads / 64 + 1) * 4;
   }
   // row records of the partition passes: u32 (sub-bucket, local pid,
-  // partition) with bit 31 = dead when those fields fit, else the u64 pair key
+  // partition) with bit 31 = dead when those fields fit (COMPACT); else the
+  // level-1 u64 packed record with a tile-relative row, then COMPACT pairs
+  // (PACKED); else the u64 pair key + u32 row (WIDE)
   const bool compact_ok = p.super_bits + p.bucket_bits + p.pk_bits <= 31;
+  const bool packed_ok = p.bucket_bits + p.pk_bits <= 31 &&
+                         p.super_bits + p.bucket_bits + p.pk_bits <= 64 - 1 - kTileRowBits;
   p.key_format = 0;
   if (p.algorithm == PDP_ALGO_BUCKETED) {
-    if (c->key_format == PDP_KEYS_COMPACT && !compact_ok) p.algorithm = -1;  // infeasible
-    p.key_format = (c->key_format == PDP_KEYS_WIDE || !compact_ok) ? PDP_KEYS_WIDE : PDP_KEYS_COMPACT;
+    const int want = c->key_format;
+    if ((want == PDP_KEYS_COMPACT && !compact_ok) || (want == PDP_KEYS_PACKED && !packed_ok))
+      p.algorithm = -1;  // infeasible
+    else if (want != PDP_KEYS_AUTO)
+      p.key_format = want;
+    else
+      p.key_format = compact_ok ? PDP_KEYS_COMPACT : (packed_ok ? PDP_KEYS_PACKED : PDP_KEYS_WIDE);
+    // one super-bucket (no level 2): PACKED degenerates to COMPACT, which then fits
+    if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
   }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave [+ pid hashes]
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
-    if (p.key_format == PDP_KEYS_COMPACT) p.lds_bytes += ((int64_t)4 << p.bucket_bits);
+    if (p.key_format != PDP_KEYS_WIDE) p.lds_bytes += ((int64_t)4 << p.bucket_bits);
   }
   if (p.merge == PDP_MERGE_RANGES) {
     int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
@@ -193,6 +207,7 @@ struct Ws {
   uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
   // bucketed path
   uint64_t counts_tm, counts, chunk_sums, cursor, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
+  uint64_t win_tile;  // PDP_KEYS_PACKED: first tile of every level-2 window
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t total;
@@ -225,15 +240,21 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
     w.super_tm = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
     w.super_off = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
-    const uint64_t kb = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;
-    w.keys1 = off; off = align256(off + n * kb);
-    w.rows1 = off; off = align256(off + n * 4);
+    const bool packed = p.key_format == PDP_KEYS_PACKED && p.super_bits > 0;
+    const uint64_t kb1 = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;  // level-1 key
+    const uint64_t kb2 = p.key_format == PDP_KEYS_WIDE ? 8 : 4;     // level-2 key
+    w.keys1 = off; off = align256(off + n * (packed ? 8 : kb1));
+    if (!packed) { w.rows1 = off; off = align256(off + n * 4); }
     if (p.super_bits > 0) {
-      w.keys2 = off; off = align256(off + n * kb);
+      w.keys2 = off; off = align256(off + n * kb2);
       w.rows2 = off; off = align256(off + n * 4);
     } else {
       w.keys2 = w.keys1;
       w.rows2 = w.rows1;
+    }
+    if (packed) {
+      const uint64_t n_win = (n + 4 * (uint64_t)p.n_supers) / kStageRows + 2 * (uint64_t)p.n_supers + 1;
+      w.win_tile = off; off = align256(off + n_win * 4);
     }
     if (p.merge == PDP_MERGE_RANGES) {
       const uint64_t recs = (uint64_t)p.n_buckets * ((uint64_t)c->l0 << p.bucket_bits);
@@ -268,7 +289,7 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad algorithm");
   if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
     return set_error(PDP_E_INVALID, "bad merge");
-  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_COMPACT)
+  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED)
     return set_error(PDP_E_INVALID, "bad key_format");
   if (pairs_mode(c)) return pairs_validate(c);
   if (c->algorithm == PDP_ALGO_PAIR_TABLE)
@@ -482,32 +503,37 @@ __global__ void __launch_bounds__(kBlock) k_init_cursors(KP kp, const unsigned* 
 // LDS-staged multi-destination write: the rows of one sub-chunk (ITEMS per
 // thread) are counting-sorted by destination in LDS and each destination's
 // run is then written contiguously at gcur[dest] (coalesced, long runs).
-constexpr int kStageItems = 8;
-constexpr int kStageRows = kPartThreads * kStageItems;  // 4096
 constexpr int kMaxDest = 1024;
 
 // row record key of the partition passes: u64 pair key (PDP_KEYS_WIDE) or u32
-// compact record (PDP_KEYS_COMPACT)
+// compact record (PDP_KEYS_COMPACT, and PDP_KEYS_PACKED from level 2 on)
 template <bool COMPACT>
 using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>::type;
+// level-1 record key per format (PACKED: the u64 packed record, no row array)
+template <int FMT>
+using L1Key = typename std::conditional<FMT == PDP_KEYS_COMPACT, uint32_t, unsigned long long>::type;
+// level-2 (bucket-order) record key per format
+template <int FMT>
+using L2Key = RecKey<FMT != PDP_KEYS_WIDE>;
 
 // MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
-// fits four workgroups per CU with compact keys instead of three
-template <typename K, int MAXD = kMaxDest>
+// fits four workgroups per CU with compact keys instead of three.  ROWS:
+// the stage carries a u32 row array beside the keys.
+template <typename K, int MAXD = kMaxDest, bool ROWS = true>
 struct StageLds {
   using D = typename std::conditional<(MAXD <= 256), uint8_t, unsigned short>::type;
   unsigned hist[MAXD];
   unsigned start[MAXD];
   unsigned gcur[MAXD];
   K keys[kStageRows];
-  unsigned rows[kStageRows];
+  unsigned rows[ROWS ? kStageRows : 1];
   D dest[kStageRows];
 };
 constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four workgroups per CU
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
-template <typename K, int MAXD>
-__device__ __forceinline__ void stage_count(StageLds<K, MAXD>& s, int ndest, const int (&d)[kStageItems],
+template <typename K, int MAXD, bool ROWS>
+__device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS>& s, int ndest, const int (&d)[kStageItems],
                                             unsigned (&rank)[kStageItems]) {
   for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
   __syncthreads();
@@ -532,8 +558,8 @@ __device__ __forceinline__ void stage_count(StageLds<K, MAXD>& s, int ndest, con
 }
 
 // phase 2: place into the LDS stage, then write every run at gcur[dest]
-template <typename K, int MAXD>
-__device__ __forceinline__ void stage_write(StageLds<K, MAXD>& s, int ndest, const int (&d)[kStageItems],
+template <typename K, int MAXD, bool ROWS>
+__device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS>& s, int ndest, const int (&d)[kStageItems],
                                             const unsigned (&rank)[kStageItems], const K (&x)[kStageItems],
                                             const unsigned (&r)[kStageItems], K* __restrict__ out_keys,
                                             unsigned* __restrict__ out_rows) {
@@ -542,8 +568,8 @@ __device__ __forceinline__ void stage_write(StageLds<K, MAXD>& s, int ndest, con
     if (d[q] < 0) continue;
     const unsigned slot = s.start[d[q]] + rank[q];
     s.keys[slot] = x[q];
-    s.rows[slot] = r[q];
-    s.dest[slot] = (typename StageLds<K, MAXD>::D)d[q];
+    if (ROWS) s.rows[slot] = r[q];
+    s.dest[slot] = (typename StageLds<K, MAXD, ROWS>::D)d[q];
   }
   __syncthreads();
   const unsigned total = s.start[ndest - 1] + s.hist[ndest - 1];
@@ -551,7 +577,7 @@ __device__ __forceinline__ void stage_write(StageLds<K, MAXD>& s, int ndest, con
     const unsigned dd = s.dest[k];
     const unsigned g = s.gcur[dd] + (k - s.start[dd]);
     out_keys[g] = s.keys[k];
-    out_rows[g] = s.rows[k];
+    if (ROWS) out_rows[g] = s.rows[k];
   }
   __syncthreads();
 }
@@ -562,6 +588,18 @@ __device__ __forceinline__ void stage_write(StageLds<K, MAXD>& s, int ndest, con
 __device__ __forceinline__ uint32_t compact_key(const KP& kp, int64_t u, int64_t k, bool dead) {
   const uint32_t mid = (uint32_t)((uint64_t)u & ((1ULL << (kp.bucket_bits + kp.super_bits)) - 1));
   return dead ? (0x80000000u | (mid << kp.pk_bits)) : ((mid << kp.pk_bits) | (uint32_t)k);
+}
+
+// Packed level-1 record (PDP_KEYS_PACKED): bit 63 = dead, bits [47, 63) = the
+// row's index within its 65,536-row tile, [pk_bits, pk_bits + bucket_bits +
+// super_bits) = bucket-within-super and bucket-local pid, [0, pk_bits) = pk.
+// The tile is not stored: level 2 recovers it from the record's position in
+// its super-bucket region (the tiles' runs there are in tile order).
+constexpr int kPackedRowShift = 63 - kTileRowBits;
+__device__ __forceinline__ uint64_t packed_key(const KP& kp, int64_t u, int64_t k, uint32_t tile_row, bool dead) {
+  const uint64_t mid = (uint64_t)u & ((1ULL << (kp.bucket_bits + kp.super_bits)) - 1);
+  return (dead ? (1ULL << 63) : 0ULL) | ((uint64_t)tile_row << kPackedRowShift) | (mid << kp.pk_bits) |
+         (dead ? 0ULL : (uint64_t)k);
 }
 
 // The pair key of a compact record: bit-identical to the key k_scatter_l1
@@ -575,18 +613,19 @@ __device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpi
 }
 
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
-template <bool COMPACT>
+template <int FMT>
 __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
                                                              const uint8_t* __restrict__ allowed,
                                                              const unsigned* __restrict__ super_off,
                                                              const unsigned* __restrict__ super_base,
-                                                             RecKey<COMPACT>* __restrict__ keys1,
+                                                             L1Key<FMT>* __restrict__ keys1,
                                                              unsigned* __restrict__ rows1, unsigned* err) {
-  using K = RecKey<COMPACT>;
+  using K = L1Key<FMT>;
+  constexpr bool ROWS = FMT != PDP_KEYS_PACKED;
   extern __shared__ unsigned long long stage_raw[];
   static_assert(kMaxSupers <= kSmallDest, "level-1 destinations must fit the small stage");
-  StageLds<K, kSmallDest>& s = *reinterpret_cast<StageLds<K, kSmallDest>*>(stage_raw);
+  StageLds<K, kSmallDest, ROWS>& s = *reinterpret_cast<StageLds<K, kSmallDest, ROWS>*>(stage_raw);
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
   // this tile's first row in each super-bucket region (k_super_scan)
@@ -639,8 +678,10 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
       } else if (allowed != nullptr && allowed[k[q]] == 0) {
         is_dead = true;
       }
-      if (COMPACT) {
+      if constexpr (FMT == PDP_KEYS_COMPACT) {
         x[q] = (K)compact_key(kp, u[q], k[q], is_dead);
+      } else if constexpr (FMT == PDP_KEYS_PACKED) {
+        x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(r[q] - (unsigned)t0), is_dead);
       } else {
         const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
         x[q] = (K)(is_dead ? (dead | midv) : pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift));
@@ -649,15 +690,6 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
 #if PDP_L1_PREFETCH
     // next sub-chunk's column loads go out before this one's LDS passes
     if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
-#endif
-#ifdef PDP_ABL_L1_NOSTAGE
-    {
-      unsigned acc = 0;
-#pragma unroll
-      for (int q = 0; q < kStageItems; ++q) acc += (unsigned)d[q] ^ (unsigned)x[q] ^ r[q];
-      if (acc == 0x9E3779B9u) rows1[threadIdx.x] = acc;  // keeps the work live
-      continue;
-    }
 #endif
     unsigned rank[kStageItems];
     stage_count(s, nd, d, rank);
@@ -670,31 +702,52 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   }
 }
 
-// Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
-template <bool COMPACT, int MAXD>
-__global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
-                                                             unsigned* __restrict__ cursor,
-                                                             const RecKey<COMPACT>* __restrict__ keys1,
-                                                             const unsigned* __restrict__ rows1,
-                                                             RecKey<COMPACT>* __restrict__ keys2,
-                                                             unsigned* __restrict__ rows2) {
-#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
-  return;  // ablation: only the level-1 pass is meaningful
-#endif
-  using K = RecKey<COMPACT>;
-  constexpr int R = 16 / sizeof(K);  // records per 16-byte key load
-  extern __shared__ unsigned long long stage_raw[];
-  StageLds<K, MAXD>& s = *reinterpret_cast<StageLds<K, MAXD>*>(stage_raw);
-  __shared__ int64_t s_first, s_base, s_r0, s_r1;
-  const int nsub = 1 << kp.super_bits;
+// Level-2 windows: every super-bucket region is cut into 4096-record windows
+// aligned at its first R-aligned record; window g's (super-bucket, base,
+// valid range [r0, r1)).  The first wave locates it (n_supers <= 64).
+template <int R>
+__device__ __forceinline__ bool locate_window(const KP& kp, const unsigned* __restrict__ super_base, int64_t g,
+                                              int* s_B, int64_t* s_base, int64_t* s_r0, int64_t* s_r1) {
+  const int lane = threadIdx.x;
+  int64_t lo = 0, hi = 0, nch = 0;
+  if (lane < kp.n_supers) {
+    lo = super_base[lane];
+    hi = super_base[lane + 1];
+    nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kStageRows - 1) / kStageRows : 0;
+  }
+  int64_t inc = nch;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  const bool mine = g >= inc - nch && g < inc;
+  const unsigned long long hit = __ballot(mine);
+  if (mine) {
+    const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kStageRows;
+    *s_B = lane;
+    *s_base = base;
+    *s_r0 = base > lo ? base : lo;
+    *s_r1 = base + kStageRows < hi ? base + kStageRows : hi;
+  }
+  return hit != 0;
+}
+
+// PDP_KEYS_PACKED: the tile holding the first record of every level-2 window.
+// One workgroup per super-bucket B walks the tiles' runs [super_off[t][B],
+// super_off[t + 1][B]) of its region; a window starting inside a run belongs
+// to that run's tile.  Windows are enumerated exactly as k_scatter_l2 does.
+__global__ void __launch_bounds__(kBlock) k_window_tiles(KP kp, const unsigned* __restrict__ super_base,
+                                                         const unsigned* __restrict__ super_off,
+                                                         unsigned* __restrict__ win_tile) {
+  constexpr int R = 2;  // u64 packed records per 16-byte load
+  __shared__ int64_t s_g0;
+  const int B = blockIdx.x;
   if (threadIdx.x < 64) {
-    // locate this workgroup's (super-bucket, chunk): chunks of a super-bucket
-    // are 4096-row windows aligned at its first R-aligned row (n_supers <= 64)
     const int lane = threadIdx.x;
-    int64_t lo = 0, hi = 0, nch = 0;
+    int64_t nch = 0;
     if (lane < kp.n_supers) {
-      lo = super_base[lane];
-      hi = super_base[lane + 1];
+      const int64_t lo = super_base[lane], hi = super_base[lane + 1];
       nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kStageRows - 1) / kStageRows : 0;
     }
     int64_t inc = nch;
@@ -703,31 +756,122 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
       const int64_t y = __shfl_up(inc, off, 64);
       if (lane >= off) inc += y;
     }
-    const int64_t g = blockIdx.x;
-    const bool mine = g >= inc - nch && g < inc;
-    const unsigned long long hit = __ballot(mine);
-    if (lane == 0 && hit == 0) s_first = -1;  // grid is an upper bound on the chunk count
-    if (mine) {
-      const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kStageRows;
-      s_first = (int64_t)lane << kp.super_bits;
-      s_base = base;
-      s_r0 = base > lo ? base : lo;
-      s_r1 = base + kStageRows < hi ? base + kStageRows : hi;
-    }
+    if (lane == B) s_g0 = inc - nch;
   }
   __syncthreads();
-  if (s_first < 0) return;
+  const int64_t lo = super_base[B], hi = super_base[B + 1];
+  if (hi <= lo) return;
+  const int64_t rel0 = (lo & ~(int64_t)(R - 1)) - lo;  // window 0's base, relative (<= 0)
+  const int64_t total = hi - lo;
+  for (int64_t t = threadIdx.x; t < kp.n_tiles; t += blockDim.x) {
+    const int64_t a = super_off[t * kp.n_supers + B];
+    const int64_t b = t + 1 < kp.n_tiles ? (int64_t)super_off[(t + 1) * kp.n_supers + B] : total;
+    if (a >= b) continue;
+    int64_t k = a == 0 ? 0 : (a - rel0 + kStageRows - 1) / kStageRows;
+    for (;; ++k) {
+      int64_t st = rel0 + k * kStageRows;
+      if (st < 0) st = 0;
+      if (st >= b) break;
+      if (st >= a) win_tile[s_g0 + k] = (unsigned)t;
+    }
+  }
+}
+
+// Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
+// PACKED input: the u64 packed records are unpacked into COMPACT (key, row)
+// pairs, the row = tile * 65,536 + tile row with the tile found from the
+// record's offset among the tiles' runs (LDS copy of super_off from the
+// window's first tile, k_window_tiles).
+constexpr int kWinTiles = 256;  // tiles' run starts held in LDS per window
+template <int FMT, int MAXD>
+__global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
+                                                             const unsigned* __restrict__ super_off,
+                                                             const unsigned* __restrict__ win_tile,
+                                                             unsigned* __restrict__ cursor,
+                                                             const L1Key<FMT>* __restrict__ keys1,
+                                                             const unsigned* __restrict__ rows1,
+                                                             L2Key<FMT>* __restrict__ keys2,
+                                                             unsigned* __restrict__ rows2) {
+#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
+  return;  // ablation: only the level-1 pass is meaningful
+#endif
+  using KI = L1Key<FMT>;
+  using KO = L2Key<FMT>;
+  constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
+  constexpr int R = 16 / sizeof(KI);  // records per 16-byte key load
+  extern __shared__ unsigned long long stage_raw[];
+  StageLds<KO, MAXD>& s = *reinterpret_cast<StageLds<KO, MAXD>*>(stage_raw);
+  __shared__ int s_B;
+  __shared__ int64_t s_base, s_r0, s_r1;
+  __shared__ unsigned toff[kWinTiles + 1];  // PACKED: run starts of tiles T0 .. T0 + J
+  __shared__ int s_J;
+  const int nsub = 1 << kp.super_bits;
+  if (threadIdx.x < 64) {
+    const bool found = locate_window<R>(kp, super_base, blockIdx.x, &s_B, &s_base, &s_r0, &s_r1);
+    if (threadIdx.x == 0 && !found) s_B = -1;  // grid is an upper bound on the window count
+  }
+  __syncthreads();
+  if (s_B < 0) return;
   const int64_t base = s_base, r0 = s_r0, r1 = s_r1;
+  const int64_t s_first = (int64_t)s_B << kp.super_bits;
+  const int64_t lo = PACKED ? (int64_t)super_base[s_B] : 0;
+  int64_t T0 = 0;
+  if constexpr (PACKED) {
+    T0 = win_tile[blockIdx.x];
+    int64_t J = kp.n_tiles - T0;
+    if (J > kWinTiles) J = kWinTiles;
+    const int64_t total = (int64_t)super_base[s_B + 1] - lo;
+    for (int64_t j = threadIdx.x; j <= J; j += blockDim.x) {
+      const int64_t t = T0 + j;
+      toff[j] = t < kp.n_tiles ? super_off[t * kp.n_supers + s_B] : (unsigned)total;
+    }
+    if (threadIdx.x == 0) s_J = (int)J;
+    __syncthreads();
+  }
+  // tile of the record at relative offset o: the last run start <= o
+  auto tile_of = [&](int64_t o) -> int64_t {
+    const int J = s_J;
+    if (o < (int64_t)toff[J]) {
+      int a = 0, b = J - 1;
+      while (a < b) {
+        const int m = (a + b + 1) >> 1;
+        if ((int64_t)toff[m] <= o) a = m;
+        else b = m - 1;
+      }
+      return T0 + a;
+    }
+    int64_t a = T0 + J, b = kp.n_tiles - 1;  // beyond the LDS span (sparse region): global search
+    while (a < b) {
+      const int64_t m = (a + b + 1) >> 1;
+      if ((int64_t)super_off[m * kp.n_supers + s_B] <= o) a = m;
+      else b = m - 1;
+    }
+    return a;
+  };
+  const int bb = kp.bucket_bits;
+  const uint32_t local_mask = (1u << bb) - 1;
+  auto unpack = [&](uint64_t v, int64_t i, KO* key, unsigned* row, int* dest) {
+    const uint32_t mid = (uint32_t)((v >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
+    *dest = (int)(mid >> bb);
+    const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
+    *key = (KO)((v >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(v & kp.pk_mask)));
+    const uint32_t trow = (uint32_t)((v >> kPackedRowShift) & (kTileRows - 1));
+    *row = (unsigned)(tile_of(i - lo) * kTileRows + trow);
+  };
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
-  K x[kStageItems];
+  KO x[kStageItems];
   unsigned r[kStageItems];
   int d[kStageItems];
 #pragma unroll
   for (int q = 0; q < kStageItems; q += R) {  // R records per 16-byte key load
     const int64_t i = base + R * ((int64_t)threadIdx.x + (int64_t)(q / R) * blockDim.x);
     if (i >= r0 && i + R - 1 < r1) {
-      if constexpr (COMPACT) {
+      if constexpr (PACKED) {
+        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
+        unpack(a.x, i, &x[q], &r[q], &d[q]);
+        unpack(a.y, i + 1, &x[q + 1], &r[q + 1], &d[q + 1]);
+      } else if constexpr (R == 4) {
         const uint4 a = *reinterpret_cast<const uint4*>(keys1 + i);
         const uint4 c = *reinterpret_cast<const uint4*>(rows1 + i);
         x[q] = a.x; x[q + 1] = a.y; x[q + 2] = a.z; x[q + 3] = a.w;
@@ -738,15 +882,22 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
         x[q] = a.x; x[q + 1] = a.y;
         r[q] = c.x; r[q + 1] = c.y;
       }
+      if constexpr (!PACKED) {
 #pragma unroll
-      for (int e = 0; e < R; ++e) d[q + e] = (int)((x[q + e] >> sub_shift) & sub_mask);
+        for (int e = 0; e < R; ++e) d[q + e] = (int)((x[q + e] >> sub_shift) & sub_mask);
+      }
     } else {
 #pragma unroll
       for (int e = 0; e < R; ++e) {
         const bool ok = i + e >= r0 && i + e < r1;
-        x[q + e] = ok ? keys1[i + e] : 0;
-        r[q + e] = ok ? rows1[i + e] : 0;
-        d[q + e] = ok ? (int)((x[q + e] >> sub_shift) & sub_mask) : -1;
+        if constexpr (PACKED) {
+          if (ok) unpack(keys1[i + e], i + e, &x[q + e], &r[q + e], &d[q + e]);
+          else { x[q + e] = 0; r[q + e] = 0; d[q + e] = -1; }
+        } else {
+          x[q + e] = ok ? keys1[i + e] : 0;
+          r[q + e] = ok ? rows1[i + e] : 0;
+          d[q + e] = ok ? (int)((x[q + e] >> sub_shift) & sub_mask) : -1;
+        }
       }
     }
   }
@@ -1417,7 +1568,7 @@ template <int VK, bool KA>
 int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w, const void* value,
                   const pdp_partition_accumulators& acc) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
-  const bool compact = p.key_format == PDP_KEYS_COMPACT;
+  const bool compact = p.key_format != PDP_KEYS_WIDE;  // PACKED: COMPACT records from level 2 on
   const void* kern = compact ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, true>
                                        : (const void*)k_bucket_bound<VK, KA, false, true>)
                              : (ranges ? (const void*)k_bucket_bound<VK, KA, true, false>
@@ -1451,35 +1602,49 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
   return PDP_OK;
 }
 
-template <bool COMPACT>
+template <int FMT>
 int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
                    const uint8_t* allowed, const unsigned* super_off, const unsigned* super_base, unsigned* cursor,
                    char* ws, const Ws& w, unsigned* err) {
-  using K = RecKey<COMPACT>;
-  const size_t lds = sizeof(StageLds<K, kSmallDest>);
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<COMPACT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  using K1 = L1Key<FMT>;
+  using K2 = L2Key<FMT>;
+  constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
+  const size_t lds = sizeof(StageLds<K1, kSmallDest, ROWS1>);
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
   PDP_PROF_BEGIN("k_scatter_l1", st);
-  hipLaunchKernelGGL(k_scatter_l1<COMPACT>, dim3((unsigned)p.n_tiles), dim3(kPartThreads), lds, st, kp, pid, pk,
-                     allowed, super_off, super_base, (K*)(ws + w.keys1), (unsigned*)(ws + w.rows1), err);
+  hipLaunchKernelGGL(k_scatter_l1<FMT>, dim3((unsigned)p.n_tiles), dim3(kPartThreads), lds, st, kp, pid, pk,
+                     allowed, super_off, super_base, (K1*)(ws + w.keys1), ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr,
+                     err);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
-    // chunks: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
+    // windows: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
     const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kStageRows + 2 * p.n_supers + 1;
+    unsigned* win_tile = nullptr;
+    if (FMT == PDP_KEYS_PACKED) {
+      win_tile = (unsigned*)(ws + w.win_tile);
+      PDP_PROF_BEGIN("k_window_tiles", st);
+      hipLaunchKernelGGL(k_window_tiles, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_base, super_off,
+                         win_tile);
+      PDP_PROF_END(st);
+      PDP_HIP_CHECK(hipGetLastError());
+    }
     const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
-    const void* l2 = small ? (const void*)k_scatter_l2<COMPACT, kSmallDest> : (const void*)k_scatter_l2<COMPACT, kMaxDest>;
-    const size_t lds2 = small ? sizeof(StageLds<K, kSmallDest>) : sizeof(StageLds<K, kMaxDest>);
+    const void* l2 = small ? (const void*)k_scatter_l2<FMT, kSmallDest> : (const void*)k_scatter_l2<FMT, kMaxDest>;
+    const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest>) : sizeof(StageLds<K2, kMaxDest>);
     PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     PDP_PROF_BEGIN("k_scatter_l2", st);
     if (small)
-      hipLaunchKernelGGL((k_scatter_l2<COMPACT, kSmallDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
-                         super_base, cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
-                         (K*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+      hipLaunchKernelGGL((k_scatter_l2<FMT, kSmallDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
+                         super_base, super_off, win_tile, cursor, (const K1*)(ws + w.keys1),
+                         ROWS1 ? (const unsigned*)(ws + w.rows1) : nullptr, (K2*)(ws + w.keys2),
+                         (unsigned*)(ws + w.rows2));
     else
-      hipLaunchKernelGGL((k_scatter_l2<COMPACT, kMaxDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
-                         super_base, cursor, (const K*)(ws + w.keys1), (const unsigned*)(ws + w.rows1),
-                         (K*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+      hipLaunchKernelGGL((k_scatter_l2<FMT, kMaxDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
+                         super_base, super_off, win_tile, cursor, (const K1*)(ws + w.keys1),
+                         ROWS1 ? (const unsigned*)(ws + w.rows1) : nullptr, (K2*)(ws + w.keys2),
+                         (unsigned*)(ws + w.rows2));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -1640,10 +1805,13 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.key_format == PDP_KEYS_COMPACT)
-    return launch_scatter<true>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor, ws,
-                                w, err);
-  return launch_scatter<false>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor, ws,
-                               w, err);
+    return launch_scatter<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                            cursor, ws, w, err);
+  if (p.key_format == PDP_KEYS_PACKED)
+    return launch_scatter<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                           cursor, ws, w, err);
+  return launch_scatter<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor,
+                                       ws, w, err);
 }
 
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,

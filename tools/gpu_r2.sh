@@ -10,7 +10,8 @@ TAG=${1:-r2}
 shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "$@" > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; echo "PYTEST FAILED"; exit 1; }
+TESTS=${@:-tests}
+timeout -k 10 1100 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; echo "PYTEST FAILED"; exit 1; }
 tail -3 $OUT/pytest_gpu.log
 if [ -n "${NO_BENCH:-}" ]; then exit 0; fi
 timeout -k 10 400 python -u bench.py > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; echo "BENCH FAILED"; exit 1; }
