@@ -423,11 +423,22 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
       device: torch device (default cuda:current).
       seed: fixes the sampling / selection / noise streams (testing only —
         a DP release must use fresh randomness, the default).
+      privacy_id_sharding: under torch.distributed, how the rows of one
+        privacy id are kept on one rank (contribution bounding is per privacy
+        id over the whole dataset, contribution_bounders.py:62-111):
+        "verify" (default) checks that no privacy id is on two ranks and
+        raises ValueError otherwise; "shuffle" moves every row to the rank
+        that owns its privacy id (one all-to-all of the rows); "trusted"
+        skips the check (the caller guarantees it).
     """
 
-    def __init__(self, device=None, seed: Optional[int] = None):
+    def __init__(self, device=None, seed: Optional[int] = None, privacy_id_sharding: str = "verify"):
+        if privacy_id_sharding not in ("verify", "shuffle", "trusted"):
+            raise ValueError(f"privacy_id_sharding must be 'verify', 'shuffle' or 'trusted', "
+                             f"got {privacy_id_sharding!r}")
         self._device = device
         self._seed = seed
+        self._pid_sharding = privacy_id_sharding
         self.last_plan_info = None
 
     # ---------------------------------------------------- recorded ops --
@@ -584,7 +595,27 @@ class AggregateRun:
             if parallel.all_ranks_any(val_t.dtype != torch.int64):  # one value kind on every rank
                 val_t = val_t.to(torch.float64)
             value_kind = N.VALUE_I64 if val_t.dtype == torch.int64 else N.VALUE_F64
+        if pid_t is not None and parallel.world_info()[0] > 1 and self.backend._pid_sharding != "trusted":
+            pid_t, pk_t, val_t, pid_enc = self._shard_privacy_ids(pid_t, pk_t, val_t, pid_enc)
         return pid_t, pk_t, val_t, value_kind, pid_enc, pk_enc, public_codes
+
+    def _shard_privacy_ids(self, pid_t, pk_t, val_t, pid_enc):
+        """Multi-rank: verify that no privacy id spans ranks, or shuffle the
+        rows to the privacy ids' owner ranks (ColumnarBackend
+        privacy_id_sharding).  Identities: integer ids themselves, else a
+        fixed-key hash of the key (parallel.key_identities)."""
+        import torch
+        table = None if pid_enc.decode is None else \
+            torch.as_tensor(parallel.key_identities(pid_enc.decode)).to(pid_t.device)
+        if self.backend._pid_sharding == "verify":
+            parallel.check_privacy_ids_disjoint(torch.unique(pid_t) if table is None else table)
+            return pid_t, pk_t, val_t, pid_enc
+        ident = pid_t if table is None else table[pid_t]
+        ident, (pk_t, val_t) = parallel.shuffle_by_privacy_id(ident, [pk_t, val_t])
+        uniq, inv = torch.unique(ident, return_inverse=True)  # dense local codes of the received ids
+        pid_t = inv.to(torch.int64).contiguous()
+        return pid_t, pk_t.contiguous(), None if val_t is None else val_t.contiguous(), \
+            C.EncodedKeys(pid_t, max(int(uniq.numel()), 1), None)
 
     def _bounding_spec(self, value_kind):
         from pipelinedp_amd.executor import BoundingSpec

@@ -179,3 +179,97 @@ def merge_histogram_bins(out, group=None):
     dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group)
     out["float_lowers"][1:2] = part
     dist.all_reduce(out["float_n_lowers"], op=dist.ReduceOp.MAX, group=group)
+
+
+# ------------------------------------------------- privacy ids across ranks --
+# Contribution bounding is exact only if all rows of a privacy id are on one
+# rank (contribution_bounders.py:62-111 bounds per privacy id over the whole
+# dataset).  ColumnarBackend either verifies that the caller sharded by
+# privacy id, or shuffles the rows so that it holds.  Privacy ids are compared
+# by a 64-bit identity: the id itself for integer ids, a fixed-key 64-bit hash
+# of the key for other ids (the same on every rank).
+
+def key_identities(keys) -> "np.ndarray":
+    """int64 identities of a dictionary's keys (pandas' fixed-key SipHash;
+    integers map to themselves)."""
+    import numpy as np
+    arr = np.asarray(keys, dtype=object)
+    if len(arr) and all(isinstance(k, (int, np.integer)) and not isinstance(k, bool) for k in arr):
+        return arr.astype(np.int64)
+    from pandas.util import hash_array
+    return hash_array(arr, categorize=False).view(np.int64)
+
+
+def _owner(ident, world: int):
+    """Rank that owns an identity: a SplitMix64-style mix mod world (so that
+    structured ids, e.g. multiples of the world size, still spread)."""
+    import torch
+    z = ident.to(torch.int64)
+    z = (z ^ (z >> 31)) * -7046029254386353131  # 0x9E3779B97F4A7C15 as int64
+    z = z ^ (z >> 29)
+    return torch.remainder(z, world)
+
+
+def _exchange(parts_by_dest, counts, group):
+    """all-to-all of one tensor already ordered by destination rank."""
+    import torch
+    import torch.distributed as dist
+    host = dist.get_backend(group) == "gloo"  # gloo moves host tensors (CPU tests, 2-rank GPU test)
+    send = counts.to(torch.int64)
+    send = send.cpu() if host else send
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    in_sizes = send.tolist()
+    out_sizes = recv.tolist()
+    out = []
+    for t in parts_by_dest:
+        src = t.contiguous().cpu() if host else t.contiguous()
+        o = torch.empty((sum(out_sizes),) + tuple(t.shape[1:]), dtype=t.dtype, device=src.device)
+        dist.all_to_all_single(o, src, output_split_sizes=out_sizes, input_split_sizes=in_sizes, group=group)
+        out.append(o.to(t.device))
+    return out
+
+
+def check_privacy_ids_disjoint(ids, group=None):
+    """Raises ValueError when a privacy id (int64 identity) is present on more
+    than one rank.  `ids`: the distinct identities of this rank.  Each
+    identity goes to its owner rank (one all-to-all of 8 B per distinct id);
+    owners look for an identity that arrived from two ranks."""
+    import torch
+    import torch.distributed as dist
+    world, rank = world_info(group)
+    if world == 1:
+        return
+    ids = ids.to(torch.int64)
+    dest = _owner(ids, world)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world)
+    (recv,) = _exchange([ids[order]], counts, group)
+    s = torch.sort(recv).values
+    dup = bool((s[1:] == s[:-1]).any()) if s.numel() > 1 else False
+    flag = torch.tensor([1 if dup else 0], dtype=torch.int64,
+                        device="cpu" if dist.get_backend(group) == "gloo" else ids.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        raise ValueError("a privacy id appears on more than one rank: rows must be sharded by privacy id "
+                         "(contribution bounding is per privacy id over the whole dataset, "
+                         "contribution_bounders.py:62-111); pass ColumnarBackend(privacy_id_sharding="
+                         "'shuffle') to let the library exchange the rows")
+
+
+def shuffle_by_privacy_id(ident, columns, group=None):
+    """Moves every row to the rank that owns its privacy id (identity):
+    returns (identities, columns) of the rows this rank now holds, in
+    (source rank, source order) order — deterministic for a fixed input.
+    `columns` may hold None entries (passed through as None)."""
+    import torch
+    world, _ = world_info(group)
+    if world == 1:
+        return ident, columns
+    dest = _owner(ident, world)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world)
+    live = [c for c in columns if c is not None]
+    out = _exchange([ident[order]] + [c[order] for c in live], counts, group)
+    it = iter(out[1:])
+    return out[0], [None if c is None else next(it) for c in columns]

@@ -219,6 +219,61 @@ def test_two_ranks_match_single_process(device):
         np.testing.assert_allclose(merged[k], single[k], rtol=1e-9, atol=1e-6)
 
 
+def _row_sharded_worker(rank, port, mode, results):
+    """Rows split by ROW index over two ranks (privacy ids span ranks)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        pid, pk, v, _, P = _rank_data()
+        half = len(pid) // 2
+        sl = slice(0, half) if rank == 0 else slice(half, None)
+        table = pdp.ColumnTable({"pid": pid[sl], "pk": pk[sl], "v": v[sl]}, n_privacy_ids=int(pid.max()) + 1,
+                                n_partitions=P)
+        params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.PRIVACY_ID_COUNT],
+                                     noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=64,
+                                     max_contributions_per_partition=64)
+        backend = CB.ColumnarBackend(seed=7, privacy_id_sharding=mode)
+        acc = pdp.NaiveBudgetAccountant(total_epsilon=1e6, total_delta=1e-6)
+        sink = pdp.DPEngine(acc, backend).aggregate(table, params, _ext(), public_partitions=list(range(P)))
+        acc.compute_budgets()
+        results[rank] = [(int(k), m.count, m.privacy_id_count) for k, m in sink]
+    except ValueError as e:
+        results[rank] = "ValueError: " + str(e)
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["verify", "shuffle"])
+def test_two_ranks_privacy_ids_spanning_ranks(device, mode):
+    """Rows sharded by row, not by privacy id: "verify" (the default) raises on
+    every rank; "shuffle" exchanges the rows to the privacy ids' owner ranks,
+    after which the result (no sampling fires: L0 = Linf = 64, eps = 1e6) is
+    the exact group-by of all rows."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.spawn(_row_sharded_worker, args=(_free_port(), mode, results), nprocs=2, join=True)
+    res = dict(results)
+    if mode == "verify":
+        assert all(isinstance(res[r], str) and "more than one rank" in res[r] for r in (0, 1)), res
+        return
+    assert all(isinstance(res[r], list) for r in (0, 1)), res
+    pid, pk, v, _, P = _rank_data()
+    cnt = np.bincount(pk, minlength=P)
+    pids = np.bincount(np.unique(pid * P + pk) % P, minlength=P)
+    merged = {}
+    for r in (0, 1):
+        for k, c, u in res[r]:
+            assert k not in merged
+            merged[k] = (c, u)
+    assert set(merged) == set(range(P))
+    for k, (c, u) in merged.items():
+        assert abs(c - cnt[k]) < 0.01 and abs(u - pids[k]) < 0.01, (k, c, cnt[k], u, pids[k])
+
+
 def test_select_partitions_matches_reference_golden(device):
     """DPEngine.select_partitions on ColumnarBackend returns the reference's
     kept keys (tests/golden/select_partitions.json, eps = 1e4)."""

@@ -127,3 +127,60 @@ def test_global_partition_dictionary_and_offsets():
     results = manager.dict()
     mp.spawn(_dict_worker, args=(_free_port(), results), nprocs=WORLD, join=True)
     assert dict(results) == {0: "ok", 1: "ok"}
+
+
+def _pid_worker(rank, port, results):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        # disjoint privacy ids: accepted
+        parallel.check_privacy_ids_disjoint(torch.arange(rank, 1000, WORLD))
+        # one shared id among many: rejected on every rank
+        ids = torch.arange(rank * 500, rank * 500 + 500)
+        ids = torch.cat([ids, torch.tensor([123_456])])
+        try:
+            parallel.check_privacy_ids_disjoint(ids)
+            results[rank] = "overlap not detected"
+            return
+        except ValueError as e:
+            assert "more than one rank" in str(e)
+        # string ids: identities are a fixed-key hash, equal across ranks
+        a = parallel.key_identities(np.asarray(["u1", "u2", f"only{rank}"], dtype=object))
+        b = parallel.key_identities(np.asarray(["u2", "u1"], dtype=object))
+        assert list(a[:2]) == list(b[::-1])
+        assert list(parallel.key_identities(np.asarray([5, 7], dtype=object))) == [5, 7]
+        # shuffle: every privacy id's rows end on its owner rank, rows preserved
+        rng = np.random.default_rng(rank)
+        pid = torch.as_tensor(rng.integers(0, 300, 2000))
+        pk = torch.as_tensor(rng.integers(0, 50, 2000))
+        val = torch.as_tensor(rng.normal(size=2000))
+        got_pid, (got_pk, got_val, none) = parallel.shuffle_by_privacy_id(pid, [pk, val, None])
+        assert none is None
+        assert bool((parallel._owner(got_pid, WORLD) == rank).all())
+        parallel.check_privacy_ids_disjoint(torch.unique(got_pid))
+        rows = sorted(zip(got_pid.tolist(), got_pk.tolist(), got_val.tolist()))
+        objs = [None] * WORLD
+        dist.all_gather_object(objs, rows)
+        every = sorted(r for part in objs for r in part)
+        mine = list(zip(pid.tolist(), pk.tolist(), val.tolist()))
+        allin = [None] * WORLD
+        dist.all_gather_object(allin, mine)
+        assert every == sorted(r for part in allin for r in part)
+        results[rank] = "ok"
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_privacy_ids_spanning_ranks_are_detected_and_shuffle_fixes_them():
+    """rows sharded by row would let one privacy id contribute on
+    several ranks (world x L0 partitions, breaking the sensitivity); the
+    library detects it, or exchanges the rows by privacy-id owner."""
+    import torch.multiprocessing as mp
+    manager = mp.Manager()
+    results = manager.dict()
+    mp.spawn(_pid_worker, args=(_free_port(), results), nprocs=WORLD, join=True)
+    assert dict(results) == {0: "ok", 1: "ok"}
