@@ -66,6 +66,11 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the "
+                         "n_gpus it sees (tests/test_bench_launcher.py)")
+    ap.add_argument("--no-api", dest="api", action="store_false",
+                    help="skip the public-API timing (DPEngine.aggregate on ColumnarBackend)")
     return ap.parse_args()
 
 
@@ -193,6 +198,44 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields):
     return out
 
 
+def api_timing(args, workload, pid, pk, value, U, P, ws):
+    """The same aggregate through the public API: DPEngine.aggregate over a
+    device-resident ColumnTable on ColumnarBackend, + compute_budgets() + the
+    materialised result (graph recognition, parameter/budget plumbing, key
+    checks, output columns included), timed like the steps."""
+    import torch
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd import columnar_backend as CB
+    w = C3 if workload == "c3" else C2
+    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U, n_partitions=P)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN],
+                                 noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=w["l0"],
+                                 max_contributions_per_partition=w["linf"], min_value=MIN_VALUE,
+                                 max_value=MAX_VALUE)
+    ext = pdp.DataExtractors(privacy_id_extractor=pdp.ColumnExtractor("pid"),
+                             partition_extractor=pdp.ColumnExtractor("pk"),
+                             value_extractor=pdp.ColumnExtractor("v"))
+
+    def api_step():
+        acc = pdp.NaiveBudgetAccountant(total_epsilon=EPS, total_delta=DELTA)
+        sink = pdp.DPEngine(acc, CB.ColumnarBackend(workspace=ws)).aggregate(table, params, ext)
+        acc.compute_budgets()
+        return len(sink.collect())
+
+    for _ in range(max(1, args.warmup)):
+        api_step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kept = 0
+    for _ in range(args.steps):
+        kept = api_step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    return {"ms_per_call": ms, "rows_per_s": len(pk) / (ms * 1e-3), "partitions_out": kept,
+            "what": "pipelinedp_amd.DPEngine.aggregate(ColumnTable of device tensors, COUNT+SUM+MEAN) on "
+                    "ColumnarBackend + compute_budgets() + collect() (AggregateResult columns on the host)"}
+
+
 def run_workload(args, workload, world, rank, device, pmc_file):
     import torch
     import torch.distributed as dist
@@ -262,6 +305,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     N.profiler_enable(False)
     kept_pairs = int(acc["privacy_id_count"].sum().item())  # last step, this rank
     kept_rows = int(acc["count"].sum().item())
+    api = api_timing(args, workload, pid, pk, value, U, P, ws) if (world == 1 and args.api) else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -324,6 +368,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                        "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(plan.key_format,
                                                                                plan.key_format)},
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
+        "api": api,
     }
 
 
@@ -333,6 +378,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "requested": args.gpus}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
@@ -365,6 +420,7 @@ def main():
         "kernels": r["kernels"],
         "bound_plan": r["bound_plan"],
         "partitions_kept": r["partitions_kept"],
+        "api": r["api"],
         "cpu_baseline": cpu[0] if cpu else None,
         "cpu_baseline_strong": cpu[1] if cpu else None,
     }
@@ -372,7 +428,7 @@ def main():
         torch.cuda.empty_cache()
         s = run_workload(args, "c2", 1, 0, device, PMC_SUMMARY["c2"])
         result["secondary"] = {k: s[k] for k in ("value", "ms_per_step", "config", "roofline",
-                                                 "path_roofline", "kernels", "bound_plan")}
+                                                 "path_roofline", "kernels", "bound_plan", "api")}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

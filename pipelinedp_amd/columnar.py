@@ -16,7 +16,8 @@ dictionary_encode or pandas.factorize.  The dictionary decodes output
 partitions back to the user's keys.
 """
 import dataclasses
-from typing import Any, Mapping, Optional, Sequence
+from collections.abc import Sequence
+from typing import Any, Mapping, Optional
 
 import numpy as np
 
@@ -217,9 +218,74 @@ class EncodedKeys:
     def key_of(self, code: int):
         return int(code) if self.decode is None else self.decode[code]
 
+    def keys_of(self, codes: np.ndarray) -> np.ndarray:
+        """Vectorised key_of (int64 codes -> int64 keys or an object array)."""
+        codes = np.asarray(codes, dtype=np.int64)
+        return codes.copy() if self.decode is None else np.asarray(self.decode, dtype=object)[codes]
+
 
 def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch")
+
+
+class AggregateResult(Sequence):
+    """The output of DPEngine.aggregate on ColumnarBackend: a sequence of
+    (partition_key, MetricsTuple) — the reference's element type
+    (combiners.py:786-788) — held as columns.
+
+    Nothing is built per partition until an element is read:
+    `partition_keys` (a NumPy array) and `columns` (field name -> float64
+    NumPy array, the MetricsTuple field order) are the materialised result;
+    indexing / iterating yields the reference's tuples on demand.  Partitions
+    come in ascending partition-code order (the reference's LocalBackend
+    yields first-appearance order; compare by key)."""
+
+    def __init__(self, partition_keys: np.ndarray, columns: dict, tuple_type):
+        self.partition_keys = partition_keys
+        self.columns = columns
+        self._fields = tuple(columns)
+        self._nt = tuple_type
+
+    @property
+    def fields(self):
+        return self._fields
+
+    def __len__(self):
+        return len(self.partition_keys)
+
+    def _row(self, i):
+        return (_py_key(self.partition_keys[i]), self._nt(*(float(self.columns[f][i]) for f in self._fields)))
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self._row(j) for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        return self._row(i)
+
+    def __iter__(self):
+        cols = [self.columns[f].tolist() for f in self._fields]
+        keys = self.partition_keys.tolist()
+        nt = self._nt
+        return (( k, nt(*vals)) for k, *vals in zip(keys, *cols))
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def to_arrow(self):
+        """pyarrow Table (partition_key + one column per metric)."""
+        import pyarrow as pa
+        return pa.table({"partition_key": pa.array(self.partition_keys.tolist()),
+                         **{f: pa.array(v) for f, v in self.columns.items()}})
+
+    def __repr__(self):
+        return f"AggregateResult({len(self)} partitions, fields={self._fields})"
+
+
+def _py_key(k):
+    return k.item() if isinstance(k, np.generic) else k
 
 
 def encode_keys(values, declared_n: Optional[int] = None) -> EncodedKeys:

@@ -93,9 +93,16 @@ class _Node:
         self._result = None
 
     def __iter__(self):
+        return iter(self.collect())
+
+    def collect(self):
+        """Executes the recognised graph once and returns its result: for
+        DPEngine.aggregate a columnar.AggregateResult (a sequence of
+        (partition_key, MetricsTuple) with `partition_keys` / `columns` arrays), for
+        select_partitions the list of keys, for add_dp_noise the pairs."""
         if self._result is None:
             self._result = self.backend._execute(self)
-        return iter(self._result)
+        return self._result
 
     def __bool__(self):
         return True
@@ -430,15 +437,19 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
         raises ValueError otherwise; "shuffle" moves every row to the rank
         that owns its privacy id (one all-to-all of the rows); "trusted"
         skips the check (the caller guarantees it).
+      workspace: an executor.BoundWorkspace to reuse (the bounding kernels'
+        device workspace; by default each backend keeps its own across runs).
     """
 
-    def __init__(self, device=None, seed: Optional[int] = None, privacy_id_sharding: str = "verify"):
+    def __init__(self, device=None, seed: Optional[int] = None, privacy_id_sharding: str = "verify",
+                 workspace=None):
         if privacy_id_sharding not in ("verify", "shuffle", "trusted"):
             raise ValueError(f"privacy_id_sharding must be 'verify', 'shuffle' or 'trusted', "
                              f"got {privacy_id_sharding!r}")
         self._device = device
         self._seed = seed
         self._pid_sharding = privacy_id_sharding
+        self._workspace = workspace
         self.last_plan_info = None
 
     # ---------------------------------------------------- recorded ops --
@@ -659,8 +670,11 @@ class AggregateRun:
         if pk_t.numel() == 0:
             acc = X.new_accumulators(P, spec, pk_t.device)
         else:
+            if self.backend._workspace is None:
+                self.backend._workspace = X.BoundWorkspace()
             acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=n_pid, n_partitions=P,
-                                     bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset)
+                                     bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset,
+                                     workspace=self.backend._workspace)
             self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec)
         return acc, spec, pk_enc, allowed
 
@@ -708,19 +722,15 @@ class AggregateRun:
                                                 partition_offset=first)
         idx = index.cpu().numpy()
         if self.plan.keys_only:  # select_partitions: "Drop accumulators, keep only partition keys"
-            return [pk_enc.key_of(first + p) for p in idx.tolist()]
-        vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((len(self.prog.fields), 0))
+            return pk_enc.keys_of(first + idx).tolist()
+        nf = len(self.prog.fields)
+        vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((nf, 0))
+        keep = np.ones(len(idx), dtype=bool)
+        if self.prog.threshold_combiner is not None:  # dp_engine.py:544-549: drop thresholded None (NaN)
+            keep = ~np.isnan(vals[self.prog.fields.index("privacy_id_count")])
         nt = pdc._get_or_create_named_tuple("MetricsTuple", tuple(self.prog.fields))
-        result = []
-        drop_nan_pid = self.prog.threshold_combiner is not None
-        pid_col = self.prog.fields.index("privacy_id_count") if drop_nan_pid else -1
-        columns = [vals[c].tolist() for c in range(len(self.prog.fields))]
-        for j, p in enumerate(idx.tolist()):
-            row = tuple(col[j] for col in columns)
-            if drop_nan_pid and row[pid_col] != row[pid_col]:
-                continue
-            result.append((pk_enc.key_of(first + p), nt(*row)))
-        return result
+        cols = {f: np.ascontiguousarray(vals[c][keep]) for c, f in enumerate(self.prog.fields)}
+        return C.AggregateResult(pk_enc.keys_of(first + idx[keep]), cols, nt)
 
     def raw_accumulators(self):
         acc, spec, pk_enc, allowed = self._bound()

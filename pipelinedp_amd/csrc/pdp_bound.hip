@@ -828,17 +828,25 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
     if (threadIdx.x == 0) s_J = (int)J;
     __syncthreads();
   }
-  // tile of the record at relative offset o: the last run start <= o
+  // tile of the record at relative offset o: the last run start <= o.  A
+  // thread's records come in increasing offsets, so after one binary search
+  // the LDS cursor only moves forward (about one tile per 1024 records).
+  int jcur = -1;
   auto tile_of = [&](int64_t o) -> int64_t {
     const int J = s_J;
     if (o < (int64_t)toff[J]) {
-      int a = 0, b = J - 1;
-      while (a < b) {
-        const int m = (a + b + 1) >> 1;
-        if ((int64_t)toff[m] <= o) a = m;
-        else b = m - 1;
+      if (jcur < 0) {
+        int a = 0, b = J - 1;
+        while (a < b) {
+          const int m = (a + b + 1) >> 1;
+          if ((int64_t)toff[m] <= o) a = m;
+          else b = m - 1;
+        }
+        jcur = a;
+      } else {
+        while (jcur + 1 < J && (int64_t)toff[jcur + 1] <= o) ++jcur;
       }
-      return T0 + a;
+      return T0 + jcur;
     }
     int64_t a = T0 + J, b = kp.n_tiles - 1;  // beyond the LDS span (sparse region): global search
     while (a < b) {
@@ -1403,24 +1411,48 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
     s2[t] = 0.0;
   }
   __syncthreads();
-  for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
-    int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (pre[mid] <= i) lo = mid;
-      else hi = mid - 1;
+  // Records in LDS accumulators; RR records per thread in flight (their run
+  // lookups and loads issued before the atomics: the hot ranges of a Zipf
+  // key column give a few workgroups most records, so latency per record
+  // matters more than bandwidth here).
+  constexpr int RR = 4;
+  for (unsigned i0 = threadIdx.x; i0 < total; i0 += RR * blockDim.x) {
+    uint64_t idx[RR];
+    bool ok[RR];
+#pragma unroll
+    for (int u = 0; u < RR; ++u) {
+      const unsigned i = i0 + u * blockDim.x;
+      ok[u] = i < total;
+      int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
+      while (ok[u] && lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      idx[u] = ok[u] ? start[lo] + (i - pre[lo]) : 0;
     }
-    const uint64_t idx = start[lo] + (i - pre[lo]);
-    const unsigned long long key = rec.key[idx];
-    const int lp = (int)((key >> 32) - (uint64_t)p0);
-    atomicAdd(pc + lp, 1u);
-    atomicAdd(cn + lp, (unsigned)key);
-    if (f0) {
-      if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(rec.f0[idx]));
-      else atomicAdd(s0 + lp, rec.f0[idx]);
+    unsigned long long key[RR];
+    double v0[RR], v1[RR], v2[RR];
+#pragma unroll
+    for (int u = 0; u < RR; ++u) {
+      key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
+      v0[u] = (ok[u] && f0) ? rec.f0[idx[u]] : 0.0;
+      v1[u] = (ok[u] && f1) ? rec.f1[idx[u]] : 0.0;
+      v2[u] = (ok[u] && f2) ? rec.f2[idx[u]] : 0.0;
     }
-    if (f1) atomicAdd(s1 + lp, rec.f1[idx]);
-    if (f2) atomicAdd(s2 + lp, rec.f2[idx]);
+#pragma unroll
+    for (int u = 0; u < RR; ++u) {
+      if (!ok[u]) continue;
+      const int lp = (int)((key[u] >> 32) - (uint64_t)p0);
+      atomicAdd(pc + lp, 1u);
+      atomicAdd(cn + lp, (unsigned)key[u]);
+      if (f0) {
+        if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0[u]));
+        else atomicAdd(s0 + lp, v0[u]);
+      }
+      if (f1) atomicAdd(s1 + lp, v1[u]);
+      if (f2) atomicAdd(s2 + lp, v2[u]);
+    }
   }
   __syncthreads();
   int64_t plen = kp.P - p0;

@@ -151,7 +151,19 @@ def exchange_histogram_stats(pkstat, psum, minmax, group=None):
     are order-preserving uint64 images; flipping the top bit makes their
     order the signed int64 order that ReduceOp.MIN / MAX use."""
     import torch.distributed as dist
-    dist.all_reduce(pkstat, op=dist.ReduceOp.SUM, group=group)
+    # each word packs (distinct pids << 32 | rows) for one rank's shard; sum
+    # the two halves separately so that a partition's global row count cannot
+    # carry into its privacy-id count, and refuse totals the packed format of
+    # pdp_dataset_histograms_finish cannot hold
+    mask = 0xFFFFFFFF
+    lo = pkstat & mask
+    hi = (pkstat >> 32) & mask
+    dist.all_reduce(lo, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.SUM, group=group)
+    if bool((lo > mask).any()) or bool((hi > mask).any()):
+        raise ValueError("a partition holds 2^32 or more rows or privacy ids over all ranks; "
+                         "the dataset histograms count per partition in 32 bits")
+    pkstat.copy_((hi << 32) | lo)
     dist.all_reduce(psum, op=dist.ReduceOp.SUM, group=group)
     signed = minmax ^ _SIGN
     lo, hi = signed[0:1].clone(), signed[1:2].clone()

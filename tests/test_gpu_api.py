@@ -271,7 +271,7 @@ def test_two_ranks_privacy_ids_spanning_ranks(device, mode):
             merged[k] = (c, u)
     assert set(merged) == set(range(P))
     for k, (c, u) in merged.items():
-        assert abs(c - cnt[k]) < 0.01 and abs(u - pids[k]) < 0.01, (k, c, cnt[k], u, pids[k])
+        assert abs(c - cnt[k]) < 0.5 and abs(u - pids[k]) < 0.5, (k, c, cnt[k], u, pids[k])  # b = 0.008
 
 
 def test_select_partitions_matches_reference_golden(device):

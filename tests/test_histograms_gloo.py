@@ -76,3 +76,28 @@ def test_exchange_and_merge_two_ranks():
     assert out["float_max"] == [[-0.5, 5.0], [3.0, -4.0]]
     assert out["float_lowers"] == [[-3.0, 0.0, 6.0], [1.0, 2.0, 4.0]]
     assert out["float_n_lowers"] == [3, 3]
+
+
+def _overflow_worker(rank, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        # rows of one partition: 2^31 + 5 on each rank -> 2^32 + 10 in total, which
+        # would carry into the packed privacy-id count
+        pkstat = torch.tensor([(1 << 32) | ((1 << 31) + 5), (1 << 32) | 3], dtype=torch.int64)
+        psum = torch.zeros(2, dtype=torch.float64)
+        minmax = torch.tensor([_ord(0.0), _ord(1.0)], dtype=torch.int64)
+        try:
+            parallel.exchange_histogram_stats(pkstat, psum, minmax, None)
+            results[rank] = "no error"
+        except ValueError as e:
+            results[rank] = "ValueError" if "2^32" in str(e) else repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_partition_counter_overflow_across_ranks_raises():
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.spawn(_overflow_worker, args=(_free_port(), results), nprocs=2, join=True)
+    assert dict(results) == {0: "ValueError", 1: "ValueError"}
