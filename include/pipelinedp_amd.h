@@ -114,7 +114,7 @@ typedef struct pdp_bound_plan_info {
   int64_t lds_bytes;   /* per bucket workgroup */
   int32_t merge;       /* resolved PDP_MERGE_* (0 for GLOBAL_SKETCH) */
   int32_t n_ranges;    /* PDP_MERGE_RANGES: partition ranges of 2^11 keys */
-  int64_t range_group; /* PDP_MERGE_RANGES: buckets per range-reduce workgroup */
+  int64_t range_group; /* PDP_MERGE_RANGES: records per range-reduce work item */
   int32_t key_format;  /* resolved PDP_KEYS_* (BUCKETED) */
   int32_t reserved;
 } pdp_bound_plan_info;

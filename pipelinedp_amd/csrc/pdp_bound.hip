@@ -57,8 +57,11 @@ constexpr int kRangeBits = 11;                // partitions per merge range = 20
 constexpr int kRangeParts = 1 << kRangeBits;
 constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= one block scan
 constexpr int kRangeThreads = 256;
-constexpr int64_t kRangeTargetGroups = 1024;  // range-reduce workgroups aimed for
-constexpr int64_t kRangeMaxGroup = 32;        // buckets per range-reduce workgroup, at most
+// range-reduce work item: the records of one partition range from a run of
+// consecutive buckets, cut at bucket boundaries every kRangeChunk records
+// (k_range_plan), so a Zipf-hot range spreads over many workgroups and a cold
+// one is a single item
+constexpr int64_t kRangeChunk = 8192;
 constexpr unsigned kRangeDirect = 256;        // records below which a workgroup adds them directly
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
@@ -111,8 +114,8 @@ struct Plan {
   int64_t lds_bytes;
   int merge;            // PDP_MERGE_* (bucketed)
   int n_ranges;         // PDP_MERGE_RANGES: ceil(P / 2^kRangeBits)
-  int64_t range_group;  // buckets per range-reduce workgroup
-  int64_t n_groups;
+  int64_t range_group;  // records per range-reduce work item (kRangeChunk)
+  int64_t n_groups;     // upper bound on the range-reduce work items (+ one sentinel per range)
   int key_format;       // PDP_KEYS_WIDE / PDP_KEYS_COMPACT (bucketed)
 };
 
@@ -186,12 +189,11 @@ Plan make_plan(const pdp_bound_config* c) {
     if (p.key_format != PDP_KEYS_WIDE) p.lds_bytes += ((int64_t)4 << p.bucket_bits);
   }
   if (p.merge == PDP_MERGE_RANGES) {
-    int64_t g = (p.n_buckets * p.n_ranges + kRangeTargetGroups - 1) / kRangeTargetGroups;
-    // at most kRangeMaxGroup buckets per workgroup: a skewed (Zipf) key column
-    // puts most kept pairs in the first ranges, which then still spread over
-    // n_buckets / kRangeMaxGroup workgroups; near-empty workgroups exit early
-    p.range_group = g < 1 ? 1 : (g > kRangeMaxGroup ? kRangeMaxGroup : g);
-    p.n_groups = (p.n_buckets + p.range_group - 1) / p.range_group;
+    // range r yields ceil(records_r / C) items + 1 sentinel, and a bucket
+    // emits at most l0 * 2^bucket_bits records in all
+    const int64_t recs = p.n_buckets * ((int64_t)c->l0 << p.bucket_bits);
+    p.range_group = kRangeChunk;
+    p.n_groups = recs / kRangeChunk + 2 * (int64_t)p.n_ranges + 1;
   } else {
     p.n_ranges = 0;
     p.range_group = 0;
@@ -210,6 +212,7 @@ struct Ws {
   uint64_t win_tile;  // PDP_KEYS_PACKED: first tile of every level-2 window
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
+  uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
   uint64_t total;
 };
 
@@ -263,6 +266,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       if (c->flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION)) { w.rec_f0 = off; off = align256(off + recs * 8); }
       if (c->flags & PDP_ACC_NSUM) { w.rec_f1 = off; off = align256(off + recs * 8); }
       if (c->flags & PDP_ACC_NSUM2) { w.rec_f2 = off; off = align256(off + recs * 8); }
+      w.rr_items = off; off = align256(off + (uint64_t)p.n_groups * 16);
+      w.rr_count = off; off = align256(off + 16);
     }
   }
   w.total = off;
@@ -306,7 +311,6 @@ struct KP {  // kernel parameters
   int pk_bits, bucket_bits, super_bits, rand_shift;
   int64_t n_buckets, n_supers, n_tiles;
   int n_ranges;
-  int64_t range_group;
   int keys_vec;  // privacy_id / partition_key columns are 16-byte aligned
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
@@ -328,7 +332,6 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.n_supers = p.n_supers;
   k.n_tiles = p.n_tiles;
   k.n_ranges = p.n_ranges;
-  k.range_group = p.range_group;
   k.keys_vec = 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
@@ -1343,10 +1346,65 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   }
 }
 
-// PDP_MERGE_RANGES: workgroup (range r, bucket group g) sums the records of
-// partitions [r*2^11, (r+1)*2^11) emitted by buckets [g*G, (g+1)*G) in LDS,
-// then adds the partial sums with coalesced device atomics.
-__global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec,
+// PDP_MERGE_RANGES work items.  Range r's records, taken bucket-major, are cut
+// into items at bucket boundaries: a new item starts after the bucket that
+// holds record position k * kRangeChunk (k >= 1), so every item holds about
+// kRangeChunk records or one bucket's run, a Zipf-hot range spreads over many
+// workgroups and a cold range is one item.  Range r appends its K_r =
+// ceil(total_r / C) items plus a sentinel at a base taken with one atomicAdd
+// (ranges land in any order); entry k + 1 holds item k's end.  Entry:
+// {r | sentinel << 31, first bucket, first record position within the range}.
+__global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsigned* __restrict__ runs,
+                                                              uint4* __restrict__ items,
+                                                              unsigned* __restrict__ n_items) {
+  __shared__ unsigned wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned s_base;
+  const int r = blockIdx.x;
+  const int64_t stride = kp.n_ranges + 1;
+  auto len_of = [&](int64_t b) -> unsigned {
+    if (b >= kp.n_buckets) return 0u;
+    const unsigned* run = runs + b * stride + r;
+    return run[1] - run[0];
+  };
+  unsigned total = 0;
+  for (int64_t c = 0; c < kp.n_buckets; c += blockDim.x) {
+    unsigned t;
+    block_excl_scan(len_of(c + threadIdx.x), wsum, &t);
+    total += t;
+    __syncthreads();
+  }
+  if (total == 0) return;  // block-uniform: no items
+  const unsigned C = (unsigned)kRangeChunk;
+  const unsigned K = (total + C - 1) / C;
+  if (threadIdx.x == 0) s_base = atomicAdd(n_items, K + 1);
+  __syncthreads();
+  const unsigned base = s_base;
+  if (threadIdx.x == 0) items[base] = make_uint4((unsigned)r, 0u, 0u, 0u);
+  if (threadIdx.x == 0 && total % C != 0)
+    items[base + K] = make_uint4((unsigned)r | 0x80000000u, (unsigned)kp.n_buckets, total, 0u);
+  unsigned carry = 0;
+  for (int64_t c = 0; c < kp.n_buckets; c += blockDim.x) {
+    const int64_t b = c + threadIdx.x;
+    const unsigned len = len_of(b);
+    unsigned t;
+    const unsigned ex = carry + block_excl_scan(len, wsum, &t);
+    if (len > 0) {
+      // items k >= 1 with k * C in (ex, ex + len] start after this bucket
+      const unsigned e = ex + len;
+      for (unsigned k = ex / C + 1; k * C <= e; ++k)
+        items[base + k] = make_uint4((unsigned)r | (k == K ? 0x80000000u : 0u), (unsigned)(b + 1), e, 0u);
+    }
+    carry += t;
+    __syncthreads();
+  }
+}
+
+// PDP_MERGE_RANGES: one workgroup per work item (k_range_plan) sums its
+// records of partitions [r*2^11, (r+1)*2^11) in LDS, then adds the partial
+// sums with coalesced device atomics (an item of few records adds them
+// directly).
+__global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec, const uint4* __restrict__ items,
+                                                               const unsigned* __restrict__ n_items,
                                                                pdp_partition_accumulators acc) {
 #if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
   return;  // ablation: only the level-1 pass is meaningful
@@ -1360,101 +1418,101 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
   unsigned* cn = pc + kRangeParts;                    // [kRangeParts] row count
   unsigned* pre = cn + kRangeParts;                   // [kRangeThreads] run prefix
   unsigned* wsum = pre + kRangeThreads;               // block-scan scratch
+  if (blockIdx.x >= *n_items) return;  // grid is an upper bound on the item count
+  const uint4 it = items[blockIdx.x];
+  if (it.x >> 31) return;  // sentinel
+  const uint4 nx = items[blockIdx.x + 1];
+  const int r = (int)it.x;
+  const int64_t b_lo = it.y, b_hi = nx.y;
+  const unsigned item_total = nx.z - it.z;
+  if (item_total == 0) return;
   const int flags = kp.clip.flags;
   const bool f0 = flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION), f1 = flags & PDP_ACC_NSUM,
              f2 = flags & PDP_ACC_NSUM2, sum_int = flags & PDP_SUM_INT;
-  const int r = blockIdx.x;
   const int64_t p0 = (int64_t)r << kRangeBits;
-  const int64_t b0 = (int64_t)blockIdx.y * kp.range_group;
-  int64_t nb = kp.n_buckets - b0;
-  if (nb > kp.range_group) nb = kp.range_group;
   const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
-  unsigned len = 0;
-  if (threadIdx.x < nb) {
-    const unsigned* run = rec.runs + (b0 + threadIdx.x) * (kp.n_ranges + 1) + r;
-    const unsigned s = run[0];
-    len = run[1] - s;
-    start[threadIdx.x] = (unsigned long long)((b0 + threadIdx.x) * n_slots + s);
-  }
-  unsigned total;
-  const unsigned ex = block_excl_scan(len, wsum, &total);
-  pre[threadIdx.x] = ex;
-  if (total == 0) return;  // block-uniform
-  __syncthreads();
-  if (total < kRangeDirect) {  // few records: straight into the accumulators
-    for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
-      int lo = 0, hi = (int)nb - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= i) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint64_t idx = start[lo] + (i - pre[lo]);
-      const unsigned long long key = rec.key[idx];
-      const int64_t p = (int64_t)(key >> 32);
-      atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
-      if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key);
-      if (f0) {
-        if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(rec.f0[idx]));
-        else unsafeAtomicAdd((double*)acc.sum + p, rec.f0[idx]);
-      }
-      if (f1) unsafeAtomicAdd(acc.normalized_sum + p, rec.f1[idx]);
-      if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, rec.f2[idx]);
+  const bool direct = item_total < kRangeDirect;  // few records: straight into the accumulators
+  if (!direct) {
+    for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
+      pc[t] = 0;
+      cn[t] = 0;
+      s0[t] = 0.0;
+      s1[t] = 0.0;
+      s2[t] = 0.0;
     }
-    return;
   }
-  for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
-    pc[t] = 0;
-    cn[t] = 0;
-    s0[t] = 0.0;
-    s1[t] = 0.0;
-    s2[t] = 0.0;
-  }
-  __syncthreads();
-  // Records in LDS accumulators; RR records per thread in flight (their run
-  // lookups and loads issued before the atomics: the hot ranges of a Zipf
-  // key column give a few workgroups most records, so latency per record
-  // matters more than bandwidth here).
+  // buckets in batches of one per thread: run starts, block scan, then the
+  // batch's records, RR per thread in flight (their run lookups and loads
+  // issued before the atomics)
   constexpr int RR = 4;
-  for (unsigned i0 = threadIdx.x; i0 < total; i0 += RR * blockDim.x) {
-    uint64_t idx[RR];
-    bool ok[RR];
+  for (int64_t bb = b_lo; bb < b_hi; bb += blockDim.x) {
+    int64_t nb = b_hi - bb;
+    if (nb > blockDim.x) nb = blockDim.x;
+    unsigned len = 0;
+    if (threadIdx.x < nb) {
+      const int64_t b = bb + threadIdx.x;
+      const unsigned* run = rec.runs + b * (kp.n_ranges + 1) + r;
+      const unsigned s = run[0];
+      len = run[1] - s;
+      start[threadIdx.x] = (unsigned long long)(b * n_slots + s);
+    }
+    unsigned total;
+    const unsigned ex = block_excl_scan(len, wsum, &total);
+    pre[threadIdx.x] = ex;
+    __syncthreads();
+    for (unsigned i0 = threadIdx.x; i0 < total; i0 += RR * blockDim.x) {
+      uint64_t idx[RR];
+      bool ok[RR];
 #pragma unroll
-    for (int u = 0; u < RR; ++u) {
-      const unsigned i = i0 + u * blockDim.x;
-      ok[u] = i < total;
-      int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
-      while (ok[u] && lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (pre[mid] <= i) lo = mid;
-        else hi = mid - 1;
+      for (int u = 0; u < RR; ++u) {
+        const unsigned i = i0 + u * blockDim.x;
+        ok[u] = i < total;
+        int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
+        while (ok[u] && lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pre[mid] <= i) lo = mid;
+          else hi = mid - 1;
+        }
+        idx[u] = ok[u] ? start[lo] + (i - pre[lo]) : 0;
       }
-      idx[u] = ok[u] ? start[lo] + (i - pre[lo]) : 0;
-    }
-    unsigned long long key[RR];
-    double v0[RR], v1[RR], v2[RR];
+      unsigned long long key[RR];
+      double v0[RR], v1[RR], v2[RR];
 #pragma unroll
-    for (int u = 0; u < RR; ++u) {
-      key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
-      v0[u] = (ok[u] && f0) ? rec.f0[idx[u]] : 0.0;
-      v1[u] = (ok[u] && f1) ? rec.f1[idx[u]] : 0.0;
-      v2[u] = (ok[u] && f2) ? rec.f2[idx[u]] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < RR; ++u) {
-      if (!ok[u]) continue;
-      const int lp = (int)((key[u] >> 32) - (uint64_t)p0);
-      atomicAdd(pc + lp, 1u);
-      atomicAdd(cn + lp, (unsigned)key[u]);
-      if (f0) {
-        if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0[u]));
-        else atomicAdd(s0 + lp, v0[u]);
+      for (int u = 0; u < RR; ++u) {
+        key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
+        v0[u] = (ok[u] && f0) ? rec.f0[idx[u]] : 0.0;
+        v1[u] = (ok[u] && f1) ? rec.f1[idx[u]] : 0.0;
+        v2[u] = (ok[u] && f2) ? rec.f2[idx[u]] : 0.0;
       }
-      if (f1) atomicAdd(s1 + lp, v1[u]);
-      if (f2) atomicAdd(s2 + lp, v2[u]);
+#pragma unroll
+      for (int u = 0; u < RR; ++u) {
+        if (!ok[u]) continue;
+        if (direct) {
+          const int64_t p = (int64_t)(key[u] >> 32);
+          atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
+          if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key[u]);
+          if (f0) {
+            if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(v0[u]));
+            else unsafeAtomicAdd((double*)acc.sum + p, v0[u]);
+          }
+          if (f1) unsafeAtomicAdd(acc.normalized_sum + p, v1[u]);
+          if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, v2[u]);
+          continue;
+        }
+        const int lp = (int)((key[u] >> 32) - (uint64_t)p0);
+        atomicAdd(pc + lp, 1u);
+        atomicAdd(cn + lp, (unsigned)key[u]);
+        if (f0) {
+          if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0[u]));
+          else atomicAdd(s0 + lp, v0[u]);
+        }
+        if (f1) atomicAdd(s1 + lp, v1[u]);
+        if (f2) atomicAdd(s2 + lp, v2[u]);
+      }
     }
+    __syncthreads();  // pre / start / wsum are reused by the next batch
   }
-  __syncthreads();
+  if (direct) return;
   int64_t plen = kp.P - p0;
   if (plen > kRangeParts) plen = kRangeParts;
   for (int t = threadIdx.x; t < plen; t += blockDim.x) {
@@ -1625,9 +1683,17 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
   if (ranges) {
     PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_range_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kRangeLds));
+    uint4* items = (uint4*)(ws + w.rr_items);
+    unsigned* n_items = (unsigned*)(ws + w.rr_count);
+    PDP_HIP_CHECK(hipMemsetAsync(n_items, 0, 4, st));
+    PDP_PROF_BEGIN("k_range_plan", st);
+    hipLaunchKernelGGL(k_range_plan, dim3((unsigned)p.n_ranges), dim3(kRangeThreads), 0, st, kp,
+                       (const unsigned*)rec.runs, items, n_items);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
     PDP_PROF_BEGIN("k_range_reduce", st);
-    hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_ranges, (unsigned)p.n_groups), dim3(kRangeThreads),
-                       kRangeLds, st, kp, rec, acc);
+    hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kRangeThreads), kRangeLds, st, kp, rec,
+                       (const uint4*)items, (const unsigned*)n_items, acc);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
