@@ -350,6 +350,41 @@ int pdp_dataset_histograms_finish(int32_t value_kind, int64_t n_rows, int64_t n_
                                   int32_t partition_histograms, const pdp_histogram_bins* out, void* workspace,
                                   uint64_t workspace_bytes, void* stream);
 
+/* Dataset histograms of pre-aggregated rows:
+ * compute_dataset_histograms_on_preaggregated_data
+ * (pipeline_dp/dataset_histograms/computing_histograms.py:713-758).  One row
+ * per (privacy id, partition) pair, as analysis/pre_aggregation.py:19-58
+ * emits them: partition in [0, n_partitions), count (rows of the pair, >= 1),
+ * sum (their value sum), n_partitions_of_pid and n_contributions_of_pid (the
+ * pair's privacy id's distinct partitions and rows, >= 1); all < 2^62.  The
+ * bins are those of pdp_dataset_histograms, except L0 / L1, which weigh every
+ * row by 1 / n_partitions_of_pid and count, per distinct value v of
+ * n_partitions_of_pid (L0) or n_contributions_of_pid (L1), the weight sum
+ * rounded half to even (_compute_weighted_frequency_histogram :81-102): such a
+ * bin can hold count 0 with max v, and it is present in the reference's
+ * histogram (present bins: count > 0 or max > 0).  Error word bit 0: partition
+ * out of range; bit 1: count / n_partitions / n_contributions outside
+ * [1, 2^62).  n_rows < 2^31.  The two-phase form mirrors
+ * pdp_dataset_histograms_pairs / _finish for rows of one privacy id on one
+ * rank: between _rows and _finish the caller sums pk_rows and pk_count
+ * (uint64[n_partitions]) and psum (double[n_partitions]) over ranks and takes
+ * min / max of the two minmax words, at the offsets _exchange_offsets gives. */
+int pdp_dataset_histograms_preaggregated_workspace_bytes(int64_t n_rows, int64_t n_partitions, uint64_t* bytes);
+int pdp_dataset_histograms_preaggregated(const int64_t* partition, const int64_t* count, const double* sum,
+                                         const int64_t* n_partitions_of_pid, const int64_t* n_contributions_of_pid,
+                                         int64_t n_rows, int64_t n_partitions, const pdp_histogram_bins* out,
+                                         void* workspace, uint64_t workspace_bytes, void* stream);
+int pdp_dataset_histograms_preaggregated_rows(const int64_t* partition, const int64_t* count, const double* sum,
+                                              const int64_t* n_partitions_of_pid,
+                                              const int64_t* n_contributions_of_pid, int64_t n_rows,
+                                              int64_t n_partitions, const pdp_histogram_bins* out, void* workspace,
+                                              uint64_t workspace_bytes, void* stream);
+int pdp_dataset_histograms_preaggregated_exchange_offsets(int64_t n_rows, int64_t n_partitions, uint64_t* pk_rows,
+                                                          uint64_t* pk_count, uint64_t* psum, uint64_t* minmax);
+int pdp_dataset_histograms_preaggregated_finish(const double* sum, int64_t n_rows, int64_t n_partitions,
+                                                int32_t partition_histograms, const pdp_histogram_bins* out,
+                                                void* workspace, uint64_t workspace_bytes, void* stream);
+
 /* Kernel profiler: when enabled, every kernel launch of this library is
  * bracketed by HIP events recorded on its launch stream.  enable(1) clears
  * previous records; report() synchronises on them and returns, per kernel

@@ -98,3 +98,53 @@ def dataset_histograms(pid, pk, value):
         "count_privacy_id_per_partition": frequency_histogram(pk_pids),
         "sum_per_partition_histogram": float_histogram(pk_sum),
     }
+
+
+def weighted_frequency_histogram(values, weights):
+    """_compute_weighted_frequency_histogram (:81-102): per distinct value,
+    int(round(sum of its weights)) (Python's round half to even; the weights
+    summed in row order, as sum_per_key does), then the frequency helper's
+    bins (:105-132): a value whose weight rounds to 0 still makes a bin with
+    count 0 and max = value."""
+    sums = {}
+    for v, w in zip(np.asarray(values, dtype=np.int64).tolist(), np.asarray(weights, dtype=np.float64).tolist()):
+        sums[v] = sums.get(v, 0.0) + w
+    bins = {}
+    for v in sorted(sums):
+        f = int(round(sums[v]))
+        lo, up = log_bin(v)
+        b = bins.get(lo)
+        bins[lo] = (lo, up, f, f * v, v) if b is None else (lo, up, b[2] + f, b[3] + f * v, max(b[4], v))
+    return [bins[k] for k in sorted(bins)]
+
+
+def preaggregated_histograms(pk, count, total, n_partitions, n_contributions):
+    """compute_dataset_histograms_on_preaggregated_data
+    (computing_histograms.py:713-758) over pre-aggregated columns, one row
+    per (privacy id, partition) pair: {field: [bins]}.  L0 weighs
+    n_partitions by 1 / n_partitions (:520-543), L1 n_contributions by
+    1 / n_partitions (:546-568), Linf is the frequency of count (:571-591),
+    Linf-sum the float histogram of sum (:594-625), and the partition
+    histograms sum count / count rows / sum sum per partition (:628-710)."""
+    pk = np.asarray(pk, dtype=np.int64)
+    count = np.asarray(count, dtype=np.int64)
+    total = np.asarray(total, dtype=np.float64)
+    npart = np.asarray(n_partitions, dtype=np.int64)
+    ncontr = np.asarray(n_contributions, dtype=np.int64)
+    if pk.size == 0:
+        return {f: [] for f in HIST_FIELDS}
+    w = np.array([1.0 / v for v in npart.tolist()], dtype=np.float64)
+    pks, inv = np.unique(pk, return_inverse=True)
+    inv = inv.reshape(-1)
+    pk_count = np.bincount(inv, weights=count.astype(np.float64)).astype(np.int64)
+    pk_rows = np.bincount(inv)
+    pk_sum = np.bincount(inv, weights=total)
+    return {
+        "l0_contributions_histogram": weighted_frequency_histogram(npart, w),
+        "l1_contributions_histogram": weighted_frequency_histogram(ncontr, w),
+        "linf_contributions_histogram": frequency_histogram(count),
+        "linf_sum_contributions_histogram": float_histogram(total),
+        "count_per_partition_histogram": frequency_histogram(pk_count),
+        "count_privacy_id_per_partition": frequency_histogram(pk_rows),
+        "sum_per_partition_histogram": float_histogram(pk_sum),
+    }

@@ -52,6 +52,11 @@ EXPORTED_SYMBOLS = (
     "pdp_dataset_histograms_pairs",
     "pdp_dataset_histograms_exchange_offsets",
     "pdp_dataset_histograms_finish",
+    "pdp_dataset_histograms_preaggregated_workspace_bytes",
+    "pdp_dataset_histograms_preaggregated",
+    "pdp_dataset_histograms_preaggregated_rows",
+    "pdp_dataset_histograms_preaggregated_exchange_offsets",
+    "pdp_dataset_histograms_preaggregated_finish",
     "pdp_bound_error_flags",
     "pdp_profiler_enable",
     "pdp_profiler_report",
@@ -200,6 +205,15 @@ def _declare(lib):
         "pdp_dataset_histograms_exchange_offsets": (ctypes.c_int, [i64, i64, i64, P(u64), P(u64), P(u64)]),
         "pdp_dataset_histograms_finish": (ctypes.c_int, [i32, i64, i64, i64, i32, P(HistogramBins),
                                                          vp, u64, vp]),
+        "pdp_dataset_histograms_preaggregated_workspace_bytes": (ctypes.c_int, [i64, i64, P(u64)]),
+        "pdp_dataset_histograms_preaggregated": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64, P(HistogramBins),
+                                                                vp, u64, vp]),
+        "pdp_dataset_histograms_preaggregated_rows": (ctypes.c_int, [vp, vp, vp, vp, vp, i64, i64,
+                                                                     P(HistogramBins), vp, u64, vp]),
+        "pdp_dataset_histograms_preaggregated_exchange_offsets": (ctypes.c_int, [i64, i64, P(u64), P(u64),
+                                                                                 P(u64), P(u64)]),
+        "pdp_dataset_histograms_preaggregated_finish": (ctypes.c_int, [vp, i64, i64, i32, P(HistogramBins),
+                                                                       vp, u64, vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),

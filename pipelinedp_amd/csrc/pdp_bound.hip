@@ -37,8 +37,17 @@ namespace pdp {
 namespace {
 
 constexpr int kPartThreads = 512;
-constexpr int kStageItems = 8;
-constexpr int kStageRows = kPartThreads * kStageItems;  // 4096 rows per LDS stage / level-2 window
+// rows per thread and LDS stage of the level-1 scatter / level-2 window
+#ifndef PDP_L1_ITEMS
+#define PDP_L1_ITEMS 8
+#endif
+#ifndef PDP_L2_ITEMS
+#define PDP_L2_ITEMS 16
+#endif
+constexpr int kL1Items = PDP_L1_ITEMS;
+constexpr int kL1Rows = kPartThreads * kL1Items;  // rows per level-1 LDS stage
+constexpr int kL2Items = PDP_L2_ITEMS;
+constexpr int kL2Rows = kPartThreads * kL2Items;  // records per level-2 window
 constexpr int kTileRowBits = 16;
 constexpr int64_t kTileRows = (int64_t)1 << kTileRowBits;
 constexpr int kUnroll = 8;
@@ -256,7 +265,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.rows2 = w.rows1;
     }
     if (packed) {
-      const uint64_t n_win = (n + 4 * (uint64_t)p.n_supers) / kStageRows + 2 * (uint64_t)p.n_supers + 1;
+      const uint64_t n_win = (n + 4 * (uint64_t)p.n_supers) / kL2Rows + 2 * (uint64_t)p.n_supers + 1;
       w.win_tile = off; off = align256(off + n_win * 4);
     }
     if (p.merge == PDP_MERGE_RANGES) {
@@ -522,26 +531,26 @@ using L2Key = RecKey<FMT != PDP_KEYS_WIDE>;
 // MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
 // fits four workgroups per CU with compact keys instead of three.  ROWS:
 // the stage carries a u32 row array beside the keys.
-template <typename K, int MAXD = kMaxDest, bool ROWS = true>
+template <typename K, int MAXD, bool ROWS, int N>
 struct StageLds {
   using D = typename std::conditional<(MAXD <= 256), uint8_t, unsigned short>::type;
   unsigned hist[MAXD];
   unsigned start[MAXD];
   unsigned gcur[MAXD];
-  K keys[kStageRows];
-  unsigned rows[ROWS ? kStageRows : 1];
-  D dest[kStageRows];
+  K keys[kPartThreads * N];
+  unsigned rows[ROWS ? kPartThreads * N : 1];
+  D dest[kPartThreads * N];
 };
 constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four workgroups per CU
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
-template <typename K, int MAXD, bool ROWS>
-__device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS>& s, int ndest, const int (&d)[kStageItems],
-                                            unsigned (&rank)[kStageItems]) {
+template <typename K, int MAXD, bool ROWS, int N>
+__device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N>& s, int ndest, const int (&d)[N],
+                                            unsigned (&rank)[N]) {
   for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
   __syncthreads();
 #pragma unroll
-  for (int q = 0; q < kStageItems; ++q) rank[q] = d[q] >= 0 ? atomicAdd(s.hist + d[q], 1u) : 0;
+  for (int q = 0; q < N; ++q) rank[q] = d[q] >= 0 ? atomicAdd(s.hist + d[q], 1u) : 0;
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan of hist by one wave
     const int lane = threadIdx.x;
@@ -561,18 +570,18 @@ __device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS>& s, int ndes
 }
 
 // phase 2: place into the LDS stage, then write every run at gcur[dest]
-template <typename K, int MAXD, bool ROWS>
-__device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS>& s, int ndest, const int (&d)[kStageItems],
-                                            const unsigned (&rank)[kStageItems], const K (&x)[kStageItems],
-                                            const unsigned (&r)[kStageItems], K* __restrict__ out_keys,
+template <typename K, int MAXD, bool ROWS, int N>
+__device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS, N>& s, int ndest, const int (&d)[N],
+                                            const unsigned (&rank)[N], const K (&x)[N],
+                                            const unsigned (&r)[N], K* __restrict__ out_keys,
                                             unsigned* __restrict__ out_rows) {
 #pragma unroll
-  for (int q = 0; q < kStageItems; ++q) {
+  for (int q = 0; q < N; ++q) {
     if (d[q] < 0) continue;
     const unsigned slot = s.start[d[q]] + rank[q];
     s.keys[slot] = x[q];
     if (ROWS) s.rows[slot] = r[q];
-    s.dest[slot] = (typename StageLds<K, MAXD, ROWS>::D)d[q];
+    s.dest[slot] = (typename StageLds<K, MAXD, ROWS, N>::D)d[q];
   }
   __syncthreads();
   const unsigned total = s.start[ndest - 1] + s.hist[ndest - 1];
@@ -628,7 +637,7 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   constexpr bool ROWS = FMT != PDP_KEYS_PACKED;
   extern __shared__ unsigned long long stage_raw[];
   static_assert(kMaxSupers <= kSmallDest, "level-1 destinations must fit the small stage");
-  StageLds<K, kSmallDest, ROWS>& s = *reinterpret_cast<StageLds<K, kSmallDest, ROWS>*>(stage_raw);
+  StageLds<K, kSmallDest, ROWS, kL1Items>& s = *reinterpret_cast<StageLds<K, kSmallDest, ROWS, kL1Items>*>(stage_raw);
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
   // this tile's first row in each super-bucket region (k_super_scan)
@@ -640,9 +649,9 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   const uint64_t mid_mask = (1ULL << mid_bits) - 1;
   const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
   // two consecutive rows per 16-byte load (tiles and chunks start even)
-  auto load = [&](int64_t c0, int64_t (&u)[kStageItems], int64_t (&k)[kStageItems]) {
+  auto load = [&](int64_t c0, int64_t (&u)[kL1Items], int64_t (&k)[kL1Items]) {
 #pragma unroll
-    for (int q = 0; q < kStageItems; q += 2) {
+    for (int q = 0; q < kL1Items; q += 2) {
       const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
       if (kp.keys_vec && i + 1 < t1) {
         const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
@@ -659,14 +668,14 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
       }
     }
   };
-  int64_t u[kStageItems], k[kStageItems];
+  int64_t u[kL1Items], k[kL1Items];
   if (t0 < t1) load(t0, u, k);
-  for (int64_t c0 = t0; c0 < t1; c0 += kStageRows) {
-    int d[kStageItems];
-    K x[kStageItems];
-    unsigned r[kStageItems];
+  for (int64_t c0 = t0; c0 < t1; c0 += kL1Rows) {
+    int d[kL1Items];
+    K x[kL1Items];
+    unsigned r[kL1Items];
 #pragma unroll
-    for (int q = 0; q < kStageItems; ++q) {
+    for (int q = 0; q < kL1Items; ++q) {
       r[q] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
       if (u[q] < 0 || u[q] >= kp.U) {  // flagged by k_part_hist, not counted
         d[q] = -1;
@@ -692,15 +701,15 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
     }
 #if PDP_L1_PREFETCH
     // next sub-chunk's column loads go out before this one's LDS passes
-    if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
+    if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
 #endif
-    unsigned rank[kStageItems];
+    unsigned rank[kL1Items];
     stage_count(s, nd, d, rank);
     stage_write(s, nd, d, rank, x, r, keys1, rows1);
     for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += s.hist[B];
     __syncthreads();
 #if !PDP_L1_PREFETCH
-    if (c0 + kStageRows < t1) load(c0 + kStageRows, u, k);
+    if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
 #endif
   }
 }
@@ -716,7 +725,7 @@ __device__ __forceinline__ bool locate_window(const KP& kp, const unsigned* __re
   if (lane < kp.n_supers) {
     lo = super_base[lane];
     hi = super_base[lane + 1];
-    nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kStageRows - 1) / kStageRows : 0;
+    nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kL2Rows - 1) / kL2Rows : 0;
   }
   int64_t inc = nch;
 #pragma unroll
@@ -727,11 +736,11 @@ __device__ __forceinline__ bool locate_window(const KP& kp, const unsigned* __re
   const bool mine = g >= inc - nch && g < inc;
   const unsigned long long hit = __ballot(mine);
   if (mine) {
-    const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kStageRows;
+    const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kL2Rows;
     *s_B = lane;
     *s_base = base;
     *s_r0 = base > lo ? base : lo;
-    *s_r1 = base + kStageRows < hi ? base + kStageRows : hi;
+    *s_r1 = base + kL2Rows < hi ? base + kL2Rows : hi;
   }
   return hit != 0;
 }
@@ -751,7 +760,7 @@ __global__ void __launch_bounds__(kBlock) k_window_tiles(KP kp, const unsigned* 
     int64_t nch = 0;
     if (lane < kp.n_supers) {
       const int64_t lo = super_base[lane], hi = super_base[lane + 1];
-      nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kStageRows - 1) / kStageRows : 0;
+      nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kL2Rows - 1) / kL2Rows : 0;
     }
     int64_t inc = nch;
 #pragma unroll
@@ -770,9 +779,9 @@ __global__ void __launch_bounds__(kBlock) k_window_tiles(KP kp, const unsigned* 
     const int64_t a = super_off[t * kp.n_supers + B];
     const int64_t b = t + 1 < kp.n_tiles ? (int64_t)super_off[(t + 1) * kp.n_supers + B] : total;
     if (a >= b) continue;
-    int64_t k = a == 0 ? 0 : (a - rel0 + kStageRows - 1) / kStageRows;
+    int64_t k = a == 0 ? 0 : (a - rel0 + kL2Rows - 1) / kL2Rows;
     for (;; ++k) {
-      int64_t st = rel0 + k * kStageRows;
+      int64_t st = rel0 + k * kL2Rows;
       if (st < 0) st = 0;
       if (st >= b) break;
       if (st >= a) win_tile[s_g0 + k] = (unsigned)t;
@@ -803,7 +812,7 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
   constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
   constexpr int R = 16 / sizeof(KI);  // records per 16-byte key load
   extern __shared__ unsigned long long stage_raw[];
-  StageLds<KO, MAXD>& s = *reinterpret_cast<StageLds<KO, MAXD>*>(stage_raw);
+  StageLds<KO, MAXD, true, kL2Items>& s = *reinterpret_cast<StageLds<KO, MAXD, true, kL2Items>*>(stage_raw);
   __shared__ int s_B;
   __shared__ int64_t s_base, s_r0, s_r1;
   __shared__ unsigned toff[kWinTiles + 1];  // PACKED: run starts of tiles T0 .. T0 + J
@@ -871,11 +880,11 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
   };
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
-  KO x[kStageItems];
-  unsigned r[kStageItems];
-  int d[kStageItems];
+  KO x[kL2Items];
+  unsigned r[kL2Items];
+  int d[kL2Items];
 #pragma unroll
-  for (int q = 0; q < kStageItems; q += R) {  // R records per 16-byte key load
+  for (int q = 0; q < kL2Items; q += R) {  // R records per 16-byte key load
     const int64_t i = base + R * ((int64_t)threadIdx.x + (int64_t)(q / R) * blockDim.x);
     if (i >= r0 && i + R - 1 < r1) {
       if constexpr (PACKED) {
@@ -912,7 +921,7 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
       }
     }
   }
-  unsigned rank[kStageItems];
+  unsigned rank[kL2Items];
   stage_count(s, nsub, d, rank);
   for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
     const int64_t b = s_first + t;
@@ -1707,7 +1716,7 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   using K1 = L1Key<FMT>;
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
-  const size_t lds = sizeof(StageLds<K1, kSmallDest, ROWS1>);
+  const size_t lds = sizeof(StageLds<K1, kSmallDest, ROWS1, kL1Items>);
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
   PDP_PROF_BEGIN("k_scatter_l1", st);
@@ -1718,7 +1727,7 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
     // windows: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
-    const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kStageRows + 2 * p.n_supers + 1;
+    const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kL2Rows + 2 * p.n_supers + 1;
     unsigned* win_tile = nullptr;
     if (FMT == PDP_KEYS_PACKED) {
       win_tile = (unsigned*)(ws + w.win_tile);
@@ -1730,7 +1739,7 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     }
     const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
     const void* l2 = small ? (const void*)k_scatter_l2<FMT, kSmallDest> : (const void*)k_scatter_l2<FMT, kMaxDest>;
-    const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest>) : sizeof(StageLds<K2, kMaxDest>);
+    const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, kL2Items>) : sizeof(StageLds<K2, kMaxDest, true, kL2Items>);
     PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     PDP_PROF_BEGIN("k_scatter_l2", st);
     if (small)

@@ -462,9 +462,11 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_h_final(IntHists H, FloatHists F, double* fmax_out) {
+// small_mask: the integer histograms whose width-1 bins hold counts only
+// (pre-aggregated L0 / L1 fill theirs in k_hp_weights)
+__global__ void __launch_bounds__(kBlock) k_h_final(IntHists H, FloatHists F, double* fmax_out, int small_mask) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 5 * kSmallBins) {
+  if (i < 5 * kSmallBins && ((small_mask >> (i / kSmallBins)) & 1)) {
     const int h = i / kSmallBins, b = i % kSmallBins;
     const int64_t g = (int64_t)h * kLogBins + b;
     const unsigned long long c = H.count[g];
@@ -480,6 +482,230 @@ __global__ void __launch_bounds__(kBlock) k_h_final(IntHists H, FloatHists F, do
 // min images all ones, max images zero
 __global__ void k_h_init(unsigned long long* minmax) {
   if (threadIdx.x < 4) minmax[threadIdx.x] = (threadIdx.x & 1) ? 0ULL : ~0ULL;
+}
+
+// ------------------------------------------------------ pre-aggregated input --
+// compute_dataset_histograms_on_preaggregated_data (computing_histograms.py:
+// 713-758): one row per (privacy id, partition) pair holding (count, sum,
+// n_partitions, n_contributions), as analysis/pre_aggregation.py:19-58 emits
+// them.  The pairs are given, so there is no pair table:
+//   k_hp_rows     per row: Linf bin of count; per partition (rows, count sum,
+//                 value sum) by atomics; min / max of the row sums; the L0 /
+//                 L1 weights 1 / n_partitions summed per distinct value
+//                 (values < 1000 in LDS, larger ones in an open-addressing
+//                 table keyed by value)
+//   k_hp_weights  per distinct value: count = round half to even of the
+//                 weight sum (_compute_weighted_frequency_histogram :81-102)
+//                 into its bin; the bin exists (max = value) even at count 0
+//   k_hp_ids, k_h_lowers, k_hp_float, k_h_final  as for raw rows
+constexpr int kWSmall = 1000;  // L0 / L1 values below this: dense LDS weight sums
+
+struct WSlot {  // key = value * 2 + histogram + 1 (0 = empty)
+  unsigned long long key;
+  double w;
+};
+
+uint64_t wtab_capacity(int64_t n_rows) {
+  uint64_t c = 2 * (uint64_t)n_rows;
+  c = (c + 255) & ~(uint64_t)255;
+  return c < kMinTable ? kMinTable : c;
+}
+
+struct PWs {
+  uint64_t err, pkrows, pkcount, psum, minmax, fmax, wsmall, wtab, total;
+};
+
+PWs playout(int64_t n, int64_t P) {
+  PWs w{};
+  uint64_t off = 0;
+  w.err = off; off = align256(off + 16);
+  w.pkrows = off; off = align256(off + (uint64_t)P * 8);
+  w.pkcount = off; off = align256(off + (uint64_t)P * 8);
+  w.psum = off; off = align256(off + (uint64_t)P * 8);
+  w.minmax = off; off = align256(off + 4 * 8);
+  w.fmax = off; off = align256(off + 2 * kSumBuckets * 8);
+  w.wsmall = off; off = align256(off + 2 * kWSmall * 8);
+  w.wtab = off; off = align256(off + wtab_capacity(n) * sizeof(WSlot));
+  w.total = off;
+  return w;
+}
+
+struct PT {
+  int64_t n, P;
+  uint64_t cap;  // weight-table slots
+  int do_parts;
+};
+
+// weight w of histogram h's value v: dense LDS sums below kWSmall, else the
+// table (plain load first, CAS only on an empty slot, linear probing)
+__device__ __forceinline__ void weight_add(double* lw, WSlot* tab, uint64_t cap, int h, uint64_t v, double w) {
+  if (v < (uint64_t)kWSmall) {
+    atomicAdd(lw + h * kWSmall + (int)v, w);
+    return;
+  }
+  const unsigned long long x = v * 2 + (uint64_t)h + 1;
+  uint64_t s = __umul64hi(mix64(x), cap);
+  for (;;) {
+    unsigned long long* k = &tab[s].key;
+    const unsigned long long cur = *k;
+    if (cur == 0) {
+      const unsigned long long old = atomicCAS(k, 0ULL, x);
+      if (old == 0 || old == x) break;
+    } else if (cur == x) {
+      break;
+    }
+    s = s + 1 == cap ? 0 : s + 1;  // cap >= 2 * rows > distinct values: a free slot always exists
+  }
+  atomicAdd(&tab[s].w, w);
+}
+
+__global__ void __launch_bounds__(kBlock) k_hp_rows(PT t, const int64_t* __restrict__ pk,
+                                                    const int64_t* __restrict__ count,
+                                                    const double* __restrict__ sum,
+                                                    const int64_t* __restrict__ npart,
+                                                    const int64_t* __restrict__ ncontr, unsigned long long* pkrows,
+                                                    unsigned long long* pkcount, double* psum, IntHists H,
+                                                    unsigned long long* minmax, double* wsmall, WSlot* wtab,
+                                                    unsigned* err) {
+  __shared__ unsigned lcnt[kSmallBins];
+  __shared__ double lw[2 * kWSmall];
+  for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) lcnt[b] = 0;
+  for (int b = threadIdx.x; b < 2 * kWSmall; b += blockDim.x) lw[b] = 0.0;
+  __syncthreads();
+  constexpr int64_t kMaxV = (int64_t)1 << 62;
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
+    const int64_t p = pk[i], c = count[i], np = npart[i], nc = ncontr[i];
+    if (p < 0 || p >= t.P) {
+      atomicOr(err, 1u);
+      continue;
+    }
+    if (c < 1 || np < 1 || nc < 1 || c >= kMaxV || np >= kMaxV || nc >= kMaxV) {
+      atomicOr(err, 2u);
+      continue;
+    }
+    const double s = sum[i];
+    int_hist_add(H, lcnt, H_LINF, 0, (unsigned long long)c);
+    atomicAdd(pkrows + p, 1ULL);
+    atomicAdd(pkcount + p, (unsigned long long)c);
+    atomicAdd(psum + p, s);
+    const unsigned long long o = ord(s);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+    const double w = __ddiv_rn(1.0, (double)np);  // 1.0 / x[2] (:536-541, :560-565)
+    weight_add(lw, wtab, t.cap, H_L0, (uint64_t)np, w);
+    weight_add(lw, wtab, t.cap, H_L1, (uint64_t)nc, w);
+  }
+  block_minmax(mn, mx, minmax);  // contains __syncthreads: every thread reaches it
+  __syncthreads();
+  flush_small(H, lcnt, 0, H_LINF);
+  for (int b = threadIdx.x; b < 2 * kWSmall; b += blockDim.x)
+    if (lw[b] != 0.0) atomicAdd(wsmall + b, lw[b]);
+}
+
+// int(round(sum of weights)) per distinct value (:94-97), into its bin
+__global__ void __launch_bounds__(kBlock) k_hp_weights(const double* __restrict__ wsmall,
+                                                       const WSlot* __restrict__ wtab, uint64_t cap, IntHists H) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 2 * kWSmall) {
+    const double w = wsmall[i];
+    if (w > 0.0) {  // weights are positive: the value occurs
+      const int h = (int)(i / kWSmall);
+      const unsigned long long v = (unsigned long long)(i % kWSmall);
+      const unsigned long long f = (unsigned long long)rint(w);
+      const int64_t g = (int64_t)h * kLogBins + (int64_t)v;  // width-1 bin: this value alone
+      H.count[g] = f;
+      H.sum[g] = f * v;
+      H.max[g] = v;
+    }
+    return;
+  }
+  const int64_t j = i - 2 * kWSmall;
+  if (j >= (int64_t)cap) return;
+  const WSlot s = wtab[j];
+  if (s.key == 0) return;
+  const unsigned long long x = s.key - 1;
+  const int h = (int)(x & 1);
+  const unsigned long long v = x >> 1;
+  const unsigned long long f = (unsigned long long)rint(s.w);
+  const int64_t g = (int64_t)h * kLogBins + log_bin_index(v);
+  if (f) {
+    atomicAdd(H.count + g, f);
+    atomicAdd(H.sum + g, f * v);
+  }
+  atomicMax(H.max + g, v);
+}
+
+// per partition with rows: COUNT_PER_PARTITION (sum of counts),
+// PRIVACY_ID_PER_PARTITION (rows), min / max of the partition sums
+__global__ void __launch_bounds__(kBlock) k_hp_ids(PT t, const unsigned long long* __restrict__ pkrows,
+                                                   const unsigned long long* __restrict__ pkcount,
+                                                   const double* __restrict__ psum, IntHists H,
+                                                   unsigned long long* minmax) {
+  __shared__ unsigned lds[2 * kSmallBins];
+  for (int b = threadIdx.x; b < 2 * kSmallBins; b += blockDim.x) lds[b] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
+    const unsigned long long r = pkrows[i];
+    if (r == 0) continue;
+    int_hist_add(H, lds, H_COUNT, 0, pkcount[i]);
+    int_hist_add(H, lds, H_PIDS, 1, r);
+    const unsigned long long o = ord(psum[i]);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+  }
+  block_minmax(mn, mx, minmax + 2);
+  __syncthreads();
+  flush_small(H, lds, 0, H_COUNT);
+  flush_small(H, lds, 1, H_PIDS);
+}
+
+// Linf-sum histogram over the rows' sums (LDS-privatised counts and sums),
+// sum-per-partition histogram over the partitions with rows
+__global__ void __launch_bounds__(kFloatBlock) k_hp_float(PT t, const double* __restrict__ sum,
+                                                          const unsigned long long* __restrict__ pkrows,
+                                                          const double* __restrict__ psum,
+                                                          const double* __restrict__ lowers,
+                                                          const int* __restrict__ n_lowers, FloatHists F) {
+  __shared__ unsigned lcnt[kSumBuckets];
+  __shared__ double lsum[kSumBuckets];
+  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
+    lcnt[b] = 0;
+    lsum[b] = 0.0;
+  }
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
+  if (nl0 > 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.n; i += stride) {
+      const double v = sum[i];
+      const int b = float_bin(lowers, nl0, v);
+      atomicAdd(lcnt + b, 1u);
+      atomicAdd(lsum + b, v);
+      max_filtered(F.omax + b, ord(v));
+    }
+  }
+  if (t.do_parts && nl1 > 0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
+      if (pkrows[i] == 0) continue;
+      const double v = psum[i];
+      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + float_bin(lowers + kNLowers, nl1, v);
+      atomicAdd(F.count + g, 1ULL);
+      atomicAdd(F.sum + g, v);
+      max_filtered(F.omax + g, ord(v));
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
+    const unsigned c = lcnt[b];
+    if (c) {
+      atomicAdd(F.count + b, (unsigned long long)c);
+      atomicAdd(F.sum + b, lsum[b]);
+    }
+  }
 }
 
 #define PDP_HLAUNCH(name, st, ...)          \
@@ -632,7 +858,7 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, (const Slot*)(ws + w.slots),
               pkstat, psum, out->float_lowers, out->float_n_lowers, c.F);
   PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
-              c.F, out->float_max);
+              c.F, out->float_max, 0x1F);
   return PDP_OK;
 }
 
@@ -684,6 +910,160 @@ int pdp_dataset_histograms_finish(int32_t value_kind, int64_t n_rows, int64_t n_
   if (rc != PDP_OK) return rc;
   c.t.do_parts = partition_histograms != 0;
   return pdp::hist_finish(c, out);
+}
+
+}  // extern "C"
+
+namespace pdp {
+namespace {
+
+struct PCall {
+  PWs w;
+  PT t;
+  char* ws;
+  hipStream_t st;
+  IntHists H;
+  FloatHists F;
+};
+
+int pre_check(int64_t n_rows, int64_t n_partitions, const pdp_histogram_bins* out, void* workspace,
+              uint64_t workspace_bytes, void* stream, PCall* c) {
+  if (out == nullptr || out->int_count == nullptr || out->int_sum == nullptr || out->int_max == nullptr ||
+      out->float_count == nullptr || out->float_sum == nullptr || out->float_max == nullptr ||
+      out->float_lowers == nullptr || out->float_n_lowers == nullptr)
+    return set_error(PDP_E_INVALID, "every pdp_histogram_bins output must be set");
+  if (n_rows < 0 || n_partitions < 0) return set_error(PDP_E_INVALID, "sizes must be >= 0");
+  if (n_rows >= (int64_t)1 << 31) return set_error(PDP_E_UNSUPPORTED, "n_rows must be < 2^31 per shard");
+  c->w = playout(n_rows, n_partitions);
+  if (workspace == nullptr || workspace_bytes < c->w.total)
+    return set_error(PDP_E_INVALID, "workspace smaller than pdp_dataset_histograms_preaggregated_workspace_bytes");
+  c->ws = (char*)workspace;
+  c->st = (hipStream_t)stream;
+  c->t = PT{n_rows, n_partitions, wtab_capacity(n_rows), 1};
+  c->H = IntHists{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
+                  (unsigned long long*)out->int_max};
+  c->F = FloatHists{(unsigned long long*)out->float_count, out->float_sum, (unsigned long long*)(c->ws + c->w.fmax)};
+  return PDP_OK;
+}
+
+// zero everything; k_hp_rows (Linf histogram, per-partition statistics,
+// row-sum min / max, L0 / L1 weight sums)
+int pre_rows(const PCall& c, const int64_t* partition, const int64_t* count, const double* sum,
+             const int64_t* n_partitions_of_pid, const int64_t* n_contributions_of_pid,
+             const pdp_histogram_bins* out) {
+  const PWs& w = c.w;
+  const PT& t = c.t;
+  char* ws = c.ws;
+  hipStream_t st = c.st;
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.err, 0, 16, st));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.pkrows, 0, w.minmax - w.pkrows, st));  // pkrows .. psum
+  PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.fmax, 0, w.total - w.fmax, st));  // fmax, weight sums, weight table
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_sum, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->int_max, 0, 5 * kLogBins * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_count, 0, 2 * kSumBuckets * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_sum, 0, 2 * kSumBuckets * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(out->float_lowers, 0, 2 * kNLowers * 8, st));
+  if (t.n == 0) return PDP_OK;
+  if (partition == nullptr || count == nullptr || sum == nullptr || n_partitions_of_pid == nullptr ||
+      n_contributions_of_pid == nullptr)
+    return set_error(PDP_E_INVALID, "NULL column");
+  PDP_HLAUNCH("k_hp_rows", st, k_hp_rows, dim3(grid_for(t.n, 2048)), dim3(kBlock), 0, st, t, partition, count, sum,
+              n_partitions_of_pid, n_contributions_of_pid, (unsigned long long*)(ws + w.pkrows),
+              (unsigned long long*)(ws + w.pkcount), (double*)(ws + w.psum), c.H,
+              (unsigned long long*)(ws + w.minmax), (double*)(ws + w.wsmall), (WSlot*)(ws + w.wtab),
+              (unsigned*)(ws + w.err));
+  return PDP_OK;
+}
+
+// weighted L0 / L1 bins, partition histograms (t.do_parts), lowers, float bins
+int pre_finish(const PCall& c, const double* sum, const pdp_histogram_bins* out) {
+  const PWs& w = c.w;
+  const PT& t = c.t;
+  char* ws = c.ws;
+  hipStream_t st = c.st;
+  unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
+  const unsigned long long* pkrows = (const unsigned long long*)(ws + w.pkrows);
+  const double* psum = (const double*)(ws + w.psum);
+  const int64_t nw = 2 * kWSmall + (int64_t)t.cap;
+  PDP_HLAUNCH("k_hp_weights", st, k_hp_weights, dim3((unsigned)((nw + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+              (const double*)(ws + w.wsmall), (const WSlot*)(ws + w.wtab), t.cap, c.H);
+  if (t.do_parts && t.P > 0)
+    PDP_HLAUNCH("k_hp_ids", st, k_hp_ids, dim3(grid_for(t.P, 2048)), dim3(kBlock), 0, st, t, pkrows,
+                (const unsigned long long*)(ws + w.pkcount), psum, c.H, minmax);
+  PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
+              out->float_lowers, out->float_n_lowers);
+  int dev = 0, cus = 256;
+  PDP_HIP_CHECK(hipGetDevice(&dev));
+  PDP_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const int64_t mf = t.n > t.P ? t.n : t.P;
+  int64_t gf = (mf + kFloatBlock - 1) / kFloatBlock;
+  gf = gf < 1 ? 1 : (gf < cus ? gf : cus);
+  if (t.n > 0 && sum == nullptr) return set_error(PDP_E_INVALID, "NULL column");
+  PDP_HLAUNCH("k_hp_float", st, k_hp_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, sum,
+              pkrows, psum, out->float_lowers, out->float_n_lowers, c.F);
+  PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
+              c.F, out->float_max, (1 << H_LINF) | (1 << H_COUNT) | (1 << H_PIDS));
+  return PDP_OK;
+}
+
+}  // namespace
+}  // namespace pdp
+
+extern "C" {
+
+int pdp_dataset_histograms_preaggregated_workspace_bytes(int64_t n_rows, int64_t n_partitions, uint64_t* bytes) {
+  if (bytes == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (n_rows < 0 || n_partitions < 0) return pdp::set_error(PDP_E_INVALID, "sizes must be >= 0");
+  *bytes = pdp::playout(n_rows, n_partitions).total;
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms_preaggregated_rows(const int64_t* partition, const int64_t* count, const double* sum,
+                                              const int64_t* n_partitions_of_pid,
+                                              const int64_t* n_contributions_of_pid, int64_t n_rows,
+                                              int64_t n_partitions, const pdp_histogram_bins* out, void* workspace,
+                                              uint64_t workspace_bytes, void* stream) {
+  pdp::PCall c;
+  const int rc = pdp::pre_check(n_rows, n_partitions, out, workspace, workspace_bytes, stream, &c);
+  return rc == PDP_OK ? pdp::pre_rows(c, partition, count, sum, n_partitions_of_pid, n_contributions_of_pid, out)
+                      : rc;
+}
+
+int pdp_dataset_histograms_preaggregated_exchange_offsets(int64_t n_rows, int64_t n_partitions, uint64_t* pk_rows,
+                                                          uint64_t* pk_count, uint64_t* psum, uint64_t* minmax) {
+  if (pk_rows == nullptr || pk_count == nullptr || psum == nullptr || minmax == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (n_rows < 0 || n_partitions < 0) return pdp::set_error(PDP_E_INVALID, "sizes must be >= 0");
+  const pdp::PWs w = pdp::playout(n_rows, n_partitions);
+  *pk_rows = w.pkrows;
+  *pk_count = w.pkcount;
+  *psum = w.psum;
+  *minmax = w.minmax;
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms_preaggregated_finish(const double* sum, int64_t n_rows, int64_t n_partitions,
+                                                int32_t partition_histograms, const pdp_histogram_bins* out,
+                                                void* workspace,
+                                                uint64_t workspace_bytes, void* stream) {
+  pdp::PCall c;
+  const int rc = pdp::pre_check(n_rows, n_partitions, out, workspace, workspace_bytes, stream, &c);
+  if (rc != PDP_OK) return rc;
+  c.t.do_parts = partition_histograms != 0;
+  return pdp::pre_finish(c, sum, out);
+}
+
+int pdp_dataset_histograms_preaggregated(const int64_t* partition, const int64_t* count, const double* sum,
+                                         const int64_t* n_partitions_of_pid, const int64_t* n_contributions_of_pid,
+                                         int64_t n_rows, int64_t n_partitions, const pdp_histogram_bins* out,
+                                         void* workspace, uint64_t workspace_bytes, void* stream) {
+  pdp::PCall c;
+  int rc = pdp::pre_check(n_rows, n_partitions, out, workspace, workspace_bytes, stream, &c);
+  if (rc == PDP_OK) rc = pdp::pre_rows(c, partition, count, sum, n_partitions_of_pid, n_contributions_of_pid, out);
+  if (rc == PDP_OK) rc = pdp::pre_finish(c, sum, out);
+  return rc;
 }
 
 }  // extern "C"

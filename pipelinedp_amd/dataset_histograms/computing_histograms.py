@@ -39,14 +39,16 @@ def log_bin_bounds(index: int):
 
 
 def histograms_from_device(raw: Dict) -> hist.DatasetHistograms:
-    """Device bin arrays of executor.dataset_histograms -> DatasetHistograms
-    (bins sorted by lower, empty bins absent, :176-195)."""
+    """Device bin arrays of executor.dataset_histograms(_preaggregated) ->
+    DatasetHistograms (bins sorted by lower, empty bins absent, :176-195)."""
     host = {k: v.cpu().numpy() for k, v in raw.items() if k != "workspace"}
     built = {}
     for h, name in enumerate(_INT_TYPES):
         cnt = host["int_count"][h]
         bins = []
-        for b in np.flatnonzero(cnt).tolist():
+        # present bins: a count, or (pre-aggregated L0 / L1) a value whose
+        # rounded weight is 0, which the reference keeps as a count-0 bin
+        for b in np.flatnonzero((cnt > 0) | (host["int_max"][h] > 0)).tolist():
             lo, up = log_bin_bounds(b)
             bins.append(hist.FrequencyBin(lower=lo, upper=up, count=int(cnt[b]), sum=int(host["int_sum"][h, b]),
                                           max=int(host["int_max"][h, b])))
@@ -125,5 +127,66 @@ def compute_dataset_histograms(col, data_extractors, backend=None) -> List[hist.
             "pdp_bound_error_flags")
     if flags.value & 1:
         raise ValueError("privacy id or partition code outside the declared range")
+    return [histograms_from_device(raw)]
+
+
+def _preaggregated_columns(col, data_extractors):
+    """(pk, count, sum, n_partitions, n_contributions) raw columns: whole
+    ColumnTable columns when the extractors name columns, else one extractor
+    call per row (:729-733)."""
+    if isinstance(col, C.ColumnTable):
+        try:
+            probe = C._ProbeRow()
+            pk = data_extractors.partition_extractor(probe)
+            pre = tuple(data_extractors.preaggregate_extractor(probe))
+        except Exception:
+            pk, pre = None, ()
+        refs = (pk,) + pre
+        if len(refs) == 5 and all(isinstance(r, C.ColumnRef) and col.has_column(r.name) for r in refs):
+            return tuple(col.column(r.name) for r in refs) + (col.n_partitions,)
+    pks, cnt, tot, npart, ncontr = [], [], [], [], []
+    for row in col:
+        pks.append(data_extractors.partition_extractor(row))
+        c, t, npp, nc = data_extractors.preaggregate_extractor(row)[:4]
+        cnt.append(c)
+        tot.append(t)
+        npart.append(npp)
+        ncontr.append(nc)
+    return (pks, np.asarray(cnt, dtype=np.int64), np.asarray(tot, dtype=np.float64),
+            np.asarray(npart, dtype=np.int64), np.asarray(ncontr, dtype=np.int64), None)
+
+
+def compute_dataset_histograms_on_preaggregated_data(col, data_extractors,
+                                                     backend=None) -> List[hist.DatasetHistograms]:
+    """Computes the dataset histograms of a pre-aggregated dataset
+    (computing_histograms.py:713-758): `col` holds one row per (privacy id,
+    partition) pair, from which data_extractors (PreAggregateExtractors) give
+    the partition key and (count, sum, n_partitions, n_contributions), as
+    analysis/pre_aggregation.py:19-58 emits them.  L0 / L1 weigh each row by
+    1 / n_partitions and round the weight sum per value (:520-568); the other
+    five histograms are those of compute_dataset_histograms.  Returns a
+    one-element list holding a DatasetHistograms.  Under torch.distributed
+    each rank passes its shard (the rows of one privacy id on one rank) and
+    every rank gets the histograms of the whole dataset.  count,
+    n_partitions and n_contributions must be >= 1 (ValueError otherwise)."""
+    from pipelinedp_amd import executor as X
+    from pipelinedp_amd.columnar_backend import _h2d, _host_or_device
+    import torch
+    device = _device(backend)
+    pk_raw, cnt, tot, npart, ncontr, n_pk = _preaggregated_columns(col, data_extractors)
+    pk_enc = C.encode_keys(_host_or_device(pk_raw), n_pk)
+    from pipelinedp_amd import parallel
+    if parallel.world_info()[0] > 1:
+        pk_enc = parallel.global_partition_keys(pk_enc)
+    t = [_h2d(c, device, dt) for c, dt in ((pk_enc.codes, torch.int64), (cnt, torch.int64),
+                                           (tot, torch.float64), (npart, torch.int64), (ncontr, torch.int64))]
+    raw = X.dataset_histograms_preaggregated(*t, n_partitions=pk_enc.n)
+    flags = ctypes.c_uint32()
+    N.check(N.lib().pdp_bound_error_flags(X._ptr(raw["workspace"]), ctypes.byref(flags), X._stream()),
+            "pdp_bound_error_flags")
+    if flags.value & 1:
+        raise ValueError("partition code outside the declared range")
+    if flags.value & 2:
+        raise ValueError("pre-aggregated count, n_partitions and n_contributions must be in [1, 2^62)")
     return [histograms_from_device(raw)]
 

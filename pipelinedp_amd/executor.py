@@ -422,18 +422,7 @@ def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                                                       ctypes.byref(nbytes)),
             "pdp_dataset_histograms_workspace_bytes")
     ws = (workspace or BoundWorkspace()).get(nbytes.value, device)
-    i64 = dict(dtype=torch.int64, device=device)
-    f64 = dict(dtype=torch.float64, device=device)
-    out = {
-        "int_count": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
-        "int_sum": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
-        "int_max": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
-        "float_count": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **i64),
-        "float_sum": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
-        "float_max": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
-        "float_lowers": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS + 1), **f64),
-        "float_n_lowers": torch.empty(N.HIST_N_FLOAT, dtype=torch.int32, device=device),
-    }
+    out = _histogram_outputs(device)
     s = N.HistogramBins(**{k: _ptr(v) for k, v in out.items()})
     from pipelinedp_amd import parallel
     world, rank = parallel.world_info(group)
@@ -466,3 +455,77 @@ def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         parallel.merge_histogram_bins(out, group)
     out["workspace"] = ws
     return out
+
+
+def _histogram_outputs(device):
+    torch = _torch()
+    i64 = dict(dtype=torch.int64, device=device)
+    f64 = dict(dtype=torch.float64, device=device)
+    return {
+        "int_count": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "int_sum": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "int_max": torch.empty((N.HIST_N_INT, N.HIST_LOG_BINS), **i64),
+        "float_count": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **i64),
+        "float_sum": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
+        "float_max": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS), **f64),
+        "float_lowers": torch.empty((N.HIST_N_FLOAT, N.HIST_SUM_BUCKETS + 1), **f64),
+        "float_n_lowers": torch.empty(N.HIST_N_FLOAT, dtype=torch.int32, device=device),
+    }
+
+
+def dataset_histograms_preaggregated(pk, count, total, n_partitions_of_pid, n_contributions_of_pid, *,
+                                     n_partitions: int, stream=None,
+                                     workspace: Optional[BoundWorkspace] = None,
+                                     group=None) -> Dict[str, "torch.Tensor"]:
+    """compute_dataset_histograms_on_preaggregated_data (computing_histograms.py:
+    713-758) on device columns, one row per (privacy id, partition) pair
+    (`pdp_dataset_histograms_preaggregated`): pk (dense codes), count (rows of
+    the pair), total (their value sum, fp64), and the pair's privacy id's
+    n_partitions / n_contributions.  Returns the raw device bin arrays of
+    `dataset_histograms`.  Under torch.distributed (the rows of one privacy id
+    on one rank, partition codes global) every rank returns the merged bins."""
+    torch = _torch()
+    lib = N.lib()
+    if not pk.is_cuda:
+        raise ValueError("columns must be device tensors")
+    device = pk.device
+    n = int(pk.numel())
+    _check_col(pk, "partition", (torch.int64,), n, device)
+    _check_col(count, "count", (torch.int64,), n, device)
+    _check_col(total, "sum", (torch.float64,), n, device)
+    _check_col(n_partitions_of_pid, "n_partitions", (torch.int64,), n, device)
+    _check_col(n_contributions_of_pid, "n_contributions", (torch.int64,), n, device)
+    nbytes = ctypes.c_uint64()
+    N.check(lib.pdp_dataset_histograms_preaggregated_workspace_bytes(n, int(n_partitions), ctypes.byref(nbytes)),
+            "pdp_dataset_histograms_preaggregated_workspace_bytes")
+    ws = (workspace or BoundWorkspace()).get(nbytes.value, device)
+    out = _histogram_outputs(device)
+    s = N.HistogramBins(**{k: _ptr(v) for k, v in out.items()})
+    cols = (_ptr(pk), _ptr(count), _ptr(total), _ptr(n_partitions_of_pid), _ptr(n_contributions_of_pid))
+    from pipelinedp_amd import parallel
+    world, rank = parallel.world_info(group)
+    P = int(n_partitions)
+    if world == 1:
+        N.check(lib.pdp_dataset_histograms_preaggregated(*cols, n, P, ctypes.byref(s), _ptr(ws), int(ws.numel()),
+                                                         _stream(stream)),
+                "pdp_dataset_histograms_preaggregated")
+    else:
+        N.check(lib.pdp_dataset_histograms_preaggregated_rows(*cols, n, P, ctypes.byref(s), _ptr(ws),
+                                                              int(ws.numel()), _stream(stream)),
+                "pdp_dataset_histograms_preaggregated_rows")
+        offs = [ctypes.c_uint64() for _ in range(4)]
+        N.check(lib.pdp_dataset_histograms_preaggregated_exchange_offsets(n, P, *[ctypes.byref(o) for o in offs]),
+                "pdp_dataset_histograms_preaggregated_exchange_offsets")
+        pk_rows = ws[offs[0].value:offs[0].value + 8 * P].view(torch.int64)
+        pk_count = ws[offs[1].value:offs[1].value + 8 * P].view(torch.int64)
+        psum = ws[offs[2].value:offs[2].value + 8 * P].view(torch.float64)
+        minmax = ws[offs[3].value:offs[3].value + 16].view(torch.int64)
+        parallel.exchange_preaggregated_stats(pk_rows, pk_count, psum, minmax, group)
+        N.check(lib.pdp_dataset_histograms_preaggregated_finish(_ptr(total), n, P, 1 if rank == 0 else 0,
+                                                                ctypes.byref(s), _ptr(ws), int(ws.numel()),
+                                                                _stream(stream)),
+                "pdp_dataset_histograms_preaggregated_finish")
+        parallel.merge_histogram_bins(out, group)
+    out["workspace"] = ws
+    return out
+

@@ -173,6 +173,22 @@ def exchange_histogram_stats(pkstat, psum, minmax, group=None):
     minmax[1:2] = hi ^ _SIGN
 
 
+def exchange_preaggregated_stats(pk_rows, pk_count, psum, minmax, group=None):
+    """Between pdp_dataset_histograms_preaggregated_rows and _finish: sums the
+    per-partition row counts, count sums and value sums over ranks and takes
+    the global minimum / maximum of the row sums (order-preserving words, as
+    in exchange_histogram_stats)."""
+    import torch.distributed as dist
+    for t in (pk_rows, pk_count, psum):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    signed = minmax ^ _SIGN
+    lo, hi = signed[0:1].clone(), signed[1:2].clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    minmax[0:1] = lo ^ _SIGN
+    minmax[1:2] = hi ^ _SIGN
+
+
 def merge_histogram_bins(out, group=None):
     """Merges the bin arrays of pdp_dataset_histograms_finish over ranks:
     counts and sums added, maxima by maximum over the bins that hold

@@ -9,14 +9,48 @@ import numpy as np
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "histograms")
 
 
-def fixtures():
+def _load(pattern, prefix):
     out = []
-    for path in sorted(glob.glob(os.path.join(GOLDEN, "*.json"))):
+    for path in sorted(glob.glob(os.path.join(GOLDEN, pattern))):
         with open(path) as f:
             d = json.load(f)
-        d["name"] = os.path.basename(path)[len("dataset_histograms_"):-len(".json")]
+        d["name"] = os.path.basename(path)[len(prefix):-len(".json")]
         out.append(d)
     return out
+
+
+def fixtures():
+    """raw-row cases: rows (pid, pk, value)"""
+    return [d for d in _load("dataset_histograms_*.json", "dataset_histograms_") if not d["name"].startswith("pre_")]
+
+
+def pre_fixtures():
+    """pre-aggregated cases: rows (pk, count, sum, n_partitions, n_contributions)"""
+    return _load("dataset_histograms_pre_*.json", "dataset_histograms_pre_")
+
+
+def pre_columns(rows):
+    """dense pk codes + the four pre-aggregated columns"""
+    pk = np.unique([str(r[0]) for r in rows], return_inverse=True)[1].astype(np.int64)
+    a = np.asarray([r[1:] for r in rows], dtype=np.float64).reshape(-1, 4)
+    return (pk, a[:, 0].astype(np.int64), a[:, 1], a[:, 2].astype(np.int64), a[:, 3].astype(np.int64))
+
+
+def preaggregate(pid, pk, val):
+    """(pk, count, sum, n_partitions, n_contributions) per (pid, pk) pair of
+    raw dense-code columns (what analysis/pre_aggregation.py:19-58 emits)"""
+    pid = np.asarray(pid, dtype=np.int64)
+    pk = np.asarray(pk, dtype=np.int64)
+    val = np.asarray(val, dtype=np.float64)
+    pairs, inv = np.unique(np.stack([pid, pk], 1), axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    cnt = np.bincount(inv)
+    tot = np.bincount(inv, weights=val)
+    upid, pid_inv = np.unique(pairs[:, 0], return_inverse=True)
+    n_part = np.bincount(pid_inv.reshape(-1))
+    rows_of_pid = np.bincount(np.searchsorted(upid, pid))
+    pi = pid_inv.reshape(-1)
+    return pairs[:, 1].copy(), cnt.astype(np.int64), tot, n_part[pi].astype(np.int64), rows_of_pid[pi].astype(np.int64)
 
 
 def codes(rows):

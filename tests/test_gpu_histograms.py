@@ -226,3 +226,124 @@ def test_many_partition_regions():
     val = np.round(rng.normal(0, 3, n) * 4) / 4
     got = _run_codes(pid, pk, val, U=5_000, P=70_000_000)
     _check_all(got, OH.dataset_histograms(pid, pk, val), "many_regions", exact=True)
+
+
+# ---------------------------------------------- pre-aggregated (:713-758) --
+def _run_pre(pk, cnt, tot, npart, ncontr, P=None):
+    import torch
+    d = _dev()
+    P = int(pk.max()) + 1 if P is None else P
+    cols = [torch.as_tensor(np.ascontiguousarray(c), device=d) for c in (pk, cnt, tot, npart, ncontr)]
+    raw = X.dataset_histograms_preaggregated(*cols, n_partitions=P)
+    return CH.histograms_from_device(raw)
+
+
+@pytest.mark.parametrize("fx", HU.pre_fixtures(), ids=lambda f: f["name"])
+def test_preaggregated_reference_golden_rows(fx):
+    """the reference's compute_dataset_histograms_on_preaggregated_data bins,
+    from rows (pk, (count, sum, n_partitions, n_contributions)) as
+    preaggregate() emits them, through PreAggregateExtractors"""
+    from pipelinedp_amd.data_extractors import PreAggregateExtractors
+    rows = [(r[0], tuple(r[1:])) for r in fx["rows"]]
+    ext = PreAggregateExtractors(partition_extractor=lambda r: r[0], preaggregate_extractor=lambda r: r[1])
+    (got,) = CH.compute_dataset_histograms_on_preaggregated_data(rows, ext)
+    for field, exp in fx["expected"].items():
+        h = getattr(got, field)
+        assert h.name.value == exp["name"]
+        HU.assert_bins_equal(h.bins, exp["bins"], f"pre_{fx['name']}/{field}",
+                             exact=fx["name"] not in ("strings", "weights"))
+
+
+def test_preaggregated_column_table():
+    from pipelinedp_amd.data_extractors import PreAggregateExtractors
+    fx = [f for f in HU.pre_fixtures() if f["name"] == "heavy"][0]
+    pk, cnt, tot, npart, ncontr = HU.pre_columns(fx["rows"])
+    t = ColumnTable({"pk": pk, "c": cnt, "s": tot, "np": npart, "nc": ncontr})
+    ext = PreAggregateExtractors(partition_extractor=ColumnExtractor("pk"),
+                                 preaggregate_extractor=lambda r: (r["c"], r["s"], r["np"], r["nc"]))
+    (got,) = CH.compute_dataset_histograms_on_preaggregated_data(t, ext)
+    for field, exp in fx["expected"].items():
+        HU.assert_bins_equal(getattr(got, field).bins, exp["bins"], field, exact=True)
+
+
+@pytest.mark.parametrize("case", ["uniform", "zipf_heavy", "big_values"])
+def test_preaggregated_against_oracle_and_raw(case):
+    """pre-aggregated columns of seeded raw data: the HIP bins equal the
+    oracle's, and equal the raw-data HIP histograms (the reference test's
+    premise, computing_histograms_test.py:820-875)"""
+    rng = np.random.default_rng({"uniform": 41, "zipf_heavy": 42, "big_values": 43}[case])
+    n = 300_000
+    if case == "zipf_heavy":
+        pid = np.minimum(rng.zipf(1.5, n) - 1, 9_999)   # pids with 10^3..10^5 rows: L1 above 1000
+        pk = np.minimum(rng.zipf(1.3, n) - 1, 19_999)
+    elif case == "big_values":
+        pid = rng.integers(0, 30, n)                    # ~10^4 rows and ~10^3 partitions per pid
+        pk = rng.integers(0, 2_500, n)
+    else:
+        pid = rng.integers(0, 40_000, n)
+        pk = rng.integers(0, 3_000, n)
+    val = np.round(rng.normal(1, 3, n) * 8) / 8
+    pre = HU.preaggregate(pid, pk, val)
+    got = _run_pre(*pre)
+    _check_all(got, OH.preaggregated_histograms(*pre), f"pre_{case}", exact=True)
+    raw = _run_codes(pid, pk, val)
+    for field in OH.HIST_FIELDS:
+        HU.assert_bins_equal(getattr(got, field).bins, HU.as_tuples(getattr(raw, field).bins), f"raw/{field}",
+                             exact=True)
+
+
+def test_preaggregated_invalid_rows_raise():
+    from pipelinedp_amd.data_extractors import PreAggregateExtractors
+    ext = PreAggregateExtractors(partition_extractor=lambda r: r[0], preaggregate_extractor=lambda r: r[1])
+    with pytest.raises(ValueError):
+        CH.compute_dataset_histograms_on_preaggregated_data([(0, (1, 1.0, 0, 1))], ext)  # n_partitions 0
+    with pytest.raises(ValueError):
+        CH.compute_dataset_histograms_on_preaggregated_data([(0, (0, 1.0, 1, 1))], ext)  # count 0
+
+
+def test_preaggregated_empty_input():
+    import torch
+    d = _dev()
+    e = torch.empty(0, dtype=torch.int64, device=d)
+    raw = X.dataset_histograms_preaggregated(e, e, torch.empty(0, dtype=torch.float64, device=d), e, e,
+                                             n_partitions=0)
+    got = CH.histograms_from_device(raw)
+    assert all(not getattr(got, f).bins for f in OH.HIST_FIELDS)
+
+
+def _pre_worker(rank, port, results):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        pid, pk, val = _two_rank_data()
+        pre = HU.preaggregate(pid, pk, val)
+        # shard the pre-aggregated rows by privacy id: rows of one pid on one rank
+        pairs_pid = np.unique(np.stack([pid, pk], 1), axis=0)[:, 0]
+        keep = pairs_pid % 2 == rank
+        h = _run_pre(*(c[keep] for c in pre), P=2000)
+        results[rank] = {f: [tuple(map(float, (b.lower, b.upper, b.count, b.sum, b.max)))
+                             for b in getattr(h, f).bins] for f in OH.HIST_FIELDS}
+    except Exception as e:
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_preaggregated_two_ranks_match_single_process():
+    import socket
+    import torch.multiprocessing as mp
+    pid, pk, val = _two_rank_data()
+    single = _run_pre(*HU.preaggregate(pid, pk, val), P=2000)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.spawn(_pre_worker, args=(port, results), nprocs=2, join=True)
+    res = dict(results)
+    assert all(isinstance(res[r], dict) for r in (0, 1)), res
+    for r in (0, 1):
+        for f in OH.HIST_FIELDS:
+            HU.assert_bins_equal(res[r][f], getattr(single, f).bins, f"rank{r}/{f}", exact=True)

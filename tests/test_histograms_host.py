@@ -108,3 +108,32 @@ def test_oracle_reference_test_known_answers(field, rows, expected):
     pid, pk, _ = HU.codes([(u, k, 0.0) for u, k in rows])
     got = OH.dataset_histograms(pid, pk, [0.0] * len(rows))[field]
     HU.assert_bins_equal(got, expected, field, exact=True)
+
+
+# ---------------------------------------------- pre-aggregated (:713-758) --
+@pytest.mark.parametrize("fx", HU.pre_fixtures(), ids=lambda f: f["name"])
+def test_preaggregated_oracle_matches_reference_golden(fx):
+    got = OH.preaggregated_histograms(*HU.pre_columns(fx["rows"]))
+    for field, exp in fx["expected"].items():
+        HU.assert_bins_equal(got[field], exp["bins"], f"pre_{fx['name']}/{field}")
+
+
+@pytest.mark.parametrize("fx", HU.fixtures(), ids=lambda f: f["name"])
+def test_preaggregated_equals_raw_histograms(fx):
+    """the reference test's premise (computing_histograms_test.py:820-875,
+    pre_aggregated=(False, True)): histograms of preaggregate(rows) equal
+    those of the rows, here through the oracle on both sides"""
+    pid, pk, val = HU.codes(fx["rows"])
+    got = OH.preaggregated_histograms(*HU.preaggregate(pid, pk, val))
+    for field, exp in fx["expected"].items():
+        HU.assert_bins_equal(got[field], exp["bins"], f"{fx['name']}/{field}")
+
+
+def test_preaggregated_weights_fixture_pins_rounding():
+    """the inconsistent fixture's L0 / L1: half-to-even rounding and a
+    count-0 bin that keeps its max"""
+    fx = [f for f in HU.pre_fixtures() if f["name"] == "weights"][0]
+    l0 = [tuple(b) for b in fx["expected"]["l0_contributions_histogram"]["bins"]]
+    assert (8, 9, 0, 0, 8) in l0 and (2, 3, 6, 12, 2) in l0
+    l1 = [tuple(b) for b in fx["expected"]["l1_contributions_histogram"]["bins"]]
+    assert (2500, 2510, 4, 10000, 2500) in l1

@@ -12,6 +12,9 @@ for so in build/variants/*.so; do
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
 r = json.loads(line)
-print(sys.argv[2], "ms/step %.3f" % r["ms_per_step"], {k: round(v, 3) for k, v in r["kernel_ms"].items() if v > 0.05})
+print(sys.argv[2], "C3 ms/step %.3f" % r["ms_per_step"], {k: round(v["ms"], 3) for k, v in r["kernels"].items() if v["ms"] > 0.05})
+s = r.get("secondary")
+if s:
+    print(sys.argv[2], "C2 ms/step %.3f" % s["ms_per_step"], {k: round(v["ms"], 3) for k, v in s["kernels"].items() if v["ms"] > 0.05})
 PY
 done
