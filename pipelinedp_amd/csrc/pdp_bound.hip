@@ -19,9 +19,11 @@
 //    that every partitioning pass writes to <= 64 destinations per workgroup
 //    (long coalesced runs; ~2000 direct destinations thrash L2 5x).
 //    k_part_hist       per-tile histogram of bucket = pid >> bucket_bits  (8 B/row)
-//    k_bucket_totals, k_scan_*   rows per bucket (column sums) -> bucket starts
-//    k_scatter_l1      rows -> super-bucket order (pair key u64, row u32)  (16 B in, 12 B out)
-//    k_scatter_l2      super-bucket chunks -> bucket order                 (12 B in, 12 B out)
+//    k_super_scan      per-tile write offsets of every super-bucket
+//    k_gscan_*, k_scan_*   rows per bucket -> bucket starts; level-2 write
+//                      cursors at every group of kL2GroupTiles tiles
+//    k_scatter_l1      rows -> super-bucket order, tile runs in tile order (16 B in, 8 B out)
+//    k_scatter_l2      per (tile group, super-bucket) -> bucket order, no atomics (8 B in, 8 B out)
 //    k_bucket_bound    one workgroup per bucket, all sampling state in LDS:
 //                      B1 bottom-l0 pair sketch per pid, B2 per-pair row count
 //                      + bottom-linf row sketch, B3 gather the sampled values
@@ -47,7 +49,27 @@ constexpr int kPartThreads = 512;
 constexpr int kL1Items = PDP_L1_ITEMS;
 constexpr int kL1Rows = kPartThreads * kL1Items;  // rows per level-1 LDS stage
 constexpr int kL2Items = PDP_L2_ITEMS;
-constexpr int kL2Rows = kPartThreads * kL2Items;  // records per level-2 window
+#ifndef PDP_L2_THREADS
+#define PDP_L2_THREADS 512
+#endif
+// level-2 occupancy attribute (A/B knob).  Two 8-wave workgroups per CU
+// need <= 128 VGPRs (MI355X_MICROARCH.md register table): the kernel as
+// written takes 121-123 with 16 records per thread; loading a stage ahead
+// (157 VGPRs, one workgroup per CU) cost 1 ms at C3
+#ifndef PDP_L2_OCC
+#define PDP_L2_OCC
+#endif
+constexpr int kL2Threads = PDP_L2_THREADS;
+constexpr int kL2Rows = kL2Threads * kL2Items;  // records per level-2 LDS stage
+// tiles per level-2 workgroup (k_scatter_l2, k_gscan_cursors)
+#ifndef PDP_L2_GROUP
+#define PDP_L2_GROUP 16
+#endif
+constexpr int kL2GroupTiles = PDP_L2_GROUP;
+constexpr int kScanWaves = 16;
+constexpr int kScanTiles = 16;  // tiles per wave in the level-2 cursor scans; multiple of kL2GroupTiles
+constexpr int kScanChunkTiles = kScanWaves * kScanTiles;
+static_assert(kScanTiles % kL2GroupTiles == 0, "group starts must fall inside a wave's tiles");
 constexpr int kTileRowBits = 16;
 constexpr int64_t kTileRows = (int64_t)1 << kTileRowBits;
 constexpr int kUnroll = 8;
@@ -217,8 +239,8 @@ struct Ws {
   // global path
   uint64_t sketch, cnt, rows, fsum, nsum, nsum2;
   // bucketed path
-  uint64_t counts_tm, counts, chunk_sums, cursor, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
-  uint64_t win_tile;  // PDP_KEYS_PACKED: first tile of every level-2 window
+  uint64_t counts_tm, counts, chunk_sums, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
+  uint64_t csum, gcur;  // level-2 cursor scans: per tile chunk, per tile group (x n_buckets)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -248,7 +270,10 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.counts_tm = off; off = align256(off + n_counts * 4);
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
-    w.cursor = off; off = align256(off + (uint64_t)p.n_buckets * 4);
+    const uint64_t n_sc = ((uint64_t)p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
+    const uint64_t n_grp = ((uint64_t)p.n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
+    w.csum = off; off = align256(off + n_sc * (uint64_t)p.n_buckets * 4);
+    w.gcur = off; off = align256(off + n_grp * (uint64_t)p.n_buckets * 4);
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
     w.super_tm = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
     w.super_off = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
@@ -263,10 +288,6 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     } else {
       w.keys2 = w.keys1;
       w.rows2 = w.rows1;
-    }
-    if (packed) {
-      const uint64_t n_win = (n + 4 * (uint64_t)p.n_supers) / kL2Rows + 2 * (uint64_t)p.n_supers + 1;
-      w.win_tile = off; off = align256(off + n_win * 4);
     }
     if (p.merge == PDP_MERGE_RANGES) {
       const uint64_t recs = (uint64_t)p.n_buckets * ((uint64_t)c->l0 << p.bucket_bits);
@@ -486,26 +507,84 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
 }
 
 
-// total[b] += sum over a chunk of tiles of counts_tm[t][b] (2-D grid: bucket
-// columns x tile chunks; integer atomics, so the result is exact)
-constexpr int kTotalsTiles = 32;
-__global__ void __launch_bounds__(kBlock) k_bucket_totals(const unsigned* __restrict__ counts_tm, int64_t n_tiles,
-                                                          int64_t n_buckets, unsigned* __restrict__ total) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n_buckets) return;
-  const int64_t t0 = (int64_t)blockIdx.y * kTotalsTiles;
-  const int64_t t1 = t0 + kTotalsTiles < n_tiles ? t0 + kTotalsTiles : n_tiles;
+// Level-2 cursors.  Level 2 runs one workgroup per (group of kL2GroupTiles
+// tiles, super-bucket): its records are the runs of those tiles in the
+// super-bucket's region, and the rows of bucket b from tiles < t start at
+// start[b] + sum over t' < t of counts_tm[t'][b].  These exclusive column
+// scans of the tile histogram, taken at group boundaries, are computed in
+// three passes over chunks of kScanWaves * kScanTiles tiles (one wave per
+// kScanTiles tiles, one lane per bucket): chunk sums, a scan over chunks
+// (which also gives the bucket totals), and the cursors at group starts.
+// Level 2 then needs no atomics and writes every bucket's rows in tile order.
+
+__device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ counts_tm, int64_t n_tiles,
+                                                  int64_t n_buckets, int64_t b, int64_t t0) {
   unsigned v = 0;
-  for (int64_t t = t0; t < t1; ++t) v += counts_tm[t * n_buckets + b];
-  if (v) atomicAdd(total + b, v);
+#pragma unroll
+  for (int j = 0; j < kScanTiles; ++j) {
+    const int64_t t = t0 + j;
+    if (t < n_tiles && b < n_buckets) v += counts_tm[t * n_buckets + b];
+  }
+  return v;
 }
 
-// cursor[b] = start of bucket b; super_base[B] = start of super-bucket B
-__global__ void __launch_bounds__(kBlock) k_init_cursors(KP kp, const unsigned* __restrict__ counts,
-                                                         unsigned* __restrict__ cursor,
-                                                         unsigned* __restrict__ super_base) {
+// csum[chunk][b] = rows of bucket b in the chunk's tiles
+__global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* __restrict__ counts_tm,
+                                                                 int64_t n_tiles, int64_t n_buckets,
+                                                                 unsigned* __restrict__ csum) {
+  __shared__ unsigned part[kScanWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
+  part[w][lane] = tile_slab_sum(counts_tm, n_tiles, n_buckets, b, t0);
+  __syncthreads();
+  if (w == 0 && b < n_buckets) {
+    unsigned v = 0;
+    for (int k = 0; k < kScanWaves; ++k) v += part[k][lane];
+    csum[(int64_t)blockIdx.y * n_buckets + b] = v;
+  }
+}
+
+// per bucket: exclusive scan of the chunk sums in place, total -> total[b]
+__global__ void __launch_bounds__(kBlock) k_gscan_chunks(unsigned* __restrict__ csum, int64_t n_chunks,
+                                                         int64_t n_buckets, unsigned* __restrict__ total) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n_buckets) return;
+  unsigned run = 0;
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const unsigned v = csum[c * n_buckets + b];
+    csum[c * n_buckets + b] = run;
+    run += v;
+  }
+  total[b] = run;
+}
+
+// gcur[g][b] = rows of bucket b in tiles < g * kL2GroupTiles
+__global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigned* __restrict__ counts_tm,
+                                                                    int64_t n_tiles, int64_t n_buckets,
+                                                                    const unsigned* __restrict__ cpre,
+                                                                    unsigned* __restrict__ gcur) {
+  __shared__ unsigned part[kScanWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
+  part[w][lane] = tile_slab_sum(counts_tm, n_tiles, n_buckets, b, t0);
+  __syncthreads();
+  if (b >= n_buckets || t0 >= n_tiles) return;
+  unsigned run = cpre[(int64_t)blockIdx.y * n_buckets + b];
+  for (int k = 0; k < w; ++k) run += part[k][lane];
+  for (int j = 0; j < kScanTiles; ++j) {
+    const int64_t t = t0 + j;
+    if (t >= n_tiles) break;
+    if (t % kL2GroupTiles == 0) gcur[(t / kL2GroupTiles) * n_buckets + b] = run;
+    run += counts_tm[t * n_buckets + b];
+  }
+}
+
+// super_base[B] = start of super-bucket B
+__global__ void __launch_bounds__(kBlock) k_super_bases(KP kp, const unsigned* __restrict__ counts,
+                                                        unsigned* __restrict__ super_base) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < kp.n_buckets) cursor[i] = counts[i];
   if (i <= kp.n_supers) {
     const int64_t b = i << kp.super_bits;
     super_base[i] = counts[b < kp.n_buckets ? b : kp.n_buckets];
@@ -531,21 +610,21 @@ using L2Key = RecKey<FMT != PDP_KEYS_WIDE>;
 // MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
 // fits four workgroups per CU with compact keys instead of three.  ROWS:
 // the stage carries a u32 row array beside the keys.
-template <typename K, int MAXD, bool ROWS, int N>
+template <typename K, int MAXD, bool ROWS, int N, int THREADS = kPartThreads>
 struct StageLds {
   using D = typename std::conditional<(MAXD <= 256), uint8_t, unsigned short>::type;
   unsigned hist[MAXD];
   unsigned start[MAXD];
   unsigned gcur[MAXD];
-  K keys[kPartThreads * N];
-  unsigned rows[ROWS ? kPartThreads * N : 1];
-  D dest[kPartThreads * N];
+  K keys[THREADS * N];
+  unsigned rows[ROWS ? THREADS * N : 1];
+  D dest[THREADS * N];
 };
 constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four workgroups per CU
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
-template <typename K, int MAXD, bool ROWS, int N>
-__device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N>& s, int ndest, const int (&d)[N],
+template <typename K, int MAXD, bool ROWS, int N, int TH>
+__device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N, TH>& s, int ndest, const int (&d)[N],
                                             unsigned (&rank)[N]) {
   for (int t = threadIdx.x; t < ndest; t += blockDim.x) s.hist[t] = 0;
   __syncthreads();
@@ -570,8 +649,8 @@ __device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N>& s, int n
 }
 
 // phase 2: place into the LDS stage, then write every run at gcur[dest]
-template <typename K, int MAXD, bool ROWS, int N>
-__device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS, N>& s, int ndest, const int (&d)[N],
+template <typename K, int MAXD, bool ROWS, int N, int TH>
+__device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS, N, TH>& s, int ndest, const int (&d)[N],
                                             const unsigned (&rank)[N], const K (&x)[N],
                                             const unsigned (&r)[N], K* __restrict__ out_keys,
                                             unsigned* __restrict__ out_rows) {
@@ -581,7 +660,7 @@ __device__ __forceinline__ void stage_write(StageLds<K, MAXD, ROWS, N>& s, int n
     const unsigned slot = s.start[d[q]] + rank[q];
     s.keys[slot] = x[q];
     if (ROWS) s.rows[slot] = r[q];
-    s.dest[slot] = (typename StageLds<K, MAXD, ROWS, N>::D)d[q];
+    s.dest[slot] = (typename StageLds<K, MAXD, ROWS, N, TH>::D)d[q];
   }
   __syncthreads();
   const unsigned total = s.start[ndest - 1] + s.hist[ndest - 1];
@@ -714,92 +793,20 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   }
 }
 
-// Level-2 windows: every super-bucket region is cut into 4096-record windows
-// aligned at its first R-aligned record; window g's (super-bucket, base,
-// valid range [r0, r1)).  The first wave locates it (n_supers <= 64).
-template <int R>
-__device__ __forceinline__ bool locate_window(const KP& kp, const unsigned* __restrict__ super_base, int64_t g,
-                                              int* s_B, int64_t* s_base, int64_t* s_r0, int64_t* s_r1) {
-  const int lane = threadIdx.x;
-  int64_t lo = 0, hi = 0, nch = 0;
-  if (lane < kp.n_supers) {
-    lo = super_base[lane];
-    hi = super_base[lane + 1];
-    nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kL2Rows - 1) / kL2Rows : 0;
-  }
-  int64_t inc = nch;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t y = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += y;
-  }
-  const bool mine = g >= inc - nch && g < inc;
-  const unsigned long long hit = __ballot(mine);
-  if (mine) {
-    const int64_t base = (lo & ~(int64_t)(R - 1)) + (g - (inc - nch)) * kL2Rows;
-    *s_B = lane;
-    *s_base = base;
-    *s_r0 = base > lo ? base : lo;
-    *s_r1 = base + kL2Rows < hi ? base + kL2Rows : hi;
-  }
-  return hit != 0;
-}
-
-// PDP_KEYS_PACKED: the tile holding the first record of every level-2 window.
-// One workgroup per super-bucket B walks the tiles' runs [super_off[t][B],
-// super_off[t + 1][B]) of its region; a window starting inside a run belongs
-// to that run's tile.  Windows are enumerated exactly as k_scatter_l2 does.
-__global__ void __launch_bounds__(kBlock) k_window_tiles(KP kp, const unsigned* __restrict__ super_base,
-                                                         const unsigned* __restrict__ super_off,
-                                                         unsigned* __restrict__ win_tile) {
-  constexpr int R = 2;  // u64 packed records per 16-byte load
-  __shared__ int64_t s_g0;
-  const int B = blockIdx.x;
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    int64_t nch = 0;
-    if (lane < kp.n_supers) {
-      const int64_t lo = super_base[lane], hi = super_base[lane + 1];
-      nch = hi > lo ? (hi - (lo & ~(int64_t)(R - 1)) + kL2Rows - 1) / kL2Rows : 0;
-    }
-    int64_t inc = nch;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int64_t y = __shfl_up(inc, off, 64);
-      if (lane >= off) inc += y;
-    }
-    if (lane == B) s_g0 = inc - nch;
-  }
-  __syncthreads();
-  const int64_t lo = super_base[B], hi = super_base[B + 1];
-  if (hi <= lo) return;
-  const int64_t rel0 = (lo & ~(int64_t)(R - 1)) - lo;  // window 0's base, relative (<= 0)
-  const int64_t total = hi - lo;
-  for (int64_t t = threadIdx.x; t < kp.n_tiles; t += blockDim.x) {
-    const int64_t a = super_off[t * kp.n_supers + B];
-    const int64_t b = t + 1 < kp.n_tiles ? (int64_t)super_off[(t + 1) * kp.n_supers + B] : total;
-    if (a >= b) continue;
-    int64_t k = a == 0 ? 0 : (a - rel0 + kL2Rows - 1) / kL2Rows;
-    for (;; ++k) {
-      int64_t st = rel0 + k * kL2Rows;
-      if (st < 0) st = 0;
-      if (st >= b) break;
-      if (st >= a) win_tile[s_g0 + k] = (unsigned)t;
-    }
-  }
-}
-
-// Level 2: one chunk of one super-bucket -> its 2^super_bits bucket regions.
-// PACKED input: the u64 packed records are unpacked into COMPACT (key, row)
-// pairs, the row = tile * 65,536 + tile row with the tile found from the
-// record's offset among the tiles' runs (LDS copy of super_off from the
-// window's first tile, k_window_tiles).
-constexpr int kWinTiles = 256;  // tiles' run starts held in LDS per window
+// Level 2: one workgroup per (group g of kL2GroupTiles tiles, super-bucket
+// B) moves the runs of those tiles in B's region -- in tile order, so one
+// contiguous range -- into B's 2^super_bits bucket regions, kL2Rows records
+// per LDS stage.  Every bucket's write cursor starts at start[b] + gcur[g][b]
+// (k_gscan_cursors) and advances in LDS: no atomics, each bucket's rows land
+// in tile order, and consecutive stages of a workgroup append to the same
+// runs (their partial cache lines meet in the same L2).  PACKED input: the
+// u64 packed records are unpacked into COMPACT (key, row) pairs, the row =
+// tile * 65,536 + tile row, the tile found among the group's run starts.
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
+__global__ void __launch_bounds__(kL2Threads) PDP_L2_OCC k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
                                                              const unsigned* __restrict__ super_off,
-                                                             const unsigned* __restrict__ win_tile,
-                                                             unsigned* __restrict__ cursor,
+                                                             const unsigned* __restrict__ bucket_start,
+                                                             const unsigned* __restrict__ gcur,
                                                              const L1Key<FMT>* __restrict__ keys1,
                                                              const unsigned* __restrict__ rows1,
                                                              L2Key<FMT>* __restrict__ keys2,
@@ -812,123 +819,97 @@ __global__ void __launch_bounds__(kPartThreads) k_scatter_l2(KP kp, const unsign
   constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
   constexpr int R = 16 / sizeof(KI);  // records per 16-byte key load
   extern __shared__ unsigned long long stage_raw[];
-  StageLds<KO, MAXD, true, kL2Items>& s = *reinterpret_cast<StageLds<KO, MAXD, true, kL2Items>*>(stage_raw);
-  __shared__ int s_B;
-  __shared__ int64_t s_base, s_r0, s_r1;
-  __shared__ unsigned toff[kWinTiles + 1];  // PACKED: run starts of tiles T0 .. T0 + J
-  __shared__ int s_J;
+  using SL = StageLds<KO, MAXD, true, kL2Items, kL2Threads>;
+  SL& s = *reinterpret_cast<SL*>(stage_raw);
+  __shared__ unsigned toff[kL2GroupTiles + 1];  // run starts of the group's tiles, relative to B's region
+  const int64_t g = blockIdx.x;
+  const int B = blockIdx.y;
+  const int64_t T0 = g * kL2GroupTiles;
+  const int J = (int)(kp.n_tiles - T0 < kL2GroupTiles ? kp.n_tiles - T0 : kL2GroupTiles);
+  const int64_t sb = super_base[B];
+  if (threadIdx.x <= J) {
+    const int64_t t = T0 + threadIdx.x;
+    toff[threadIdx.x] = t < kp.n_tiles ? super_off[t * kp.n_supers + B] : (unsigned)(super_base[B + 1] - sb);
+  }
   const int nsub = 1 << kp.super_bits;
-  if (threadIdx.x < 64) {
-    const bool found = locate_window<R>(kp, super_base, blockIdx.x, &s_B, &s_base, &s_r0, &s_r1);
-    if (threadIdx.x == 0 && !found) s_B = -1;  // grid is an upper bound on the window count
+  const int64_t s_first = (int64_t)B << kp.super_bits;
+  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+    const int64_t b = s_first + t;
+    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * kp.n_buckets + b] : 0u;
   }
   __syncthreads();
-  if (s_B < 0) return;
-  const int64_t base = s_base, r0 = s_r0, r1 = s_r1;
-  const int64_t s_first = (int64_t)s_B << kp.super_bits;
-  const int64_t lo = PACKED ? (int64_t)super_base[s_B] : 0;
-  int64_t T0 = 0;
-  if constexpr (PACKED) {
-    T0 = win_tile[blockIdx.x];
-    int64_t J = kp.n_tiles - T0;
-    if (J > kWinTiles) J = kWinTiles;
-    const int64_t total = (int64_t)super_base[s_B + 1] - lo;
-    for (int64_t j = threadIdx.x; j <= J; j += blockDim.x) {
-      const int64_t t = T0 + j;
-      toff[j] = t < kp.n_tiles ? super_off[t * kp.n_supers + s_B] : (unsigned)total;
-    }
-    if (threadIdx.x == 0) s_J = (int)J;
-    __syncthreads();
-  }
-  // tile of the record at relative offset o: the last run start <= o.  A
-  // thread's records come in increasing offsets, so after one binary search
-  // the LDS cursor only moves forward (about one tile per 1024 records).
-  int jcur = -1;
-  auto tile_of = [&](int64_t o) -> int64_t {
-    const int J = s_J;
-    if (o < (int64_t)toff[J]) {
-      if (jcur < 0) {
-        int a = 0, b = J - 1;
-        while (a < b) {
-          const int m = (a + b + 1) >> 1;
-          if ((int64_t)toff[m] <= o) a = m;
-          else b = m - 1;
-        }
-        jcur = a;
-      } else {
-        while (jcur + 1 < J && (int64_t)toff[jcur + 1] <= o) ++jcur;
-      }
-      return T0 + jcur;
-    }
-    int64_t a = T0 + J, b = kp.n_tiles - 1;  // beyond the LDS span (sparse region): global search
-    while (a < b) {
-      const int64_t m = (a + b + 1) >> 1;
-      if ((int64_t)super_off[m * kp.n_supers + s_B] <= o) a = m;
-      else b = m - 1;
-    }
-    return a;
-  };
+  const int64_t lo = sb + toff[0], hi = sb + toff[J];
+  if (lo >= hi) return;  // block-uniform
   const int bb = kp.bucket_bits;
   const uint32_t local_mask = (1u << bb) - 1;
+  // PACKED: tile of the record at absolute index i; a thread's records come
+  // in increasing order, so the cursor only moves forward
+  int jcur = 0;
+  auto tile_of = [&](int64_t i) -> int64_t {
+    const int64_t o = i - sb;
+    while (jcur + 1 < J && (int64_t)toff[jcur + 1] <= o) ++jcur;
+    return T0 + jcur;
+  };
   auto unpack = [&](uint64_t v, int64_t i, KO* key, unsigned* row, int* dest) {
     const uint32_t mid = (uint32_t)((v >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
     *dest = (int)(mid >> bb);
     const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
     *key = (KO)((v >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(v & kp.pk_mask)));
     const uint32_t trow = (uint32_t)((v >> kPackedRowShift) & (kTileRows - 1));
-    *row = (unsigned)(tile_of(i - lo) * kTileRows + trow);
+    *row = (unsigned)(tile_of(i) * kTileRows + trow);
   };
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
   const uint64_t sub_mask = (uint64_t)nsub - 1;
-  KO x[kL2Items];
-  unsigned r[kL2Items];
-  int d[kL2Items];
+  for (int64_t base = lo & ~(int64_t)(R - 1); base < hi; base += kL2Rows) {
+    const int64_t r0 = base > lo ? base : lo;
+    const int64_t r1 = base + kL2Rows < hi ? base + kL2Rows : hi;
+    KO x[kL2Items];
+    unsigned r[kL2Items];
+    int d[kL2Items];
 #pragma unroll
-  for (int q = 0; q < kL2Items; q += R) {  // R records per 16-byte key load
-    const int64_t i = base + R * ((int64_t)threadIdx.x + (int64_t)(q / R) * blockDim.x);
-    if (i >= r0 && i + R - 1 < r1) {
-      if constexpr (PACKED) {
-        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
-        unpack(a.x, i, &x[q], &r[q], &d[q]);
-        unpack(a.y, i + 1, &x[q + 1], &r[q + 1], &d[q + 1]);
-      } else if constexpr (R == 4) {
-        const uint4 a = *reinterpret_cast<const uint4*>(keys1 + i);
-        const uint4 c = *reinterpret_cast<const uint4*>(rows1 + i);
-        x[q] = a.x; x[q + 1] = a.y; x[q + 2] = a.z; x[q + 3] = a.w;
-        r[q] = c.x; r[q + 1] = c.y; r[q + 2] = c.z; r[q + 3] = c.w;
-      } else {
-        const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
-        const uint2 c = *reinterpret_cast<const uint2*>(rows1 + i);
-        x[q] = a.x; x[q + 1] = a.y;
-        r[q] = c.x; r[q + 1] = c.y;
-      }
-      if constexpr (!PACKED) {
-#pragma unroll
-        for (int e = 0; e < R; ++e) d[q + e] = (int)((x[q + e] >> sub_shift) & sub_mask);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < R; ++e) {
-        const bool ok = i + e >= r0 && i + e < r1;
+    for (int q = 0; q < kL2Items; q += R) {  // R records per 16-byte key load
+      const int64_t i = base + R * ((int64_t)threadIdx.x + (int64_t)(q / R) * blockDim.x);
+      if (i >= r0 && i + R - 1 < r1) {
         if constexpr (PACKED) {
-          if (ok) unpack(keys1[i + e], i + e, &x[q + e], &r[q + e], &d[q + e]);
-          else { x[q + e] = 0; r[q + e] = 0; d[q + e] = -1; }
+          const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
+          unpack(a.x, i, &x[q], &r[q], &d[q]);
+          unpack(a.y, i + 1, &x[q + 1], &r[q + 1], &d[q + 1]);
+        } else if constexpr (R == 4) {
+          const uint4 a = *reinterpret_cast<const uint4*>(keys1 + i);
+          const uint4 c = *reinterpret_cast<const uint4*>(rows1 + i);
+          x[q] = a.x; x[q + 1] = a.y; x[q + 2] = a.z; x[q + 3] = a.w;
+          r[q] = c.x; r[q + 1] = c.y; r[q + 2] = c.z; r[q + 3] = c.w;
         } else {
-          x[q + e] = ok ? keys1[i + e] : 0;
-          r[q + e] = ok ? rows1[i + e] : 0;
-          d[q + e] = ok ? (int)((x[q + e] >> sub_shift) & sub_mask) : -1;
+          const ulonglong2 a = *reinterpret_cast<const ulonglong2*>(keys1 + i);
+          const uint2 c = *reinterpret_cast<const uint2*>(rows1 + i);
+          x[q] = a.x; x[q + 1] = a.y;
+          r[q] = c.x; r[q + 1] = c.y;
+        }
+        if constexpr (!PACKED) {
+#pragma unroll
+          for (int e = 0; e < R; ++e) d[q + e] = (int)((x[q + e] >> sub_shift) & sub_mask);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < R; ++e) {
+          const bool ok = i + e >= r0 && i + e < r1;
+          if constexpr (PACKED) {
+            if (ok) unpack(keys1[i + e], i + e, &x[q + e], &r[q + e], &d[q + e]);
+            else { x[q + e] = 0; r[q + e] = 0; d[q + e] = -1; }
+          } else {
+            x[q + e] = ok ? keys1[i + e] : 0;
+            r[q + e] = ok ? rows1[i + e] : 0;
+            d[q + e] = ok ? (int)((x[q + e] >> sub_shift) & sub_mask) : -1;
+          }
         }
       }
     }
+    unsigned rank[kL2Items];
+    stage_count(s, nsub, d, rank);
+    stage_write(s, nsub, d, rank, x, r, keys2, rows2);
+    for (int t = threadIdx.x; t < nsub; t += blockDim.x) s.gcur[t] += s.hist[t];
+    __syncthreads();
   }
-  unsigned rank[kL2Items];
-  stage_count(s, nsub, d, rank);
-  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
-    const int64_t b = s_first + t;
-    s.gcur[t] = (s.hist[t] && b < kp.n_buckets) ? atomicAdd(cursor + b, s.hist[t]) : 0;
-  }
-  __syncthreads();
-  stage_write(s, nsub, d, rank, x, r, keys2, rows2);
 }
 
 // exclusive block-wide scan of one u32 per thread; wsum = LDS[blockDim/64]
@@ -962,13 +943,9 @@ __device__ __forceinline__ unsigned block_excl_scan(unsigned x, unsigned* wsum, 
 // tiles, one workgroup per super-bucket): the level-1 scatter's per-tile
 // write offsets, read as one contiguous row per tile
 __global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __restrict__ super_tm,
-                                                       unsigned* __restrict__ super_off,
-                                                       unsigned* __restrict__ bucket_total) {
+                                                       unsigned* __restrict__ super_off) {
   __shared__ unsigned wsum[kBlock / 64 + 1];
   const int64_t B = blockIdx.x;
-  // also clears the bucket totals k_bucket_totals accumulates into next
-  for (int64_t b = B * blockDim.x + threadIdx.x; b <= kp.n_buckets; b += (int64_t)gridDim.x * blockDim.x)
-    bucket_total[b] = 0;
   unsigned carry = 0;
   for (int64_t t0 = 0; t0 < kp.n_tiles; t0 += blockDim.x) {
     const int64_t t = t0 + threadIdx.x;
@@ -1711,8 +1688,8 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
 
 template <int FMT>
 int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
-                   const uint8_t* allowed, const unsigned* super_off, const unsigned* super_base, unsigned* cursor,
-                   char* ws, const Ws& w, unsigned* err) {
+                   const uint8_t* allowed, const unsigned* super_off, const unsigned* super_base,
+                   const unsigned* bucket_start, const unsigned* gcur, char* ws, const Ws& w, unsigned* err) {
   using K1 = L1Key<FMT>;
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
@@ -1726,32 +1703,21 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.super_bits > 0) {
-    // windows: <= n_rows / 4096 full windows + 2 partial ones per super-bucket
-    const int64_t n_l2 = (kp.n + 4 * p.n_supers) / kL2Rows + 2 * p.n_supers + 1;
-    unsigned* win_tile = nullptr;
-    if (FMT == PDP_KEYS_PACKED) {
-      win_tile = (unsigned*)(ws + w.win_tile);
-      PDP_PROF_BEGIN("k_window_tiles", st);
-      hipLaunchKernelGGL(k_window_tiles, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_base, super_off,
-                         win_tile);
-      PDP_PROF_END(st);
-      PDP_HIP_CHECK(hipGetLastError());
-    }
+    const int64_t n_grp = (p.n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
     const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
     const void* l2 = small ? (const void*)k_scatter_l2<FMT, kSmallDest> : (const void*)k_scatter_l2<FMT, kMaxDest>;
-    const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, kL2Items>) : sizeof(StageLds<K2, kMaxDest, true, kL2Items>);
+    const size_t lds2 =
+        small ? sizeof(StageLds<K2, kSmallDest, true, kL2Items, kL2Threads>)
+              : sizeof(StageLds<K2, kMaxDest, true, kL2Items, kL2Threads>);
     PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    const K1* keys1 = (const K1*)(ws + w.keys1);
+    const unsigned* rows1 = ROWS1 ? (const unsigned*)(ws + w.rows1) : nullptr;
+    K2* keys2 = (K2*)(ws + w.keys2);
+    unsigned* rows2 = (unsigned*)(ws + w.rows2);
+    void* args[] = {(void*)&kp, (void*)&super_base, (void*)&super_off, (void*)&bucket_start, (void*)&gcur,
+                    (void*)&keys1, (void*)&rows1, (void*)&keys2, (void*)&rows2};
     PDP_PROF_BEGIN("k_scatter_l2", st);
-    if (small)
-      hipLaunchKernelGGL((k_scatter_l2<FMT, kSmallDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
-                         super_base, super_off, win_tile, cursor, (const K1*)(ws + w.keys1),
-                         ROWS1 ? (const unsigned*)(ws + w.rows1) : nullptr, (K2*)(ws + w.keys2),
-                         (unsigned*)(ws + w.rows2));
-    else
-      hipLaunchKernelGGL((k_scatter_l2<FMT, kMaxDest>), dim3((unsigned)n_l2), dim3(kPartThreads), lds2, st, kp,
-                         super_base, super_off, win_tile, cursor, (const K1*)(ws + w.keys1),
-                         ROWS1 ? (const unsigned*)(ws + w.rows1) : nullptr, (K2*)(ws + w.keys2),
-                         (unsigned*)(ws + w.rows2));
+    PDP_HIP_CHECK(hipLaunchKernel(l2, dim3((unsigned)n_grp, (unsigned)p.n_supers), dim3(kL2Threads), args, lds2, st));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -1893,32 +1859,46 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_super_scan", st);
-  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off, counts);
+  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_bucket_totals", st);
-  hipLaunchKernelGGL(k_bucket_totals, dim3((unsigned)((p.n_buckets + kBlock - 1) / kBlock),
-                                           (unsigned)((p.n_tiles + kTotalsTiles - 1) / kTotalsTiles)),
-                     dim3(kBlock), 0, st, counts_tm, p.n_tiles, p.n_buckets, counts);
+  // rows per bucket (and, with two levels, the level-2 cursors at tile-group starts)
+  const int64_t n_bblk = (p.n_buckets + 63) / 64;
+  const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
+  unsigned* csum = (unsigned*)(ws + w.csum);
+  unsigned* gcur = (unsigned*)(ws + w.gcur);
+  PDP_PROF_BEGIN("k_gscan_sums", st);
+  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
+                     p.n_tiles, p.n_buckets, csum);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_gscan_chunks", st);
+  hipLaunchKernelGGL(k_gscan_chunks, dim3(grid_for(p.n_buckets)), dim3(kBlock), 0, st, csum, n_sc, p.n_buckets,
+                     counts);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  if (p.super_bits > 0) {
+    PDP_PROF_BEGIN("k_gscan_cursors", st);
+    hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
+                       counts_tm, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
   rc = scan_u32(counts, p.n_buckets, chunk_sums, st);
   if (rc != PDP_OK) return rc;
-  unsigned* cursor = (unsigned*)(ws + w.cursor);
   unsigned* super_base = (unsigned*)(ws + w.super_base);
-  const int64_t n_init = (p.n_buckets > p.n_supers + 1 ? p.n_buckets : p.n_supers + 1);
-  PDP_PROF_BEGIN("k_init_cursors", st);
-  hipLaunchKernelGGL(k_init_cursors, dim3(grid_for(n_init)), dim3(kBlock), 0, st, kp, counts, cursor, super_base);
+  PDP_PROF_BEGIN("k_super_bases", st);
+  hipLaunchKernelGGL(k_super_bases, dim3(grid_for(p.n_supers + 1)), dim3(kBlock), 0, st, kp, counts, super_base);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   if (p.key_format == PDP_KEYS_COMPACT)
     return launch_scatter<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
-                                            cursor, ws, w, err);
+                                            counts, gcur, ws, w, err);
   if (p.key_format == PDP_KEYS_PACKED)
     return launch_scatter<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
-                                           cursor, ws, w, err);
-  return launch_scatter<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base, cursor,
-                                       ws, w, err);
+                                           counts, gcur, ws, w, err);
+  return launch_scatter<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                       counts, gcur, ws, w, err);
 }
 
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,
