@@ -75,9 +75,11 @@ typedef struct pdp_bound_config {
   int32_t reserved;
 } pdp_bound_config;
 
-#define PDP_MAX_L0 256
-#define PDP_MAX_LINF 256
-#define PDP_MAX_CONTRIBUTIONS 256
+/* bounds up to int32; above 256 (l0, linf) the pair-table algorithm runs, and
+ * a cap above 256 is applied by radix select instead of a sorted sketch */
+#define PDP_MAX_L0 2147483647
+#define PDP_MAX_LINF 2147483647
+#define PDP_MAX_CONTRIBUTIONS 2147483647
 
 /* bounding algorithms (identical results, different data movement) */
 #define PDP_ALGO_AUTO 0
@@ -85,7 +87,9 @@ typedef struct pdp_bound_config {
 #define PDP_ALGO_BUCKETED 2      /* rows partitioned by pid bucket, sketches in LDS */
 #define PDP_ALGO_PAIR_TABLE 3    /* device hash table of (pid, pk) pairs: the bounders
                                     without cross-partition sampling (l0 = 0,
-                                    max_contributions, rows_are_units); chosen by AUTO */
+                                    max_contributions, rows_are_units), and any bounder
+                                    with l0 or linf > 256 (L0 over the table's distinct
+                                    pairs, the GLOBAL path's pair keys); chosen by AUTO */
 
 /* row records moved by the BUCKETED partition passes (identical results) */
 #define PDP_KEYS_AUTO 0

@@ -30,9 +30,9 @@ NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
 ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED, ALGO_PAIR_TABLE = 0, 1, 2, 3
 MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
 KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED = 0, 1, 2, 3
-MAX_L0 = 256
-MAX_LINF = 256
-MAX_CONTRIBUTIONS = 256
+MAX_L0 = 2**31 - 1            # pipelinedp_amd.h PDP_MAX_*
+MAX_LINF = 2**31 - 1
+MAX_CONTRIBUTIONS = 2**31 - 1
 MAX_OPS = 8
 
 EXPORTED_SYMBOLS = (

@@ -313,9 +313,11 @@ int validate(const pdp_bound_config* c) {
   if (c->n_partitions < 1 || c->n_partitions >= ((int64_t)1 << 32))
     return set_error(PDP_E_INVALID, "n_partitions must be in [1, 2^32)");
   if (c->l0 < 0 || c->l0 > PDP_MAX_L0)
-    return set_error(PDP_E_UNSUPPORTED, "l0 out of supported range [0, 256]");
+    return set_error(PDP_E_UNSUPPORTED, "l0 out of supported range [0, PDP_MAX_L0]");
   if (c->linf < 0 || c->linf > PDP_MAX_LINF)
-    return set_error(PDP_E_UNSUPPORTED, "linf out of supported range [0, 256]");
+    return set_error(PDP_E_UNSUPPORTED, "linf out of supported range [0, PDP_MAX_LINF]");
+  if (c->max_contributions < 0 || c->max_contributions > PDP_MAX_CONTRIBUTIONS)
+    return set_error(PDP_E_UNSUPPORTED, "max_contributions out of supported range [0, PDP_MAX_CONTRIBUTIONS]");
   if (c->value_kind < PDP_VALUE_NONE || c->value_kind > PDP_VALUE_I64)
     return set_error(PDP_E_INVALID, "bad value_kind");
   if (c->value_kind != PDP_VALUE_I64 && (c->flags & PDP_SUM_INT))
@@ -327,8 +329,6 @@ int validate(const pdp_bound_config* c) {
   if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED)
     return set_error(PDP_E_INVALID, "bad key_format");
   if (pairs_mode(c)) return pairs_validate(c);
-  if (c->algorithm == PDP_ALGO_PAIR_TABLE)
-    return set_error(PDP_E_UNSUPPORTED, "PDP_ALGO_PAIR_TABLE runs only the bounders without L0 sampling");
   if (make_plan(c).algorithm < 0)
     return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge / compact keys infeasible for this l0/linf/U/P");
   return PDP_OK;

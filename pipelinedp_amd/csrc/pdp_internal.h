@@ -443,8 +443,13 @@ int scan_u32(unsigned* v, int64_t n, unsigned* chunk_sums, hipStream_t st);
 // Pair-table path (pdp_pairs.hip): LinfSampler / NoOpSampler (l0 == 0),
 // SamplingPerPrivacyIdContributionBounder (max_contributions > 0) and
 // contribution_bounds_already_enforced (rows_are_units).
+// Bounds above this go to the pair-table path, where a cap beyond it selects
+// by radix select instead of an atomicMin-cascade sketch (pdp_pairs.hip).
+#define PDP_SKETCH_MAX 256
+
 inline bool pairs_mode(const pdp_bound_config* c) {
-  return c->l0 == 0 || c->max_contributions > 0 || c->rows_are_units != 0;
+  return c->l0 == 0 || c->max_contributions > 0 || c->rows_are_units != 0 || c->l0 > PDP_SKETCH_MAX ||
+         c->linf > PDP_SKETCH_MAX || c->algorithm == PDP_ALGO_PAIR_TABLE;
 }
 int pairs_validate(const pdp_bound_config* c);
 uint64_t pairs_workspace_bytes(const pdp_bound_config* c);

@@ -142,8 +142,8 @@ def test_workspace_bytes(lib):
 
 
 @pytest.mark.parametrize("field,value,code,msg", [
-    ("l0", -1, -4, b"l0"), ("l0", 257, -4, b"l0"), ("linf", -1, -4, b"linf"),
-    ("max_contributions", 257, -4, b"max_contributions"),
+    ("l0", -1, -4, b"l0"), ("linf", -1, -4, b"linf"),
+    ("max_contributions", -1, -4, b"max_contributions"),
     ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
     ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
     ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 4, -1, b"key_format"),
@@ -171,7 +171,15 @@ def test_pair_table_modes_plan(lib):
     assert b"max_contributions" in lib.pdp_last_error()
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=0, linf=1, rows_are_units=1)), ctypes.byref(info)) == -1
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=0, algorithm=N.ALGO_BUCKETED)), ctypes.byref(info)) == -4
-    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=2, algorithm=N.ALGO_PAIR_TABLE)), ctypes.byref(info)) == -4
+    # PAIR_TABLE with cross-partition sampling: L0 over the table's distinct pairs
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=2, algorithm=N.ALGO_PAIR_TABLE)), ctypes.byref(info)) == 0
+    assert info.algorithm == N.ALGO_PAIR_TABLE
+    # bounds above 256 (l0, linf, max_contributions) resolve to the pair table
+    for kw in (dict(l0=257), dict(l0=2, linf=300), dict(l0=100_000, linf=100_000),
+               dict(l0=0, linf=0, max_contributions=10_000), dict(l0=2**31 - 1, linf=1)):
+        assert lib.pdp_bound_plan(ctypes.byref(_cfg(**kw)), ctypes.byref(info)) == 0, kw
+        assert info.algorithm == N.ALGO_PAIR_TABLE, kw
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(l0=300, algorithm=N.ALGO_BUCKETED)), ctypes.byref(info)) == -4
     # rows_are_units needs no privacy-id column
     cfg = _cfg(n_rows=10, l0=0, linf=0, rows_are_units=1)
     need = ctypes.c_uint64(0)

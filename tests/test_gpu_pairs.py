@@ -155,3 +155,104 @@ def test_pair_table_at_scale_count_identity(device):
     distinct = torch.unique(pid * P + pk).numel()
     assert int(acc["privacy_id_count"].sum()) == distinct
     assert int(acc["count"].sum()) == n
+
+
+# ------------------------------------------------ bounds above 256 -------
+# (l0, linf, max_contributions, value_kind, flags): l0 or linf > 256 run the
+# pair-table path with L0 over its distinct pairs; a cap > 256 selects by
+# radix select (k_select) instead of a sorted sketch.
+BIG = {
+    "linf_300": (0, 300, 0, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
+    "linf_1000_int": (0, 1000, 0, O.VALUE_I64, O.ACC_SUM | O.SUM_INT),
+    "maxc_400": (0, 0, 400, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2),
+    "maxc_3000_count": (0, 0, 3000, O.VALUE_NONE, 0),
+    "l0_500_linf_1": (500, 1, 0, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
+    "l0_300_linf_3": (300, 3, 0, O.VALUE_I64, O.SUM_PER_PARTITION | O.SUM_INT),
+    "l0_400_linf_500": (400, 500, 0, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM | O.ACC_NSUM2),
+    "l0_2_linf_700": (2, 700, 0, O.VALUE_F64, O.SUM_PER_PARTITION),
+    "l0_600_keep_all": (600, 0, 0, O.VALUE_F64, O.ACC_SUM),
+}
+
+
+def _big_spec(mode):
+    from pipelinedp_amd import executor as X
+    l0, linf, maxc, vk, flags = BIG[mode]
+    return X.BoundingSpec(l0=l0, linf=linf, value_kind=vk, flags=flags, min_value=0.0, max_value=10.0,
+                          middle=5.0, min_sum=-50.0, max_sum=3000.0, max_contributions=maxc)
+
+
+def _big_data(seed, vk):
+    """privacy ids 0..3 with 1,000-4,000 distinct partitions and pairs of
+    100..20,000 rows (heavy groups above every cap), plus light background"""
+    rng = np.random.default_rng(seed)
+    parts = [rng.integers(0, 200, 40_000)]                 # background pids 10..209, light
+    pid = [rng.integers(10, 210, 40_000)]
+    for u, (npk, n) in enumerate([(4000, 30_000), (1200, 9_000), (700, 2_000), (1, 20_000)]):
+        pid.append(np.full(n, u))
+        parts.append(rng.integers(0, npk, n) if npk > 1 else np.zeros(n, dtype=np.int64))
+    pid.append(np.full(5_000, 4))                           # pid 4: a few pairs of 100s of rows
+    parts.append(rng.integers(0, 12, 5_000))
+    pid, pk = np.concatenate(pid).astype(np.int64), np.concatenate(parts).astype(np.int64)
+    perm = rng.permutation(len(pid))
+    pid, pk = pid[perm], pk[perm]
+    n = len(pid)
+    val = rng.normal(5.0, 4.0, n) if vk == O.VALUE_F64 else (
+        rng.integers(-3, 12, n, dtype=np.int64) if vk == O.VALUE_I64 else None)
+    return pid, pk, val
+
+
+@pytest.mark.parametrize("mode", sorted(BIG))
+def test_large_bounds_match_oracle(device, mode):
+    spec = _big_spec(mode)
+    U, P = 210, 4000
+    pid, pk, val = _big_data(21, spec.value_kind)
+    from pipelinedp_amd import executor as X
+    plan = X.bound_plan(len(pid), U, P, spec)
+    assert plan.algorithm == 3  # PDP_ALGO_PAIR_TABLE
+    got = _gpu(device, pid, pk, val, U, P, spec, seed=4321)
+    want = _oracle(pid, pk, val, U, P, spec, seed=4321)
+    _compare(got, want, _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle) + 3000.0)
+    full = _oracle(pid, pk, val, U, P, _spec("noop_count_only"), seed=1)
+    assert got["count"].sum() < full["count"].sum()  # sampling fired
+
+
+def test_pair_table_l0_matches_oracle_small_bounds(device):
+    """PDP_ALGO_PAIR_TABLE asked for with l0 = 3, linf = 2: L0 over the table's
+    distinct pairs with the GLOBAL path's pair keys (rand_shift = pk_bits)"""
+    from pipelinedp_amd import executor as X
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM, min_value=0.0,
+                          max_value=10.0, middle=5.0)
+    n, U, P = 50_000, 2_000, 500
+    pid, pk, val = _data(13, n, U, P, O.VALUE_F64, heavy=True)
+    import torch
+    acc = X.bound_and_reduce(torch.as_tensor(pid).to(device), torch.as_tensor(pk).to(device),
+                             torch.as_tensor(val).to(device), n_privacy_ids=U, n_partitions=P, bounding=spec,
+                             seed=99, algorithm=3)
+    got = {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+    want = _oracle(pid, pk, val, U, P, spec, seed=99)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 10.0, 5.0) + 40.0)
+
+
+def test_large_linf_sampling_is_uniform(device):
+    """One pair with 600 rows, keep 300 (radix select): per seed the GPU keeps
+    the oracle's rows (the sum of the kept row indices agrees exactly), and
+    over seeds every row is kept about equally often (np.random.choice's law)."""
+    from scipy.stats import chisquare
+    import torch
+    from pipelinedp_amd import executor as X
+    from oracle.columnar import derive_row_seed, row_priority
+    n = 600
+    spec = X.BoundingSpec(l0=0, linf=300, value_kind=O.VALUE_F64, flags=O.ACC_SUM, min_value=0.0,
+                          max_value=1e6, middle=5e5)
+    pid = torch.zeros(n, dtype=torch.int64, device=device)
+    pk = torch.zeros(n, dtype=torch.int64, device=device)
+    idx = np.arange(n)
+    val = torch.as_tensor(idx.astype(np.float64), device=device)
+    hits = np.zeros(n)
+    for s in range(200):
+        acc = X.bound_and_reduce(pid, pk, val, n_privacy_ids=1, n_partitions=1, bounding=spec, seed=s)
+        kept = np.argsort(row_priority(derive_row_seed(s), idx, idx), kind="stable")[:300]
+        assert int(acc["count"][0]) == 300
+        assert float(acc["sum"][0]) == float(kept.sum())
+        hits[kept] += 1
+    assert chisquare(hits).pvalue > 1e-4
