@@ -13,6 +13,19 @@ Workloads:
      partitions, values N(5, 3) clipped to [0, 10], L0 = 8, Linf = 2.  Weak
      scaling.  At N = 1 with the default workload it also runs as the
      `secondary` object of the JSON line.
+  c4 (BASELINE configs[3]): VARIANCE + PRIVACY_ID_COUNT,
+     Gaussian noise, private partition selection, 1e7 uniform partitions,
+     values U(0, 10), L0 = 4, Linf = 2; 1.25e8 rows and 1.25e7 privacy ids
+     per GPU, so N = 8 is the 1e9-row, 1e8-id configuration.  Weak scaling.
+  c5 (BASELINE configs[4]): COUNT + SUM + MEAN, no public
+     partitions, rows per privacy id discrete Pareto(1.5) capped at 1e6 and
+     rescaled to the row count (rows shuffled), partition keys Zipf(1.1)
+     folded into 1e7, values lognormal(1, 1) clipped to [0, 20], L0 = 4,
+     Linf = 2; 6.25e8 rows and 1.25e7 privacy ids per GPU, so N = 8 is the
+     5e9-row, 1e8-id configuration.  Weak scaling.
+  c4 and c5 time the public API: pipelinedp_amd.DPEngine.aggregate over a
+  device-resident ColumnTable on ColumnarBackend (trusted privacy-id
+  sharding), + compute_budgets() + the collected result, per step.
 
 A step = one full aggregate over the resident batch: contribution bounding
 (L0 + Linf sampling), per-partition reduction, [RCCL reduce-scatter of the
@@ -20,7 +33,7 @@ accumulators], partition selection, compaction and noisy metrics, ending with
 the kept-partition count on the host.  Inputs are resident in HBM before
 timing starts.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
   With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts
   `python -m torch.distributed.run --nproc-per-node N` on itself as a child
   process (before touching the GPU) and exits with its status.
@@ -51,6 +64,9 @@ PMC_SUMMARY = {"c3": os.path.join(HERE, "profiles", "r02", "c3_pmc.json"),
 # workload constants
 C2 = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000, l0=8, linf=2)
 C3 = dict(rows=1_000_000_000, privacy_ids=10_000_000, partitions=1_000_000, l0=2, linf=1, zipf=1.1)
+C4 = dict(rows=125_000_000, privacy_ids=12_500_000, partitions=10_000_000, l0=4, linf=2)
+C5 = dict(rows=625_000_000, privacy_ids=12_500_000, partitions=10_000_000, l0=4, linf=2, pareto=1.5,
+          max_rows_per_id=1_000_000, zipf=1.1, max_value=20.0)
 MIN_VALUE, MAX_VALUE = 0.0, 10.0
 EPS, DELTA = 1.0, 1e-6
 
@@ -60,7 +76,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("c3", "c2"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5"), default="c3")
     ap.add_argument("--rows", type=int, default=0, help="override: rows in total (c3) / per GPU (c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
@@ -179,6 +195,143 @@ def gen_c2(n, U, P, rank, device, seed):
     value = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(
         MIN_VALUE, MAX_VALUE)
     return pid, pk, value
+
+
+def gen_c4(n, U, P, rank, device, seed):
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+    pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
+    value = torch.rand(n, generator=g, device=device, dtype=torch.float64) * MAX_VALUE
+    return pid, pk, value
+
+
+def gen_c5(n, U, P, rank, device, seed):
+    """SURVEY §8(d) C5 shard: rows per privacy id discrete Pareto(1.5)
+    (floor(x_m * u^(-1/1.5)), capped at 1e6, rescaled so they sum to n, the
+    remainder spread one row each over random ids), rows shuffled; pk Zipf(1.1)
+    folded into P; values lognormal(1, 1) clipped to [0, 20]."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    u = torch.rand(U, generator=g, device=device, dtype=torch.float64).clamp_(min=1e-300)
+    cnt = u.pow_(-1.0 / C5["pareto"]).floor_().clamp_(max=C5["max_rows_per_id"])
+    cnt = (cnt * (n / float(cnt.sum()))).floor_().to(torch.int64).clamp_(min=0)
+    short = n - int(cnt.sum())
+    if short > 0:
+        cnt.index_add_(0, torch.randint(0, U, (short,), generator=g, device=device),
+                       torch.ones(short, dtype=torch.int64, device=device))
+    pid = torch.repeat_interleave(torch.arange(U, device=device), cnt)
+    del u, cnt
+    pid = pid[torch.randperm(n, generator=g, device=device)]
+    w = torch.arange(1, P + 1, device=device, dtype=torch.float64).pow_(-C5["zipf"])
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    pk = torch.empty(n, device=device, dtype=torch.int64)
+    for c0 in range(0, n, 1 << 27):  # bounded temporaries
+        c1 = min(n, c0 + (1 << 27))
+        x = torch.rand(c1 - c0, generator=g, device=device, dtype=torch.float64)
+        pk[c0:c1] = torch.searchsorted(cdf, x).clamp_(max=P - 1)
+        del x
+    del w, cdf
+    value = torch.randn(n, generator=g, device=device, dtype=torch.float64).add_(1.0).exp_().clamp_(
+        0.0, C5["max_value"])
+    return pid, pk, value
+
+
+def run_api_workload(args, workload, world, rank, device):
+    """c4 / c5: one step = DPEngine.aggregate (the public API) over this
+    rank's device-resident rows on ColumnarBackend, compute_budgets(), and
+    the collected result; the accumulator exchange runs over RCCL at N > 1."""
+    import torch
+    import torch.distributed as dist
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd import _native as N
+    from pipelinedp_amd import columnar_backend as CB
+    from pipelinedp_amd import executor as X
+    w = C4 if workload == "c4" else C5
+    n, U, P = args.rows or w["rows"], w["privacy_ids"], w["partitions"]
+    gen = gen_c4 if workload == "c4" else gen_c5
+    pid, pk, value = gen(n, U, P, rank, device, 4000 if workload == "c4" else 5000)
+    pid += rank * U  # privacy ids of different ranks are different people
+    torch.cuda.synchronize()
+    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U * world, n_partitions=P)
+    if workload == "c4":
+        params = pdp.AggregateParams(metrics=[pdp.Metrics.VARIANCE, pdp.Metrics.PRIVACY_ID_COUNT],
+                                     noise_kind=pdp.NoiseKind.GAUSSIAN, max_partitions_contributed=w["l0"],
+                                     max_contributions_per_partition=w["linf"], min_value=MIN_VALUE,
+                                     max_value=MAX_VALUE)
+    else:
+        params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN],
+                                     noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=w["l0"],
+                                     max_contributions_per_partition=w["linf"], min_value=MIN_VALUE,
+                                     max_value=C5["max_value"])
+    ext = pdp.DataExtractors(privacy_id_extractor=pdp.ColumnExtractor("pid"),
+                             partition_extractor=pdp.ColumnExtractor("pk"),
+                             value_extractor=pdp.ColumnExtractor("v"))
+    ws = X.BoundWorkspace()
+
+    def step():
+        acc = pdp.NaiveBudgetAccountant(total_epsilon=EPS, total_delta=DELTA)
+        backend = CB.ColumnarBackend(privacy_id_sharding="trusted", workspace=ws)
+        sink = pdp.DPEngine(acc, backend).aggregate(table, params, ext)
+        acc.compute_budgets()
+        return len(sink.collect()), backend
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kept = 0
+    for _ in range(args.steps):
+        kept, backend = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    N.profiler_enable(True)
+    for _ in range(args.steps):
+        step()
+    kernels = N.profiler_report()
+    N.profiler_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    info = backend.last_plan_info
+    del pid, pk, value, table, ws
+    kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
+    launches = {k: v[1] / args.steps for k, v in kernels.items()}
+    ms_per_step = elapsed / args.steps * 1e3
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
+    path_bytes = 24.0 * n
+    path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
+    desc = ("C4: DPEngine.aggregate VARIANCE+PRIVACY_ID_COUNT, Gaussian, private partitions (truncated "
+            "geometric), L0=4, Linf=2, uniform keys" if workload == "c4" else
+            "C5: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions, L0=4, Linf=2, rows per "
+            "privacy id Pareto(1.5) capped at 1e6, Zipf(1.1) partition keys, lognormal values in [0, 20]")
+    return {
+        "value": n * world * args.steps / elapsed,
+        "ms_per_step": ms_per_step,
+        "config": {"workload": f"{desc}, {n:.3g} rows and {U:.3g} privacy ids per GPU, {P:.3g} partitions",
+                   "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
+                   "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
+                   "timed": "public API per step: DPEngine.aggregate + compute_budgets() + collect()"},
+        "roofline": {"bound": "hbm", "kernel": dom, "avg_ms": kernel_ms[dom], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s"},
+        "path_roofline": {"achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes},
+        "kernels": {k: {"ms": kernel_ms[k], "launches_per_step": launches[k]} for k in kernel_ms},
+        "bound_plan": None if info is None else {
+            "algorithm": info.algorithm, "bucket_bits": info.bucket_bits, "n_buckets": info.n_buckets,
+            "lds_bytes": info.lds_bytes,
+            "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(info.key_format, info.key_format)},
+        "partitions_kept": kept,
+    }
 
 
 def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields):
@@ -389,7 +542,7 @@ def main():
             dist.destroy_process_group()
         return
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2"):
         cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
     import torch
     import torch.distributed as dist
@@ -398,7 +551,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
 
-    r = run_workload(args, args.workload, world, rank, device, PMC_SUMMARY[args.workload])
+    if args.workload in ("c4", "c5"):
+        r = run_api_workload(args, args.workload, world, rank, device)
+        r.setdefault("api", None)
+    else:
+        r = run_workload(args, args.workload, world, rank, device, PMC_SUMMARY[args.workload])
     result = {
         "metric": "input rows/sec aggregated (whole node) + achieved HBM GB/s vs peak",
         "value": r["value"],
@@ -409,11 +566,15 @@ def main():
         "ms_per_step": r["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong" if args.workload == "c3" else "weak",
+        "workload_name": args.workload,
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (uniform pid, Zipf(1.1) pk, U(0,10) values), generated on device"
-                 if args.workload == "c3" else
-                 "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device"),
+        "data": {"c3": "synthetic (uniform pid, Zipf(1.1) pk, U(0,10) values), generated on device",
+                 "c2": "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device",
+                 "c4": "synthetic (uniform pid/pk, U(0,10) values), generated on device",
+                 "c5": "synthetic (Pareto(1.5) rows per pid, Zipf(1.1) pk, lognormal(1,1) values clipped to "
+                       "[0,20]), generated on device",
+                 }[args.workload],
         "config": r["config"],
         "roofline": r["roofline"],
         "path_roofline": r["path_roofline"],

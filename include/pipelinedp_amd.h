@@ -93,7 +93,9 @@ typedef struct pdp_bound_config {
 
 /* row records moved by the BUCKETED partition passes (identical results) */
 #define PDP_KEYS_AUTO 0
-#define PDP_KEYS_WIDE 1    /* u64 pair key + u32 row: 12 B per row and pass */
+#define PDP_KEYS_WIDE 1    /* u64 record (bit 63 dead | bucket-within-super and bucket-local
+                              pid | partition) + u32 row: 12 B per row and pass; any
+                              partition count (pair keys are rebuilt in the bucket kernel) */
 #define PDP_KEYS_COMPACT 2 /* u32 (bucket-local pid, partition) + u32 row: 8 B per row and pass;
                               needs super/bucket/partition bits <= 31 (AUTO picks it then) */
 #define PDP_KEYS_PACKED 3  /* level 1: one u64 (row within its 65,536-row tile | bucket-local pid |

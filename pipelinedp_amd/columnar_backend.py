@@ -593,7 +593,9 @@ class AggregateRun:
         if parallel.world_info()[0] > 1:  # one partition dictionary for all ranks
             pk_enc = parallel.global_partition_keys(pk_enc)
             if public is not None and pk_enc.decode is not None:
-                public_codes = np.asarray([pk_enc.encode[k] for k in public], dtype=np.int64)
+                enc_map = pk_enc.encode if pk_enc.encode is not None else \
+                    {k: i for i, k in enumerate(pk_enc.decode)}
+                public_codes = np.asarray([enc_map[k] for k in public], dtype=np.int64)
         pid_t = None if pid_enc is None else \
             _h2d(pid_enc.codes, device, torch.int64)
         pk_t = _h2d(pk_enc.codes, device, torch.int64)

@@ -46,8 +46,12 @@ constexpr int kPartThreads = 512;
 #ifndef PDP_L2_ITEMS
 #define PDP_L2_ITEMS 16
 #endif
+#ifndef PDP_L1_THREADS
+#define PDP_L1_THREADS 512
+#endif
+constexpr int kL1Threads = PDP_L1_THREADS;
 constexpr int kL1Items = PDP_L1_ITEMS;
-constexpr int kL1Rows = kPartThreads * kL1Items;  // rows per level-1 LDS stage
+constexpr int kL1Rows = kL1Threads * kL1Items;  // rows per level-1 LDS stage
 constexpr int kL2Items = PDP_L2_ITEMS;
 #ifndef PDP_L2_THREADS
 #define PDP_L2_THREADS 512
@@ -87,6 +91,11 @@ constexpr int kMaxSupers = 64;               // destinations of a level-1 scatte
 constexpr int kRangeBits = 11;                // partitions per merge range = 2048
 constexpr int kRangeParts = 1 << kRangeBits;
 constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= one block scan
+// More partitions than kMaxRanges ranges of 2^kRangeBits: the bucket kernel
+// groups kept pairs by coarse ranges of 2^range_bits partitions (<= kCoarseRanges
+// of them), k_split_* re-sort each coarse range's records into its
+// 2^kRangeBits-partition ranges, k_fine_reduce sums them (two-level merge)
+constexpr int kCoarseRanges = 256;
 constexpr int kRangeThreads = 256;
 // range-reduce work item: the records of one partition range from a run of
 // consecutive buckets, cut at bucket boundaries every kRangeChunk records
@@ -144,7 +153,11 @@ struct Plan {
   int64_t n_tiles;
   int64_t lds_bytes;
   int merge;            // PDP_MERGE_* (bucketed)
-  int n_ranges;         // PDP_MERGE_RANGES: ceil(P / 2^kRangeBits)
+  int n_ranges;         // PDP_MERGE_RANGES: ceil(P / 2^range_bits)
+  int range_bits;       // partitions per merge range of the bucket kernel (kRangeBits, or coarse)
+  int two_level;        // range_bits > kRangeBits: coarse ranges, then k_split_* / k_fine_*
+  int64_t n_fine;       // two-level: ceil(P / 2^kRangeBits)
+  int64_t fine_items;   // two-level: upper bound on the k_fine_reduce work items
   int64_t range_group;  // records per range-reduce work item (kRangeChunk)
   int64_t n_groups;     // upper bound on the range-reduce work items (+ one sentinel per range)
   int key_format;       // PDP_KEYS_WIDE / PDP_KEYS_COMPACT (bucketed)
@@ -169,20 +182,26 @@ Plan make_plan(const pdp_bound_config* c) {
     if (s > u_bits) s = u_bits;                          // one bucket covers all pids
     const int64_t nb = (c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s;
     while (((nb + ((int64_t)1 << s2) - 1) >> s2) > kMaxSupers) ++s2;
-    if (nb > kMaxBuckets || 64 - p.pk_bits - s - s2 < kMinRandomBits) s = -1;
+    // pair keys: random bits above rand_shift = pk_bits + bucket_bits
+    if (nb > kMaxBuckets || 64 - p.pk_bits - s < kMinRandomBits) s = -1;
   }
   const int auto_algo = s >= 0 ? PDP_ALGO_BUCKETED : PDP_ALGO_GLOBAL_SKETCH;
   p.algorithm = c->algorithm == PDP_ALGO_AUTO ? auto_algo : c->algorithm;
   if (p.algorithm == PDP_ALGO_BUCKETED && s < 0) p.algorithm = -1;  // infeasible
   p.bucket_bits = s < 0 ? 0 : s;
   p.super_bits = s < 0 ? 0 : s2;
-  p.rand_shift = p.pk_bits + p.bucket_bits + p.super_bits;
+  p.rand_shift = p.pk_bits + p.bucket_bits;
   p.n_buckets = (c->n_privacy_ids + ((int64_t)1 << p.bucket_bits) - 1) >> p.bucket_bits;
   p.n_supers = (p.n_buckets + ((int64_t)1 << p.super_bits) - 1) >> p.super_bits;
   p.n_tiles = (c->n_rows + kTileRows - 1) / kTileRows;
   if (p.n_tiles < 1) p.n_tiles = 1;
   p.lds_bytes = ((int64_t)1 << p.bucket_bits) * per_pid;
-  p.n_ranges = (int)((c->n_partitions + kRangeParts - 1) >> kRangeBits);
+  p.range_bits = kRangeBits;
+  p.n_fine = (c->n_partitions + kRangeParts - 1) >> kRangeBits;
+  p.two_level = p.n_fine > kMaxRanges;
+  if (p.two_level)
+    while (((c->n_partitions + ((int64_t)1 << p.range_bits) - 1) >> p.range_bits) > kCoarseRanges) ++p.range_bits;
+  p.n_ranges = (int)((c->n_partitions + ((int64_t)1 << p.range_bits) - 1) >> p.range_bits);
   const bool ranges_ok = p.n_ranges <= kMaxRanges;
   if (p.algorithm != PDP_ALGO_BUCKETED) {
     p.merge = 0;
@@ -215,9 +234,9 @@ Plan make_plan(const pdp_bound_config* c) {
     // one super-bucket (no level 2): PACKED degenerates to COMPACT, which then fits
     if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
   }
-  if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave [+ pid hashes]
+  if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
-    if (p.key_format != PDP_KEYS_WIDE) p.lds_bytes += ((int64_t)4 << p.bucket_bits);
+    p.lds_bytes += ((int64_t)4 << p.bucket_bits);
   }
   if (p.merge == PDP_MERGE_RANGES) {
     // range r yields ceil(records_r / C) items + 1 sentinel, and a bucket
@@ -225,10 +244,13 @@ Plan make_plan(const pdp_bound_config* c) {
     const int64_t recs = p.n_buckets * ((int64_t)c->l0 << p.bucket_bits);
     p.range_group = kRangeChunk;
     p.n_groups = recs / kRangeChunk + 2 * (int64_t)p.n_ranges + 1;
+    p.fine_items = p.two_level ? recs / kRangeChunk + p.n_fine + 1 : 0;
   } else {
     p.n_ranges = 0;
     p.range_group = 0;
     p.n_groups = 0;
+    p.two_level = 0;
+    p.fine_items = 0;
   }
   return p;
 }
@@ -244,6 +266,9 @@ struct Ws {
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
+  // two-level merge: fine-range totals / starts (+ scan scratch), write cursors,
+  // the records re-sorted by fine range, fine work items and their count
+  uint64_t fine_total, fine_chunks, fine_cur, stg_key, stg_f0, stg_f1, stg_f2, fine_items, fine_count;
   uint64_t total;
 };
 
@@ -298,6 +323,18 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       if (c->flags & PDP_ACC_NSUM2) { w.rec_f2 = off; off = align256(off + recs * 8); }
       w.rr_items = off; off = align256(off + (uint64_t)p.n_groups * 16);
       w.rr_count = off; off = align256(off + 16);
+      if (p.two_level) {  // fine-range counts, starts, cursors; records re-sorted by fine range
+        const uint64_t nf = (uint64_t)p.n_fine;
+        w.fine_total = off; off = align256(off + (nf + 1) * 4);
+        w.fine_chunks = off; off = align256(off + (uint64_t)scan_chunk_sums_len((int64_t)nf) * 4);
+        w.fine_cur = off; off = align256(off + nf * 4);
+        w.stg_key = off; off = align256(off + recs * 8);
+        if (w.rec_f0) { w.stg_f0 = off; off = align256(off + recs * 8); }
+        if (w.rec_f1) { w.stg_f1 = off; off = align256(off + recs * 8); }
+        if (w.rec_f2) { w.stg_f2 = off; off = align256(off + recs * 8); }
+        w.fine_items = off; off = align256(off + (uint64_t)p.fine_items * 16);
+        w.fine_count = off; off = align256(off + 16);
+      }
     }
   }
   w.total = off;
@@ -341,6 +378,8 @@ struct KP {  // kernel parameters
   int pk_bits, bucket_bits, super_bits, rand_shift;
   int64_t n_buckets, n_supers, n_tiles;
   int n_ranges;
+  int range_bits;
+  int64_t n_fine_ranges;  // two-level merge: ceil(P / 2^kRangeBits)
   int keys_vec;  // privacy_id / partition_key columns are 16-byte aligned
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
@@ -362,6 +401,8 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.n_supers = p.n_supers;
   k.n_tiles = p.n_tiles;
   k.n_ranges = p.n_ranges;
+  k.range_bits = p.range_bits;
+  k.n_fine_ranges = p.n_fine;
   k.keys_vec = 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
@@ -596,7 +637,8 @@ __global__ void __launch_bounds__(kBlock) k_super_bases(KP kp, const unsigned* _
 // run is then written contiguously at gcur[dest] (coalesced, long runs).
 constexpr int kMaxDest = 1024;
 
-// row record key of the partition passes: u64 pair key (PDP_KEYS_WIDE) or u32
+// row record key of the partition passes: u64 record (PDP_KEYS_WIDE: dead bit
+// 63, bucket-within-super and local pid, partition; expand_key gives its pair key) or u32
 // compact record (PDP_KEYS_COMPACT, and PDP_KEYS_PACKED from level 2 on)
 template <bool COMPACT>
 using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>::type;
@@ -693,19 +735,27 @@ __device__ __forceinline__ uint64_t packed_key(const KP& kp, int64_t u, int64_t 
          (dead ? 0ULL : (uint64_t)k);
 }
 
-// The pair key of a compact record: bit-identical to the key k_scatter_l1
-// writes in the wide format (dead records -> kEmpty, skipped).  hpid[] holds
-// pid_hash of the bucket's 2^bucket_bits privacy ids (LDS).
+// The pair key of a row record (dead records -> kEmpty, skipped): random
+// bits from rand_shift = pk_bits + bucket_bits up, the bucket-local pid, the
+// partition -- pair_key(seed, pid, pk, local << pk_bits, rand_shift).  hpid[]
+// holds pid_hash of the bucket's 2^bucket_bits privacy ids (LDS).  COMPACT
+// records are u32 (bit 31 dead), WIDE records u64 (bit 63 dead); both keep
+// the bucket-within-super bits above the local pid, which the key drops.
 __device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, uint32_t v) {
   if (v >> 31) return kEmpty;
-  const uint64_t mid = (uint64_t)(v >> kp.pk_bits);
-  const uint32_t h = hpid[mid & ((1ULL << kp.bucket_bits) - 1)];
-  return pair_key_from(h, kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask), mid << kp.pk_bits, kp.rand_shift);
+  const uint64_t local = (uint64_t)(v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1);
+  return pair_key_from(hpid[local], kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask), local << kp.pk_bits,
+                       kp.rand_shift);
+}
+__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, unsigned long long v) {
+  if (v >> 63) return kEmpty;
+  const uint64_t local = (v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1);
+  return pair_key_from(hpid[local], kp.seed, (int64_t)(v & kp.pk_mask), local << kp.pk_bits, kp.rand_shift);
 }
 
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
 template <int FMT>
-__global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
+__global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
                                                              const uint8_t* __restrict__ allowed,
                                                              const unsigned* __restrict__ super_off,
@@ -716,7 +766,8 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   constexpr bool ROWS = FMT != PDP_KEYS_PACKED;
   extern __shared__ unsigned long long stage_raw[];
   static_assert(kMaxSupers <= kSmallDest, "level-1 destinations must fit the small stage");
-  StageLds<K, kSmallDest, ROWS, kL1Items>& s = *reinterpret_cast<StageLds<K, kSmallDest, ROWS, kL1Items>*>(stage_raw);
+  using SL = StageLds<K, kSmallDest, ROWS, kL1Items, kL1Threads>;
+  SL& s = *reinterpret_cast<SL*>(stage_raw);
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
   // this tile's first row in each super-bucket region (k_super_scan)
@@ -726,7 +777,6 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
   const int mid_bits = kp.bucket_bits + kp.super_bits;
   const uint64_t mid_mask = (1ULL << mid_bits) - 1;
-  const uint64_t dead = ~((1ULL << kp.rand_shift) - 1);
   // two consecutive rows per 16-byte load (tiles and chunks start even)
   auto load = [&](int64_t c0, int64_t (&u)[kL1Items], int64_t (&k)[kL1Items]) {
 #pragma unroll
@@ -773,9 +823,9 @@ __global__ void __launch_bounds__(kPartThreads) PDP_L1_OCC k_scatter_l1(KP kp, c
         x[q] = (K)compact_key(kp, u[q], k[q], is_dead);
       } else if constexpr (FMT == PDP_KEYS_PACKED) {
         x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(r[q] - (unsigned)t0), is_dead);
-      } else {
+      } else {  // WIDE: u64 (dead bit 63 | bucket-within-super and local pid | partition)
         const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
-        x[q] = (K)(is_dead ? (dead | midv) : pair_key(kp.seed, u[q], k[q], midv, kp.rand_shift));
+        x[q] = (K)(is_dead ? ((1ULL << 63) | midv) : (midv | (uint64_t)k[q]));
       }
     }
 #if PDP_L1_PREFETCH
@@ -1165,10 +1215,9 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int wave = threadIdx.x >> 6;
   const WaveQueue wq{qbase + wave * kQueueCap,
                      (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
-  // COMPACT: pid_hash of the bucket's privacy ids, after the queues
+  // pid_hash of the bucket's privacy ids, after the queues (expand_key)
   uint32_t* hpid = (uint32_t*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap;
-  if (COMPACT)
-    for (int64_t t = threadIdx.x; t < S; t += blockDim.x) hpid[t] = pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t);
+  for (int64_t t = threadIdx.x; t < S; t += blockDim.x) hpid[t] = pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t);
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
@@ -1185,10 +1234,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int64_t begin = offsets[b];
   const int64_t end = offsets[b + 1];  // offsets has n_buckets + 1 entries
   const uint64_t bmask = (uint64_t)S - 1;
-  auto conv = [&](RecKey<COMPACT> v) -> uint64_t {
-    if constexpr (COMPACT) return expand_key(kp, hpid, v);
-    else return v;
-  };
+  auto conv = [&](RecKey<COMPACT> v) -> uint64_t { return expand_key(kp, hpid, v); };
   // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys below
   // their sketch's current maximum
   stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, false>(
@@ -1289,7 +1335,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
       const uint64_t x = sk[slot];
       if (x == kEmpty || cnt[slot] == 0) continue;
-      atomicAdd(rh + ((x & kp.pk_mask) >> kRangeBits), 1u);
+      atomicAdd(rh + ((x & kp.pk_mask) >> kp.range_bits), 1u);
     }
     __syncthreads();
     const unsigned h = threadIdx.x < kp.n_ranges ? rh[threadIdx.x] : 0u;  // n_ranges <= blockDim
@@ -1320,7 +1366,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
       ps = PairSums{(long long)c, 0, 0.0, 0.0, 0.0};
     }
     if (RANGES) {
-      const int64_t i = b * n_slots + atomicAdd(rcur + (p >> kRangeBits), 1u);
+      const int64_t i = b * n_slots + atomicAdd(rcur + (p >> kp.range_bits), 1u);
       rec.key[i] = ((unsigned long long)p << 32) | (unsigned long long)(uint32_t)ps.count;
       if (flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION))
         rec.f0[i] = (flags & PDP_SUM_INT) ? __longlong_as_double(ps.isum) : ps.fsum;
@@ -1515,6 +1561,230 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
   }
 }
 
+// ----------------------------------------------------- two-level merge --
+// Records of coarse range r (work item from k_range_plan, buckets [b_lo,
+// b_hi)) in batches of one bucket per thread; visit(idx, ok) for RR records
+// per thread at a time (ok = a real record), then `after()` once per round.
+template <typename V, typename A>
+__device__ __forceinline__ void item_rounds(const KP& kp, const PairRecords& rec, int r, int64_t b_lo, int64_t b_hi,
+                                            unsigned long long* start, unsigned* pre, unsigned* wsum, V&& visit,
+                                            A&& after) {
+  constexpr int RR = 4;
+  const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
+  for (int64_t bb = b_lo; bb < b_hi; bb += blockDim.x) {
+    int64_t nb = b_hi - bb;
+    if (nb > blockDim.x) nb = blockDim.x;
+    unsigned len = 0;
+    if (threadIdx.x < nb) {
+      const int64_t b = bb + threadIdx.x;
+      const unsigned* run = rec.runs + b * (kp.n_ranges + 1) + r;
+      const unsigned s0 = run[0];
+      len = run[1] - s0;
+      start[threadIdx.x] = (unsigned long long)(b * n_slots + s0);
+    }
+    unsigned total;
+    const unsigned ex = block_excl_scan(len, wsum, &total);
+    pre[threadIdx.x] = ex;
+    __syncthreads();
+    for (unsigned i0 = 0; i0 < total; i0 += RR * blockDim.x) {  // block-uniform trip count
+      uint64_t idx[RR];
+      bool ok[RR];
+#pragma unroll
+      for (int u = 0; u < RR; ++u) {
+        const unsigned i = i0 + threadIdx.x + u * blockDim.x;
+        ok[u] = i < total;
+        int lo = 0, hi = (int)nb - 1;  // last run with pre <= i
+        while (ok[u] && lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (pre[mid] <= i) lo = mid;
+          else hi = mid - 1;
+        }
+        idx[u] = ok[u] ? start[lo] + (i - pre[lo]) : 0;
+      }
+      visit(idx, ok);
+      after();
+    }
+    __syncthreads();  // pre / start / wsum are reused by the next batch
+  }
+}
+
+constexpr int kFinePerCoarseMax = 1 << 13;  // 2^(range_bits - kRangeBits) <= 2^13 (P < 2^32, 256 coarse ranges)
+
+// fine-range totals: per item an LDS histogram of its records' fine ranges,
+// added to fine_total with one atomic per touched fine range
+__global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecords rec, const uint4* __restrict__ items,
+                                                              const unsigned* __restrict__ n_items,
+                                                              unsigned* __restrict__ fine_total) {
+  __shared__ unsigned long long start[kRangeThreads];
+  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned lh[kFinePerCoarseMax];
+  if (blockIdx.x >= *n_items) return;
+  const uint4 it = items[blockIdx.x];
+  if (it.x >> 31) return;  // sentinel
+  const uint4 nx = items[blockIdx.x + 1];
+  if (nx.z == it.z) return;  // empty item
+  const int r = (int)it.x;
+  const int F = 1 << (kp.range_bits - kRangeBits);
+  const int64_t f0 = (int64_t)r << (kp.range_bits - kRangeBits);
+  for (int t = threadIdx.x; t < F; t += blockDim.x) lh[t] = 0;
+  __syncthreads();
+  item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
+              [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (ok[u]) atomicAdd(lh + (int)((rec.key[idx[u]] >> (32 + kRangeBits)) - f0), 1u);
+              },
+              [] {});
+  __syncthreads();
+  for (int t = threadIdx.x; t < F; t += blockDim.x)
+    if (lh[t] && f0 + t < kp.n_fine_ranges) atomicAdd(fine_total + f0 + t, lh[t]);
+}
+
+// records of an item -> the fine-range-sorted arrays: per round an LDS rank
+// per fine range, one atomic per touched fine range reserves its slots at
+// fine_cur (initialised to the fine-range starts), then the records move
+__global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairRecords rec, PairRecords stg,
+                                                                const uint4* __restrict__ items,
+                                                                const unsigned* __restrict__ n_items,
+                                                                unsigned* __restrict__ fine_cur) {
+  __shared__ unsigned long long start[kRangeThreads];
+  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned lh[kFinePerCoarseMax];
+  if (blockIdx.x >= *n_items) return;
+  const uint4 it = items[blockIdx.x];
+  if (it.x >> 31) return;
+  const uint4 nx = items[blockIdx.x + 1];
+  if (nx.z == it.z) return;
+  const int r = (int)it.x;
+  const int F = 1 << (kp.range_bits - kRangeBits);
+  const int64_t f0 = (int64_t)r << (kp.range_bits - kRangeBits);
+  for (int t = threadIdx.x; t < F; t += blockDim.x) lh[t] = 0;
+  __syncthreads();
+  item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
+              [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
+                unsigned long long key[4];
+                int f[4];
+                unsigned rank[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
+                  f[u] = (int)((key[u] >> (32 + kRangeBits)) - f0);
+                  rank[u] = ok[u] ? atomicAdd(lh + f[u], 1u) : 0u;
+                }
+                __syncthreads();
+                // reserve: lh[t] -> this round's base of fine range t (then 0)
+                for (int t = threadIdx.x; t < F; t += blockDim.x) {
+                  const unsigned c = lh[t];
+                  lh[t] = c ? atomicAdd(fine_cur + f0 + t, c) : 0u;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  if (!ok[u]) continue;
+                  const uint64_t o = (uint64_t)lh[f[u]] + rank[u];
+                  stg.key[o] = key[u];
+                  if (stg.f0) stg.f0[o] = rec.f0[idx[u]];
+                  if (stg.f1) stg.f1[o] = rec.f1[idx[u]];
+                  if (stg.f2) stg.f2[o] = rec.f2[idx[u]];
+                }
+                __syncthreads();
+                for (int t = threadIdx.x; t < F; t += blockDim.x) lh[t] = 0;
+              },
+              [] { __syncthreads(); });
+}
+
+// fine work items: fine range f's records [start_f, start_f+1) in chunks of
+// kRangeChunk, appended at a base taken with one atomic (any order)
+__global__ void __launch_bounds__(kBlock) k_fine_plan(KP kp, const unsigned* __restrict__ fine_start,
+                                                      uint4* __restrict__ items, unsigned* __restrict__ n_items) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= kp.n_fine_ranges) return;
+  const unsigned s0 = fine_start[f], s1 = fine_start[f + 1];
+  if (s1 <= s0) return;
+  const unsigned C = (unsigned)kRangeChunk;
+  const unsigned k = (s1 - s0 + C - 1) / C;
+  const unsigned base = atomicAdd(n_items, k);
+  for (unsigned j = 0; j < k; ++j) {
+    const unsigned a = s0 + j * C;
+    items[base + j] = make_uint4((unsigned)f, a, (s1 - a < C ? s1 - a : C), 0u);
+  }
+}
+
+// one workgroup per fine item: contiguous records of one 2^kRangeBits range,
+// summed in LDS (or added directly when few), then coalesced atomics
+__global__ void __launch_bounds__(kRangeThreads) k_fine_reduce(KP kp, PairRecords stg, const uint4* __restrict__ items,
+                                                              const unsigned* __restrict__ n_items,
+                                                              pdp_partition_accumulators acc) {
+  extern __shared__ unsigned long long smem[];
+  double* s0 = (double*)smem;
+  double* s1 = s0 + kRangeParts;
+  double* s2 = s1 + kRangeParts;
+  unsigned* pc = (unsigned*)(s2 + kRangeParts);
+  unsigned* cn = pc + kRangeParts;
+  if (blockIdx.x >= *n_items) return;
+  const uint4 it = items[blockIdx.x];
+  const int64_t p0 = (int64_t)it.x << kRangeBits;
+  const uint64_t a = it.y;
+  const unsigned len = it.z;
+  const int flags = kp.clip.flags;
+  const bool f0 = flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION), f1 = flags & PDP_ACC_NSUM,
+             f2 = flags & PDP_ACC_NSUM2, sum_int = flags & PDP_SUM_INT;
+  const bool direct = len < kRangeDirect;
+  if (!direct) {
+    for (int t = threadIdx.x; t < kRangeParts; t += blockDim.x) {
+      pc[t] = 0;
+      cn[t] = 0;
+      s0[t] = 0.0;
+      s1[t] = 0.0;
+      s2[t] = 0.0;
+    }
+    __syncthreads();
+  }
+  for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
+    const uint64_t o = a + i;
+    const unsigned long long key = stg.key[o];
+    const double v0 = f0 ? stg.f0[o] : 0.0, v1 = f1 ? stg.f1[o] : 0.0, v2 = f2 ? stg.f2[o] : 0.0;
+    if (direct) {
+      const int64_t p = (int64_t)(key >> 32);
+      atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
+      if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key);
+      if (f0) {
+        if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(v0));
+        else unsafeAtomicAdd((double*)acc.sum + p, v0);
+      }
+      if (f1) unsafeAtomicAdd(acc.normalized_sum + p, v1);
+      if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, v2);
+      continue;
+    }
+    const int lp = (int)((key >> 32) - (uint64_t)p0);
+    atomicAdd(pc + lp, 1u);
+    atomicAdd(cn + lp, (unsigned)key);
+    if (f0) {
+      if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0));
+      else atomicAdd(s0 + lp, v0);
+    }
+    if (f1) atomicAdd(s1 + lp, v1);
+    if (f2) atomicAdd(s2 + lp, v2);
+  }
+  if (direct) return;
+  __syncthreads();
+  int64_t plen = kp.P - p0;
+  if (plen > kRangeParts) plen = kRangeParts;
+  for (int t = threadIdx.x; t < plen; t += blockDim.x) {
+    if (pc[t] == 0) continue;
+    const int64_t p = p0 + t;
+    atomicAdd((unsigned long long*)(acc.privacy_id_count + p), (unsigned long long)pc[t]);
+    if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)cn[t]);
+    if (f0) {
+      if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(s0[t]));
+      else unsafeAtomicAdd((double*)acc.sum + p, s0[t]);
+    }
+    if (f1) unsafeAtomicAdd(acc.normalized_sum + p, s1[t]);
+    if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, s2[t]);
+  }
+}
+constexpr size_t kFineLds = kRangeParts * (3 * 8 + 2 * 4);
+
 // exclusive scan of u32 counts[0..n) in place, total -> counts[n]
 __global__ void __launch_bounds__(kBlock) k_scan_chunks(const unsigned* __restrict__ v, int64_t n,
                                                         unsigned* __restrict__ chunk_sums) {
@@ -1677,9 +1947,50 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
                        (const unsigned*)rec.runs, items, n_items);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
-    PDP_PROF_BEGIN("k_range_reduce", st);
-    hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kRangeThreads), kRangeLds, st, kp, rec,
-                       (const uint4*)items, (const unsigned*)n_items, acc);
+    if (!p.two_level) {
+      PDP_PROF_BEGIN("k_range_reduce", st);
+      hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kRangeThreads), kRangeLds, st, kp, rec,
+                         (const uint4*)items, (const unsigned*)n_items, acc);
+      PDP_PROF_END(st);
+      PDP_HIP_CHECK(hipGetLastError());
+      return PDP_OK;
+    }
+    // two-level: coarse items -> fine-range totals -> starts -> records
+    // re-sorted by fine range -> fine items -> LDS sums
+    unsigned* fine_total = (unsigned*)(ws + w.fine_total);
+    unsigned* fine_cur = (unsigned*)(ws + w.fine_cur);
+    PairRecords stg{};
+    stg.key = (unsigned long long*)(ws + w.stg_key);
+    stg.f0 = w.stg_f0 ? (double*)(ws + w.stg_f0) : nullptr;
+    stg.f1 = w.stg_f1 ? (double*)(ws + w.stg_f1) : nullptr;
+    stg.f2 = w.stg_f2 ? (double*)(ws + w.stg_f2) : nullptr;
+    PDP_HIP_CHECK(hipMemsetAsync(fine_total, 0, (uint64_t)(p.n_fine + 1) * 4, st));
+    PDP_PROF_BEGIN("k_split_count", st);
+    hipLaunchKernelGGL(k_split_count, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec,
+                       (const uint4*)items, (const unsigned*)n_items, fine_total);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    const int rc = scan_u32(fine_total, p.n_fine, (unsigned*)(ws + w.fine_chunks), st);
+    if (rc != PDP_OK) return rc;
+    PDP_HIP_CHECK(hipMemcpyAsync(fine_cur, fine_total, (uint64_t)p.n_fine * 4, hipMemcpyDeviceToDevice, st));
+    PDP_PROF_BEGIN("k_split_scatter", st);
+    hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
+                       (const uint4*)items, (const unsigned*)n_items, fine_cur);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    uint4* fitems = (uint4*)(ws + w.fine_items);
+    unsigned* n_fitems = (unsigned*)(ws + w.fine_count);
+    PDP_HIP_CHECK(hipMemsetAsync(n_fitems, 0, 4, st));
+    PDP_PROF_BEGIN("k_fine_plan", st);
+    hipLaunchKernelGGL(k_fine_plan, dim3(grid_for(p.n_fine, 1 << 20)), dim3(kBlock), 0, st, kp,
+                       (const unsigned*)fine_total, fitems, n_fitems);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_fine_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)kFineLds));
+    PDP_PROF_BEGIN("k_fine_reduce", st);
+    hipLaunchKernelGGL(k_fine_reduce, dim3((unsigned)p.fine_items), dim3(kRangeThreads), kFineLds, st, kp, stg,
+                       (const uint4*)fitems, (const unsigned*)n_fitems, acc);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -1693,11 +2004,11 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   using K1 = L1Key<FMT>;
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
-  const size_t lds = sizeof(StageLds<K1, kSmallDest, ROWS1, kL1Items>);
+  const size_t lds = sizeof(StageLds<K1, kSmallDest, ROWS1, kL1Items, kL1Threads>);
   PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1<FMT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
   PDP_PROF_BEGIN("k_scatter_l1", st);
-  hipLaunchKernelGGL(k_scatter_l1<FMT>, dim3((unsigned)p.n_tiles), dim3(kPartThreads), lds, st, kp, pid, pk,
+  hipLaunchKernelGGL(k_scatter_l1<FMT>, dim3((unsigned)p.n_tiles), dim3(kL1Threads), lds, st, kp, pid, pk,
                      allowed, super_off, super_base, (K1*)(ws + w.keys1), ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr,
                      err);
   PDP_PROF_END(st);

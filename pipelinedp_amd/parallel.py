@@ -72,16 +72,65 @@ def shard_by_privacy_id(privacy_ids, world: int, rank: int):
                         for p in pid), dtype=bool, count=len(pid))
 
 
+def _coll_device(group=None):
+    """Device of the tensors a collective takes: the GPU under nccl (RCCL),
+    the CPU under gloo."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _all_gather_sizes(n: int, group=None):
+    import torch
+    import torch.distributed as dist
+    world, _ = world_info(group)
+    dev = _coll_device(group)
+    mine = torch.tensor([int(n)], dtype=torch.int64, device=dev)
+    out = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(out, mine, group=group)
+    return [int(t.item()) for t in out]
+
+
+def _all_gather_var(arr, group=None):
+    """All-gather of a variable-length 1-D int64 / uint8 numpy array as one
+    padded tensor collective: every rank gets the list of all ranks' arrays
+    (rank order)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    world, _ = world_info(group)
+    dev = _coll_device(group)
+    sizes = _all_gather_sizes(len(arr), group)
+    width = max(max(sizes), 1)
+    buf = torch.zeros(width, dtype=torch.from_numpy(np.zeros(0, dtype=arr.dtype)).dtype, device=dev)
+    if len(arr):
+        buf[:len(arr)] = torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+    out = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(out, buf, group=group)
+    return [o[:m].cpu().numpy() for o, m in zip(out, sizes)]
+
+
 def row_offset(n_rows: int, group=None) -> int:
     """Global index of this rank's first row (ranks' shards concatenated in
     rank order); row sampling priorities are keyed by it."""
     world, rank = world_info(group)
     if world == 1:
         return 0
-    import torch.distributed as dist
-    counts = [None] * world
-    dist.all_gather_object(counts, int(n_rows), group=group)
-    return int(sum(counts[:rank]))
+    return int(sum(_all_gather_sizes(n_rows, group)[:rank]))
+
+
+def _key_kind(decode) -> str:
+    import numpy as np
+    if decode is None:
+        return "ids"
+    arr = np.asarray(decode, dtype=object)
+    if all(isinstance(k, (int, np.integer)) and not isinstance(k, bool) for k in arr):
+        return "int"
+    if all(isinstance(k, str) for k in arr):
+        return "str"
+    return "object"
 
 
 def global_partition_keys(enc, group=None):
@@ -89,7 +138,10 @@ def global_partition_keys(enc, group=None):
     every rank gets the same dense code for the same key, so the per-partition
     accumulators of all ranks line up for the exchange.  Dense integer keys
     keep the identity encoding (range = max over ranks); other keys get one
-    dictionary in rank-then-first-appearance order."""
+    dictionary in rank-then-first-appearance order.  Integer and string keys
+    travel as tensors (int64 keys; UTF-8 bytes + lengths), so 1e7-key
+    dictionaries need no pickling; other key types fall back to
+    all_gather_object."""
     world, rank = world_info(group)
     if world == 1:
         return enc
@@ -97,11 +149,66 @@ def global_partition_keys(enc, group=None):
     import torch
     import torch.distributed as dist
     from pipelinedp_amd.columnar import EncodedKeys
+    kind = _key_kind(enc.decode)
+    code = {"ids": 0, "int": 1, "str": 2, "object": 3}[kind]
+    dev = _coll_device(group)
+    mine = torch.tensor([code, int(enc.n)], dtype=torch.int64, device=dev)
+    infos = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(infos, mine, group=group)
+    kinds = [int(t[0].item()) for t in infos]
+    ns = [int(t[1].item()) for t in infos]
+    if all(k == 0 for k in kinds):
+        return EncodedKeys(enc.codes, max(ns), None)
+    if max(kinds) <= 1:  # identity ranges and integer dictionaries: int64 tensors
+        local = np.arange(enc.n, dtype=np.int64) if kind == "ids" else np.asarray(enc.decode, dtype=np.int64)
+        parts = _all_gather_var(local, group)
+        allk = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+        uniq, first = np.unique(allk, return_index=True)
+        order = np.argsort(first, kind="stable")      # rank-then-first-appearance
+        decode = uniq[order]
+        rank_of = np.empty(len(uniq), dtype=np.int64)
+        rank_of[order] = np.arange(len(uniq))
+        remap = rank_of[np.searchsorted(uniq, local)] if len(local) else np.zeros(0, np.int64)
+        dec_obj = decode
+    elif all(k == 2 for k in kinds):  # string dictionaries: UTF-8 bytes + byte lengths
+        local_keys = list(enc.decode)
+        enc_keys = [k.encode("utf-8") for k in local_keys]
+        lens = np.fromiter((len(b) for b in enc_keys), dtype=np.int64, count=len(enc_keys))
+        all_lens = _all_gather_var(lens, group)
+        all_blobs = _all_gather_var(np.frombuffer(b"".join(enc_keys), dtype=np.uint8), group)
+        mapping, dec = {}, []
+        for ln, bl in zip(all_lens, all_blobs):
+            raw, pos = bl.tobytes(), 0
+            for m in ln.tolist():
+                k = raw[pos:pos + m].decode("utf-8")
+                pos += m
+                if k not in mapping:
+                    mapping[k] = len(dec)
+                    dec.append(k)
+        remap = np.fromiter((mapping[k] for k in local_keys), dtype=np.int64, count=len(local_keys))
+        dec_obj = np.asarray(dec, dtype=object)
+        decode = dec_obj
+    else:
+        return _global_keys_objects(enc, group)
+    codes = enc.codes
+    if type(codes).__module__.startswith("torch"):
+        codes = torch.as_tensor(remap, device=codes.device)[codes]
+    else:
+        codes = remap[np.asarray(codes)] if len(remap) else np.asarray(codes, dtype=np.int64)
+    return EncodedKeys(codes, max(len(decode), 1), np.asarray(dec_obj, dtype=object), None)
+
+
+def _global_keys_objects(enc, group=None):
+    """global_partition_keys for key types without a tensor form (tuples,
+    mixed types): the dictionaries travel through all_gather_object."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from pipelinedp_amd.columnar import EncodedKeys
+    world, _ = world_info(group)
     mine = ("ids", int(enc.n)) if enc.decode is None else ("dict", list(enc.decode))
     objs = [None] * world
     dist.all_gather_object(objs, mine, group=group)
-    if all(kind == "ids" for kind, _ in objs):
-        return EncodedKeys(enc.codes, max(n for _, n in objs), None)
     mapping, decode = {}, []
     for kind, payload in objs:
         keys = range(payload) if kind == "ids" else payload
@@ -121,24 +228,29 @@ def global_partition_keys(enc, group=None):
 
 def broadcast_seeds(seeds, group=None):
     """Rank 0's seeds on every rank (selection and noise are keyed by global
-    partition index, so all ranks must draw from the same streams)."""
+    partition index, so all ranks must draw from the same streams): one
+    uint64 tensor broadcast."""
     world, _ = world_info(group)
     if world == 1:
         return tuple(seeds)
+    import torch
     import torch.distributed as dist
-    obj = [tuple(seeds)]
-    dist.broadcast_object_list(obj, src=0, group=group)
-    return tuple(obj[0])
+    vals = [int(x) & 0xFFFFFFFFFFFFFFFF for x in seeds]
+    t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in vals], dtype=torch.int64,
+                     device=_coll_device(group))
+    dist.broadcast(t, src=0, group=group)
+    return tuple(int(v) & 0xFFFFFFFFFFFFFFFF for v in t.cpu().tolist())
 
 
 def all_ranks_any(flag: bool, group=None) -> bool:
     world, _ = world_info(group)
     if world == 1:
         return bool(flag)
+    import torch
     import torch.distributed as dist
-    objs = [None] * world
-    dist.all_gather_object(objs, bool(flag), group=group)
-    return any(objs)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int64, device=_coll_device(group))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
 
 
 _SIGN = -(1 << 63)

@@ -213,6 +213,27 @@ def test_range_merge_matches_oracle_many_ranges(device, P):
     _compare(got, want, _abs_scale(pid, pk, val, P, 0, 9, 4.5))
 
 
+@pytest.mark.parametrize("P,skew", [(2_097_153, False), (10_000_000, False), (10_000_000, True),
+                                     (40_000_000, False)])
+def test_two_level_range_merge_matches_oracle(device, P, skew):
+    """More than 1024 ranges of 2,048 partitions: kept pairs grouped by <= 256
+    coarse ranges in the bucket kernel, re-sorted by fine range (k_split_*),
+    summed per fine range (k_fine_reduce); Zipf-hot partitions included."""
+    from pipelinedp_amd import executor as X
+    n, U = 400_000, 30_000
+    rng = np.random.default_rng(P % 1000 + skew)
+    pid = rng.integers(0, U, n)
+    pk = (np.minimum(rng.zipf(1.2, n) - 1, P - 1) if skew else rng.integers(0, P, n)).astype(np.int64)
+    val = rng.normal(4.0, 3.0, n)
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64,
+                          flags=O.ACC_SUM | O.ACC_NSUM | O.ACC_NSUM2, min_value=0.0, max_value=9.0, middle=4.5)
+    info = X.bound_plan(n, U, P, spec)
+    assert info.merge == 2 and info.n_ranges <= 256 and (P + 2047) // 2048 > 1024
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 33)
+    want = _oracle(pid, pk, val, U, P, spec, 33)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
+
+
 def test_compact_records_chosen_when_they_fit():
     """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records; wider key
     spaces fall back to the 12-byte (u64 key + row) format."""
