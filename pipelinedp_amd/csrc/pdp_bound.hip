@@ -263,6 +263,7 @@ struct Ws {
   // bucketed path
   uint64_t counts_tm, counts, chunk_sums, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
   uint64_t csum, gcur;  // level-2 cursor scans: per tile chunk, per tile group (x n_buckets)
+  uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, record index)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -314,6 +315,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.keys2 = w.keys1;
       w.rows2 = w.rows1;
     }
+    w.cand_key = off; off = align256(off + n * kb2);
+    w.cand_idx = off; off = align256(off + n * 4);
     if (p.merge == PDP_MERGE_RANGES) {
       const uint64_t recs = (uint64_t)p.n_buckets * ((uint64_t)c->l0 << p.bucket_bits);
       w.runs = off; off = align256(off + (uint64_t)p.n_buckets * (p.n_ranges + 1) * 4);
@@ -1028,10 +1031,16 @@ __device__ __forceinline__ void wave_lds_fence() {
 // candidate on compacted wavefronts.  R = 16 / sizeof(K) rows per lane per
 // 16-byte key load (and 4·R-byte row load when ROWS), KU loads in flight per
 // lane; every wave runs the same trip count so the queue stays convergent.
-template <int KU, bool ROWS, typename K, typename CV, typename P, typename W>
+// RM: what a candidate carries beside its key -- kRowNone, kRowLoad (rows[i],
+// a 16-byte load per R records beside the keys) or kRowIndex (the record's
+// position i in `keys`, for candidate lists).
+constexpr int kRowNone = 0, kRowLoad = 1, kRowIndex = 2;
+template <int KU, int RM, typename K, typename CV, typename P, typename W>
 __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const unsigned* __restrict__ rows,
                                               int64_t begin, int64_t end, WaveQueue q, CV&& conv, P&& pred,
                                               W&& work) {
+  constexpr bool ROWS = RM != kRowNone;
+  constexpr bool LOADR = RM == kRowLoad;
   constexpr int R = 16 / sizeof(K);
   using KV = typename std::conditional<R == 4, uint4, ulonglong2>::type;
   using RV = typename std::conditional<R == 4, uint4, uint2>::type;
@@ -1075,11 +1084,13 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
     const int t = threadIdx.x;
     if (t < R - 1 && begin + t < a0) {
       x = conv(keys[begin + t]);
-      if (ROWS) r = rows[begin + t];
+      if (LOADR) r = rows[begin + t];
+      if (RM == kRowIndex) r = (uint32_t)(begin + t);
     }
     if (t >= R && t < 2 * R - 1 && a1 + (t - R) < end) {
       x = conv(keys[a1 + (t - R)]);
-      if (ROWS) r = rows[a1 + (t - R)];
+      if (LOADR) r = rows[a1 + (t - R)];
+      if (RM == kRowIndex) r = (uint32_t)(a1 + (t - R));
     }
     push(x, r);
   }
@@ -1093,7 +1104,7 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
       const int64_t g = g0 + (int64_t)u * blockDim.x + threadIdx.x;
       if (g < np) {
         kx[u] = kv[g];
-        if (ROWS) rx[u] = rv[g];
+        if (LOADR) rx[u] = rv[g];
       } else {
         if constexpr (R == 4) kx[u] = make_uint4(~0u, ~0u, ~0u, ~0u);  // dead records
         else kx[u] = make_ulonglong2(kEmpty, kEmpty);
@@ -1104,6 +1115,17 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
   RV rx[KU];
   if (np > 0) load(0, kx, rx);
   for (int64_t g0 = 0; g0 < np; g0 += step) {
+    // the row carried by component e of this lane's load u
+    auto rowv = [&](int u, int e) -> uint32_t {
+      if constexpr (RM == kRowIndex) {
+        return (uint32_t)(a0 + (g0 + (int64_t)u * blockDim.x + threadIdx.x) * R + e);
+      } else if constexpr (RM == kRowLoad) {
+        if constexpr (R == 4) return e == 0 ? rx[u].x : (e == 1 ? rx[u].y : (e == 2 ? rx[u].z : rx[u].w));
+        else return e == 0 ? rx[u].x : rx[u].y;
+      } else {
+        return 0u;
+      }
+    };
 #if PDP_PIPE
     // software pipeline: the next batch's loads are in flight while this
     // batch runs through the queue (LDS work only, no vector memory)
@@ -1135,27 +1157,20 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
     for (int i = 0; i < KU * R; ++i) ps[i] = pred(xs[i]);
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-      if constexpr (R == 4) {
-        push_p(xs[u * 4 + 0], ROWS ? rx[u].x : 0u, ps[u * 4 + 0]);
-        push_p(xs[u * 4 + 1], ROWS ? rx[u].y : 0u, ps[u * 4 + 1]);
-        push_p(xs[u * 4 + 2], ROWS ? rx[u].z : 0u, ps[u * 4 + 2]);
-        push_p(xs[u * 4 + 3], ROWS ? rx[u].w : 0u, ps[u * 4 + 3]);
-      } else {
-        push_p(xs[u * 2 + 0], ROWS ? rx[u].x : 0u, ps[u * 2 + 0]);
-        push_p(xs[u * 2 + 1], ROWS ? rx[u].y : 0u, ps[u * 2 + 1]);
-      }
+#pragma unroll
+      for (int e = 0; e < R; ++e) push_p(xs[u * R + e], rowv(u, e), ps[u * R + e]);
     }
 #else
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       if constexpr (R == 4) {
-        push(conv(kx[u].x), ROWS ? rx[u].x : 0u);
-        push(conv(kx[u].y), ROWS ? rx[u].y : 0u);
-        push(conv(kx[u].z), ROWS ? rx[u].z : 0u);
-        push(conv(kx[u].w), ROWS ? rx[u].w : 0u);
+        push(conv(kx[u].x), rowv(u, 0));
+        push(conv(kx[u].y), rowv(u, 1));
+        push(conv(kx[u].z), rowv(u, 2));
+        push(conv(kx[u].w), rowv(u, 3));
       } else {
-        push(conv(kx[u].x), ROWS ? rx[u].x : 0u);
-        push(conv(kx[u].y), ROWS ? rx[u].y : 0u);
+        push(conv(kx[u].x), rowv(u, 0));
+        push(conv(kx[u].y), rowv(u, 1));
       }
     }
 #endif
@@ -1164,7 +1179,7 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
         kx[u] = nk[u];
-        if (ROWS) rx[u] = nr[u];
+        if (LOADR) rx[u] = nr[u];
       }
     }
 #else
@@ -1190,7 +1205,9 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
                                                                  const unsigned* __restrict__ rowidx,
                                                                  const unsigned* __restrict__ offsets,
                                                                  const void* __restrict__ value,
-                                                                 pdp_partition_accumulators acc, PairRecords rec) {
+                                                                 pdp_partition_accumulators acc, PairRecords rec,
+                                                                 RecKey<COMPACT>* __restrict__ cand_key,
+                                                                 unsigned* __restrict__ cand_idx) {
 #if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
   return;  // ablation: only the level-1 pass is meaningful
 #endif
@@ -1235,39 +1252,61 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int64_t end = offsets[b + 1];  // offsets has n_buckets + 1 entries
   const uint64_t bmask = (uint64_t)S - 1;
   auto conv = [&](RecKey<COMPACT> v) -> uint64_t { return expand_key(kp, hpid, v); };
-  // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys below
-  // their sketch's current maximum
-  stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, false>(
+  // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys at or
+  // below their sketch's current maximum.  A pair kept in the end entered the
+  // sketch at its first row and never left it (the maximum only decreases),
+  // so every one of its rows is a candidate here: the candidates still in
+  // their sketch after the insert are appended to a per-bucket list
+  // (record-local key + record index) and B2 reads only that list.
+  __shared__ unsigned ccount;
+  if (threadIdx.x == 0) ccount = 0;
+  __syncthreads();
+  const uint64_t lbits = ((uint64_t)1 << (kp.pk_bits + kp.bucket_bits)) - 1;  // local pid | partition
+  stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, kRowIndex>(
       keys, rowidx, begin, end, wq, conv,
       [&](uint64_t x) {
 #ifdef PDP_ABL_B1_NOPRED
         return x == 0;
 #endif
-        return !dead_key(x, kp.rand_shift) && x < sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
+        return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
       },
-      [&](uint64_t x, uint32_t) PDP_WORK_ATTR {
+      [&](uint64_t x, uint32_t i) PDP_WORK_ATTR {
         unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask);
 #if PDP_INSERT_SKIP
         if (x < s[(l0 - 1) * S]) sketch_insert_strided_skip(s, l0, S, x);
 #else
         if (x < s[(l0 - 1) * S]) sketch_insert_strided(s, l0, S, x);
 #endif
+        const bool keep = x <= s[(l0 - 1) * S];
+        const unsigned long long active = __ballot(true);
+        const unsigned long long m = __ballot(keep);
+        const int leader = __ffsll((long long)active) - 1;
+        unsigned base = 0;
+        if ((int)(threadIdx.x & 63) == leader && m) base = atomicAdd(&ccount, (unsigned)__popcll(m));
+        base = __shfl(base, leader, 64);
+        if (keep) {
+          const int64_t o = begin + base + __popcll(m & ((1ULL << (threadIdx.x & 63)) - 1));
+          cand_key[o] = (RecKey<COMPACT>)(x & lbits);
+          cand_idx[o] = i;
+        }
       });
   __syncthreads();
 #ifdef PDP_ABL_B1_ONLY
   return;
 #endif
-  // B2: rows of kept pairs
+  // B2: rows of kept pairs, from B1's candidate list (the row index gathered
+  // for the rows of kept pairs only)
   const int flags = kp.clip.flags;
-  stream_bucket<COMPACT ? PDP_B2_KU_COMPACT : kUnroll / 2, true>(
-      keys, rowidx, begin, end, wq, conv,
+  stream_bucket<COMPACT ? PDP_B2_KU_COMPACT : kUnroll / 2, kRowLoad>(
+      cand_key, cand_idx, begin, begin + ccount, wq, conv,
       [&](uint64_t x) {
         return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
       },
-      [&](uint64_t x, uint32_t r) PDP_WORK_ATTR {
+      [&](uint64_t x, uint32_t ci) PDP_WORK_ATTR {
       const int64_t pl = (x >> kp.pk_bits) & bmask;
       const int j = sketch_find_strided(sk + pl, l0, S, x);
       if (j < 0) return;
+      const uint32_t r = rowidx[ci];
       const int64_t slot = j * S + pl;  // entry j of pid pl (structure of arrays)
       atomicAdd(cnt + slot, 1u);
       if (!KEEP_ALL_ROWS) {
@@ -1931,7 +1970,10 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
   const void* keys2 = ws + w.keys2;
   const unsigned* rows2 = (const unsigned*)(ws + w.rows2);
   const unsigned* counts = (const unsigned*)(ws + w.counts);
-  void* args[] = {(void*)&kp, (void*)&keys2, (void*)&rows2, (void*)&counts, (void*)&value, (void*)&acc, (void*)&rec};
+  void* cand_key = ws + w.cand_key;
+  unsigned* cand_idx = (unsigned*)(ws + w.cand_idx);
+  void* args[] = {(void*)&kp,  (void*)&keys2, (void*)&rows2,    (void*)&counts,  (void*)&value,
+                  (void*)&acc, (void*)&rec,   (void*)&cand_key, (void*)&cand_idx};
   PDP_PROF_BEGIN("k_bucket_bound", st);
   PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
   PDP_PROF_END(st);

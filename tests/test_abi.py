@@ -129,13 +129,14 @@ def test_workspace_bytes(lib):
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(n_rows=1000)), ctypes.byref(small)) == 0
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg()), ctypes.byref(big)) == 0
     assert 0 < small.value < big.value
-    # bucketed, compact records: two levels of (4 B record + 4 B row) + pair records
+    # bucketed, compact records: two levels of (4 B record + 4 B row), the
+    # bucket kernel's candidate list (4 B key + 4 B index) + pair records
     # (8 B key + 8 B nsum per kept slot)
-    assert big.value >= 100_000_000 * 16 + 1_000_000 * 8 * 16
-    assert big.value < 100_000_000 * 18 + 1_000_000 * 8 * 16 + (64 << 20)
+    assert big.value >= 100_000_000 * 24 + 1_000_000 * 8 * 16
+    assert big.value < 100_000_000 * 26 + 1_000_000 * 8 * 16 + (64 << 20)
     wide = ctypes.c_uint64(0)
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(key_format=N.KEYS_WIDE)), ctypes.byref(wide)) == 0
-    assert wide.value >= 100_000_000 * 24 + 1_000_000 * 8 * 16
+    assert wide.value >= 100_000_000 * 36 + 1_000_000 * 8 * 16
     cb = ctypes.c_uint64(0)
     assert lib.pdp_compact_workspace_bytes(1 << 20, ctypes.byref(cb)) == 0 and cb.value > 0
 
