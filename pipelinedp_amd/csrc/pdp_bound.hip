@@ -107,7 +107,7 @@ constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
 // 16-byte key loads in flight per lane in the bucket kernel's B1 / B2 passes
 #ifndef PDP_B1_KU_COMPACT
-#define PDP_B1_KU_COMPACT 1
+#define PDP_B1_KU_COMPACT 4
 #endif
 #ifndef PDP_PIPE
 #define PDP_PIPE 1
@@ -130,6 +130,10 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #ifndef PDP_L1_OCC
 #define PDP_L1_OCC
 #endif
+// tile-local level 1 when its LDS fits (A/B knob: 0 = histogram pass + global offsets)
+#ifndef PDP_L1_LOCAL
+#define PDP_L1_LOCAL 1
+#endif
 #ifndef PDP_GATHER_VALUES
 #define PDP_GATHER_VALUES 1
 #endif
@@ -141,6 +145,10 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #endif
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
+
+constexpr int64_t kL1HistMax = 8192;         // tile-local level 1: buckets counted in its LDS
+constexpr int64_t kL1LocalLds = 80 * 1024;   // ... and its LDS cap (two workgroups per CU)
+size_t l1_stage_bytes(int key_format);       // LDS of one level-1 stage (after StageLds)
 
 struct Plan {
   int algorithm;   // PDP_ALGO_*
@@ -161,6 +169,8 @@ struct Plan {
   int64_t range_group;  // records per range-reduce work item (kRangeChunk)
   int64_t n_groups;     // upper bound on the range-reduce work items (+ one sentinel per range)
   int key_format;       // PDP_KEYS_WIDE / PDP_KEYS_COMPACT (bucketed)
+  int l1_local;         // tile-local level 1 (k_scatter_l1_local / k_scatter_l2_local), no histogram pass
+  int64_t n_stages;     // level-1 stages of kL1Rows rows
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -234,6 +244,18 @@ Plan make_plan(const pdp_bound_config* c) {
     // one super-bucket (no level 2): PACKED degenerates to COMPACT, which then fits
     if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
   }
+  p.n_stages = (c->n_rows + kL1Rows - 1) / kL1Rows;
+  p.l1_local = 0;
+  if (PDP_L1_LOCAL && p.algorithm == PDP_ALGO_BUCKETED && p.super_bits > 0 && p.n_buckets <= kL1HistMax) {
+    // tile-local level 1 prefers PACKED records to COMPACT ones: one u64
+    // array, so level 2 reads each run as one span
+    const int fmt = (c->key_format == PDP_KEYS_AUTO && p.key_format == PDP_KEYS_COMPACT && packed_ok)
+                        ? PDP_KEYS_PACKED : p.key_format;
+    if ((int64_t)l1_stage_bytes(fmt) + 4 * p.n_buckets <= kL1LocalLds) {
+      p.l1_local = 1;
+      p.key_format = fmt;
+    }
+  }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
     p.lds_bytes += ((int64_t)4 << p.bucket_bits);
@@ -264,6 +286,7 @@ struct Ws {
   uint64_t counts_tm, counts, chunk_sums, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
   uint64_t csum, gcur;  // level-2 cursor scans: per tile chunk, per tile group (x n_buckets)
   uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, record index)
+  uint64_t soff;                // tile-local level 1: per stage, super-bucket run starts (u16)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -306,8 +329,10 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const bool packed = p.key_format == PDP_KEYS_PACKED && p.super_bits > 0;
     const uint64_t kb1 = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;  // level-1 key
     const uint64_t kb2 = p.key_format == PDP_KEYS_WIDE ? 8 : 4;     // level-2 key
-    w.keys1 = off; off = align256(off + n * (packed ? 8 : kb1));
-    if (!packed) { w.rows1 = off; off = align256(off + n * 4); }
+    const uint64_t n1 = p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n;  // level-1 records (stage blocks)
+    w.keys1 = off; off = align256(off + n1 * (packed ? 8 : kb1));
+    if (!packed) { w.rows1 = off; off = align256(off + n1 * 4); }
+    if (p.l1_local) { w.soff = off; off = align256(off + (uint64_t)p.n_stages * (p.n_supers + 1) * 2); }
     if (p.super_bits > 0) {
       w.keys2 = off; off = align256(off + n * kb2);
       w.rows2 = off; off = align256(off + n * 4);
@@ -667,6 +692,14 @@ struct StageLds {
 };
 constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four workgroups per CU
 
+size_t l1_stage_bytes(int key_format) {
+  switch (key_format) {
+    case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kL1Items, kL1Threads>);
+    case PDP_KEYS_PACKED: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kL1Items, kL1Threads>);
+    default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kL1Items, kL1Threads>);
+  }
+}
+
 // phase 1: histogram + local rank (dest < 0 = drop the row)
 template <typename K, int MAXD, bool ROWS, int N, int TH>
 __device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N, TH>& s, int ndest, const int (&d)[N],
@@ -1008,6 +1041,258 @@ __global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __
     if (t < kp.n_tiles) super_off[t * kp.n_supers + B] = carry + ex;
     carry += total;
     __syncthreads();  // wsum is reused by the next chunk
+  }
+}
+
+// ------------------------------------------------ tile-local level 1 / 2 --
+// Plan.l1_local: level 1 needs no histogram pass before it.  Each 4,096-row
+// stage is counting-sorted by super-bucket in LDS and written whole to its
+// own block keys1[stage * kL1Rows, + rows kept) -- one contiguous span per
+// stage -- with soff[stage][B] (u16, n_supers + 1 entries) = where
+// super-bucket B's run starts in that block.  The tile's rows per bucket
+// (counts_tm, the level-2 cursor input) are counted in LDS on the way, so the
+// privacy-id column is read once (k_part_hist + k_super_scan are not run).
+constexpr int kStagesPerTile = (int)(kTileRows / kL1Rows);
+constexpr int kL2Runs = kL2GroupTiles * kStagesPerTile;  // level-1 runs per level-2 workgroup
+static_assert(kTileRows % kL1Rows == 0, "a tile is a whole number of level-1 stages");
+static_assert(kL2Runs <= kL2Threads && kL2Runs <= 256, "one run per thread in the run scan; u8 run tags");
+
+// the LDS stage block [0, total) -> dst, 16 bytes per lane
+template <typename K>
+__device__ __forceinline__ void copy_block(K* __restrict__ dst, const K* src, unsigned total) {
+  constexpr unsigned V = 16 / sizeof(K);
+  using VT = typename std::conditional<V == 4, uint4, ulonglong2>::type;
+  const unsigned nv = total / V;
+  for (unsigned k = threadIdx.x; k < nv; k += blockDim.x)
+    reinterpret_cast<VT*>(dst)[k] = reinterpret_cast<const VT*>(src)[k];
+  for (unsigned k = nv * V + threadIdx.x; k < total; k += blockDim.x) dst[k] = src[k];
+}
+
+template <int FMT>
+__global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP kp, const int64_t* __restrict__ pid,
+                                                                   const int64_t* __restrict__ pk,
+                                                                   const uint8_t* __restrict__ allowed,
+                                                                   unsigned* __restrict__ counts_tm,
+                                                                   uint16_t* __restrict__ soff,
+                                                                   L1Key<FMT>* __restrict__ keys1,
+                                                                   unsigned* __restrict__ rows1, unsigned* err) {
+  using K = L1Key<FMT>;
+  constexpr bool ROWS = FMT != PDP_KEYS_PACKED;
+  extern __shared__ unsigned long long stage_raw[];
+  using SL = StageLds<K, kSmallDest, ROWS, kL1Items, kL1Threads>;
+  SL& s = *reinterpret_cast<SL*>(stage_raw);
+  unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);  // [n_buckets] rows per bucket
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) bh[b] = 0;
+  __syncthreads();
+  const int64_t t = blockIdx.x;
+  const int nd = (int)kp.n_supers;
+  const int64_t t0 = t * kTileRows;
+  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  const int mid_bits = kp.bucket_bits + kp.super_bits;
+  const uint64_t mid_mask = (1ULL << mid_bits) - 1;
+  auto load = [&](int64_t c0, int64_t (&u)[kL1Items], int64_t (&k)[kL1Items]) {
+#pragma unroll
+    for (int q = 0; q < kL1Items; q += 2) {
+      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+      if (kp.keys_vec && i + 1 < t1) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+        const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
+        u[q] = a.x;
+        u[q + 1] = a.y;
+        k[q] = c.x;
+        k[q + 1] = c.y;
+      } else {
+        u[q] = i < t1 ? pid[i] : 0;
+        k[q] = i < t1 ? pk[i] : 0;
+        u[q + 1] = i + 1 < t1 ? pid[i + 1] : 0;
+        k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
+      }
+    }
+  };
+  int64_t u[kL1Items], k[kL1Items];
+  if (t0 < t1) load(t0, u, k);
+  for (int64_t c0 = t0; c0 < t1; c0 += kL1Rows) {
+    const int64_t st = c0 / kL1Rows;  // global stage index
+    int d[kL1Items];
+    K x[kL1Items];
+    unsigned r[kL1Items];
+#pragma unroll
+    for (int q = 0; q < kL1Items; ++q) {
+      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+      r[q] = (unsigned)i;
+      d[q] = -1;
+      x[q] = 0;
+      if (i >= t1) continue;
+      if (u[q] < 0 || u[q] >= kp.U) {  // invalid privacy id: flagged, not counted
+        atomicOr(err, 1u);
+        continue;
+      }
+      atomicAdd(bh + (u[q] >> kp.bucket_bits), 1u);
+      d[q] = (int)(u[q] >> mid_bits);
+      bool is_dead = false;
+      if (k[q] < 0 || k[q] >= kp.P) {
+        atomicOr(err, 1u);
+        is_dead = true;
+      } else if (allowed != nullptr && allowed[k[q]] == 0) {
+        is_dead = true;
+      }
+      if constexpr (FMT == PDP_KEYS_COMPACT) {
+        x[q] = (K)compact_key(kp, u[q], k[q], is_dead);
+      } else if constexpr (FMT == PDP_KEYS_PACKED) {
+        x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), is_dead);
+      } else {
+        const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
+        x[q] = (K)(is_dead ? ((1ULL << 63) | midv) : (midv | (uint64_t)k[q]));
+      }
+    }
+    unsigned rank[kL1Items];
+    stage_count(s, nd, d, rank);
+#pragma unroll
+    for (int q = 0; q < kL1Items; ++q) {
+      if (d[q] < 0) continue;
+      const unsigned slot = s.start[d[q]] + rank[q];
+      s.keys[slot] = x[q];
+      if (ROWS) s.rows[slot] = r[q];
+    }
+    __syncthreads();
+    const unsigned total = s.start[nd - 1] + s.hist[nd - 1];
+    copy_block(keys1 + st * kL1Rows, s.keys, total);
+    if (ROWS) copy_block(rows1 + st * kL1Rows, s.rows, total);
+    for (int B = threadIdx.x; B <= nd; B += blockDim.x)
+      soff[st * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] : total);
+    __syncthreads();
+    if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
+  }
+  __syncthreads();
+  unsigned* row = counts_tm + t * kp.n_buckets;  // tile-major: coalesced
+  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) row[b] = bh[b];
+}
+
+// Level 2 over tile-local level-1 blocks: workgroup (group g of kL2GroupTiles
+// tiles, super-bucket B) takes B's run from each of the group's stages
+// (kL2Runs runs: keys1[st * kL1Rows + soff[st][B], + soff[st][B + 1])),
+// concatenated in stage order, kL2Rows records per LDS window.  Per window an
+// LDS map (the run of every record, in the stage's destination-tag array
+// before the counting sort reuses it) lets each thread address its own
+// records, so all of a thread's loads go out together.  Cursors as in
+// k_scatter_l2; PACKED rows are (stage / kStagesPerTile) * 65,536 + tile row.
+template <int FMT, int MAXD>
+__global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+                                                                   const unsigned* __restrict__ bucket_start,
+                                                                   const unsigned* __restrict__ gcur,
+                                                                   const L1Key<FMT>* __restrict__ keys1,
+                                                                   const unsigned* __restrict__ rows1,
+                                                                   L2Key<FMT>* __restrict__ keys2,
+                                                                   unsigned* __restrict__ rows2) {
+  using KI = L1Key<FMT>;
+  using KO = L2Key<FMT>;
+  constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
+  constexpr bool ROWS1 = !PACKED;
+  extern __shared__ unsigned long long stage_raw[];
+  using SL = StageLds<KO, MAXD, true, kL2Items, kL2Threads>;
+  using D = typename SL::D;
+  SL& s = *reinterpret_cast<SL*>(stage_raw);
+  __shared__ unsigned rbeg[kL2Runs + 1];  // start of each run in the concatenation
+  __shared__ unsigned rsrc[kL2Runs];      // its first record in keys1
+  __shared__ unsigned wsum[kL2Threads / 64 + 1];
+  // XCD-aware order: a group's workgroups (all super-buckets) run one after
+  // another on one XCD (blocks are placed round-robin, linear id % 8), so the
+  // cache lines that two neighbouring runs of a stage block share are read
+  // from that XCD's L2
+  const int nd = (int)kp.n_supers;
+  const int64_t n_grp = (kp.n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
+  const int64_t lin = blockIdx.x, kx = lin >> 3;
+  const int64_t g = (kx / nd) * 8 + (lin & 7);
+  const int B = (int)(kx % nd);
+  if (g >= n_grp) return;  // block-uniform
+  const int64_t n_stages = (kp.n + kL1Rows - 1) / kL1Rows;
+  const int64_t S0 = g * kL2Runs;
+  const int nr = (int)(n_stages - S0 < kL2Runs ? n_stages - S0 : kL2Runs);
+  unsigned len = 0, src = 0;
+  if ((int)threadIdx.x < nr) {
+    const uint16_t* o = soff + (S0 + threadIdx.x) * (nd + 1) + B;
+    len = (unsigned)o[1] - (unsigned)o[0];
+    src = (unsigned)((S0 + threadIdx.x) * kL1Rows) + o[0];
+  }
+  unsigned total;
+  const unsigned ex = block_excl_scan(len, wsum, &total);
+  if ((int)threadIdx.x < nr) {
+    rbeg[threadIdx.x] = ex;
+    rsrc[threadIdx.x] = src;
+  }
+  if ((int)threadIdx.x == nr) rbeg[nr] = total;
+  const int nsub = 1 << kp.super_bits;
+  const int64_t s_first = (int64_t)B << kp.super_bits;
+  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+    const int64_t b = s_first + t;
+    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * kp.n_buckets + b] : 0u;
+  }
+  __syncthreads();
+  if (total == 0) return;  // block-uniform
+  const int bb = kp.bucket_bits;
+  const uint32_t local_mask = (1u << bb) - 1;
+  const int sub_shift = kp.pk_bits + kp.bucket_bits;
+  const uint64_t sub_mask = (uint64_t)nsub - 1;
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  int j0 = 0;  // first run overlapping the window (block-uniform)
+  for (unsigned base = 0; base < total; base += kL2Rows) {
+    const unsigned wend = base + kL2Rows < total ? base + kL2Rows : total;
+    while (rbeg[j0 + 1] <= base) ++j0;
+    for (int j = j0 + (int)(threadIdx.x >> 6); j < nr && rbeg[j] < wend; j += nw) {
+      const unsigned a = rbeg[j] > base ? rbeg[j] : base;
+      const unsigned e = rbeg[j + 1] < wend ? rbeg[j + 1] : wend;
+      for (unsigned v = a + lane; v < e; v += 64) s.dest[v - base] = (D)(j - j0);
+    }
+    __syncthreads();
+    // records in two halves of loads in flight (register budget of two
+    // workgroups per CU), unpacked into the counting sort's items
+    KO x[kL2Items];
+    unsigned r[kL2Items];
+    int d[kL2Items];
+    constexpr int H = kL2Items / 2;
+#pragma unroll
+    for (int h = 0; h < kL2Items; h += H) {
+      KI raw[H];
+      unsigned rr[H];  // PACKED: the record's tile's first row; else its row
+      bool live[H];
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        const unsigned v = base + threadIdx.x + (unsigned)(h + q) * blockDim.x;
+        live[q] = v < wend;
+        if (live[q]) {
+          const int j = j0 + (int)s.dest[v - base];
+          const unsigned i = rsrc[j] + (v - rbeg[j]);
+          raw[q] = keys1[i];
+          if (ROWS1) rr[q] = rows1[i];
+          else rr[q] = (unsigned)(((S0 + j) / kStagesPerTile) * kTileRows);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < H; ++q) {
+        d[h + q] = -1;
+        x[h + q] = 0;
+        r[h + q] = 0;
+        if (!live[q]) continue;
+        if constexpr (PACKED) {
+          const uint64_t v = raw[q];
+          const uint32_t mid = (uint32_t)((v >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
+          d[h + q] = (int)(mid >> bb);
+          const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
+          x[h + q] = (KO)((v >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(v & kp.pk_mask)));
+          r[h + q] = rr[q] + (uint32_t)((v >> kPackedRowShift) & (kTileRows - 1));
+        } else {
+          x[h + q] = (KO)raw[q];
+          r[h + q] = rr[q];
+          d[h + q] = (int)((raw[q] >> sub_shift) & sub_mask);
+        }
+      }
+    }
+    __syncthreads();  // the destination tags are rewritten by the counting sort
+    unsigned rank[kL2Items];
+    stage_count(s, nsub, d, rank);
+    stage_write(s, nsub, d, rank, x, r, keys2, rows2);
+    for (int t = threadIdx.x; t < nsub; t += blockDim.x) s.gcur[t] += s.hist[t];
+    __syncthreads();
   }
 }
 
@@ -2077,6 +2362,71 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   return PDP_OK;
 }
 
+// tile-local level 1 -> level-2 cursors and bucket starts -> tile-local level 2
+template <int FMT>
+int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
+                 const uint8_t* allowed, char* ws, const Ws& w, unsigned* err) {
+  using K1 = L1Key<FMT>;
+  using K2 = L2Key<FMT>;
+  constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
+  unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
+  unsigned* counts = (unsigned*)(ws + w.counts);
+  uint16_t* soff = (uint16_t*)(ws + w.soff);
+  K1* keys1 = (K1*)(ws + w.keys1);
+  unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
+  const size_t lds1 = l1_stage_bytes(FMT) + ((size_t)p.n_buckets * 4 + 7) / 8 * 8 + 8;
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1_local<FMT>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+  PDP_PROF_BEGIN("k_scatter_l1", st);
+  hipLaunchKernelGGL(k_scatter_l1_local<FMT>, dim3((unsigned)p.n_tiles), dim3(kL1Threads), lds1, st, kp, pid, pk,
+                     allowed, counts_tm, soff, keys1, rows1, err);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  const int64_t n_bblk = (p.n_buckets + 63) / 64;
+  const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
+  unsigned* csum = (unsigned*)(ws + w.csum);
+  unsigned* gcur = (unsigned*)(ws + w.gcur);
+  PDP_PROF_BEGIN("k_gscan_sums", st);
+  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
+                     p.n_tiles, p.n_buckets, csum);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_gscan_chunks", st);
+  hipLaunchKernelGGL(k_gscan_chunks, dim3(grid_for(p.n_buckets)), dim3(kBlock), 0, st, csum, n_sc, p.n_buckets,
+                     counts);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_gscan_cursors", st);
+  hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
+                     counts_tm, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  const int rc = scan_u32(counts, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);
+  if (rc != PDP_OK) return rc;
+  const int64_t n_grp = (p.n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
+  const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
+  const void* l2 = small ? (const void*)k_scatter_l2_local<FMT, kSmallDest>
+                         : (const void*)k_scatter_l2_local<FMT, kMaxDest>;
+  const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, kL2Items, kL2Threads>)
+                            : sizeof(StageLds<K2, kMaxDest, true, kL2Items, kL2Threads>);
+  PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+  const uint16_t* soff_c = soff;
+  const unsigned* counts_c = counts;
+  const unsigned* gcur_c = gcur;
+  const K1* keys1_c = keys1;
+  const unsigned* rows1_c = rows1;
+  K2* keys2 = (K2*)(ws + w.keys2);
+  unsigned* rows2 = (unsigned*)(ws + w.rows2);
+  void* args[] = {(void*)&kp, (void*)&soff_c, (void*)&counts_c, (void*)&gcur_c, (void*)&keys1_c, (void*)&rows1_c,
+                  (void*)&keys2, (void*)&rows2};
+  PDP_PROF_BEGIN("k_scatter_l2", st);
+  const int64_t n_blk = (n_grp + 7) / 8 * 8 * p.n_supers;  // k_scatter_l2_local maps ids to (group, super)
+  PDP_HIP_CHECK(hipLaunchKernel(l2, dim3((unsigned)n_blk), dim3(kL2Threads), args, lds2, st));
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
 template <template <int, bool> class F, typename... A>
 int dispatch(int value_kind, bool keep_all, A&&... args) {
   switch (value_kind) {
@@ -2198,6 +2548,13 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   if (cfg->n_rows == 0) {
     PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (p.n_buckets + 1) * 4, st));
     return PDP_OK;
+  }
+  if (p.l1_local) {
+    if (p.key_format == PDP_KEYS_COMPACT)
+      return launch_local<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    if (p.key_format == PDP_KEYS_PACKED)
+      return launch_local<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    return launch_local<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   }
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
   unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);

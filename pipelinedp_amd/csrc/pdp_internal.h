@@ -68,8 +68,27 @@ __host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, int64_t pid
   return fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^ (uint32_t)seed);
 }
 
+#ifndef PDP_PAIR_HASH_VARIANT
+#define PDP_PAIR_HASH_VARIANT 0
+#endif
+__host__ __device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
+  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
+}
 __host__ __device__ __forceinline__ uint32_t pair_hash_from(uint32_t hpid, uint64_t seed, int64_t pk) {
+#if PDP_PAIR_HASH_VARIANT == 1
+  return fmix32(hpid ^ (uint32_t)pk ^ (uint32_t)(seed >> 32));
+#elif PDP_PAIR_HASH_VARIANT == 2
+  return hpid ^ (uint32_t)pk;
+#elif PDP_PAIR_HASH_VARIANT == 3
+  uint32_t h = hpid ^ umul24((uint32_t)pk ^ ((uint32_t)pk >> 24), 0x2B2AE3u) ^ (uint32_t)(seed >> 32);
+  h ^= h >> 16;
+  h = umul24(h, 0xEBCA6Bu);
+  h ^= h >> 13;
+  h = umul24(h, 0xB2AE35u);
+  return h ^ (h >> 16);
+#else
   return fmix32(hpid ^ ((uint32_t)pk * 0xC2B2AE3DU + (uint32_t)(seed >> 32)));
+#endif
 }
 
 __host__ __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {

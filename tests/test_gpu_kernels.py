@@ -234,13 +234,38 @@ def test_two_level_range_merge_matches_oracle(device, P, skew):
     _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
 
 
+@pytest.mark.parametrize("keys", [1, 2, 3], ids=["wide", "compact", "packed"])
+@pytest.mark.parametrize("public", [False, True])
+def test_tile_local_partition_matches_oracle(device, keys, public):
+    """The tile-local level 1 (stage blocks + per-stage super-bucket offsets,
+    bucket counts from its LDS) and the level 2 that gathers those runs, for
+    every record format: 23 tiles (two level-2 groups, a partial last stage),
+    37 super-buckets, a heavy privacy id, dead (non-public) rows."""
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(21 + keys)
+    n, U, P = 1_500_123, 300_000, 5_000
+    pid = rng.integers(0, U, n)
+    pid[:40_000] = 12_345
+    pk = np.minimum(rng.zipf(1.3, n) - 1, P - 1).astype(np.int64)
+    val = rng.normal(4.0, 3.0, n)
+    allowed = (np.arange(P) % 5 != 1) if public else None
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM,
+                          min_value=0.0, max_value=9.0, middle=4.5)
+    info = X.bound_plan(n, U, P, spec, 2, 2, keys)
+    assert info.algorithm == 2 and info.n_buckets > 64 and info.key_format == keys
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 71, allowed=allowed, algorithm=2, merge=2, key_format=keys)
+    want = _oracle(pid, pk, val, U, P, spec, 71, allowed=allowed, algorithm=2)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
+
+
 def test_compact_records_chosen_when_they_fit():
-    """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records; wider key
-    spaces fall back to the 12-byte (u64 key + row) format."""
+    """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records: PACKED
+    (one u64 per row) through the tile-local level 1, then COMPACT pairs; wider
+    key spaces fall back to the 12-byte (u64 key + row) format."""
     from pipelinedp_amd import executor as X
     spec = X.BoundingSpec(l0=8, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_NSUM, min_value=0.0,
                           max_value=10.0, middle=5.0)
-    assert X.bound_plan(100_000_000, 1_000_000, 100_000, spec).key_format == 2
+    assert X.bound_plan(100_000_000, 1_000_000, 100_000, spec).key_format == 3
     assert X.bound_plan(100_000_000, 1_000_000, 10_000_000, spec).key_format == 1
 
 

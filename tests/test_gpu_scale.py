@@ -150,7 +150,7 @@ def test_c2_full_scale_sampling_matches_oracle(device):
     pid, pk, val, U, P = _c2()
     spec = _spec(8, 2, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM)
     plan = _plan(len(pid), U, P, spec)
-    assert plan.algorithm == 2 and plan.key_format == 2  # the bench's plan: bucketed, compact records
+    assert plan.algorithm == 2 and plan.key_format == 3  # the bench's plan: bucketed, packed level-1 records
     got = _gpu(device, pid, pk, val, U, P, spec, 0xC2)
     want = _oracle(pid, pk, val, U, P, spec, 0xC2, plan.rand_shift)
     _compare(got, want, _scale(pk, val, P, spec))
