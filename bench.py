@@ -341,12 +341,14 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields):
     kb, rb = {N.KEYS_COMPACT: (4, 4), N.KEYS_WIDE: (8, 4), N.KEYS_PACKED: (8, 0)}.get(plan.key_format, (8, 4))
     rec = kb + rb
     pair_rec = 8 + 8 * n_fields
-    out = {"k_part_hist": 8.0 * n,
-           "k_scatter_l1": (16.0 + rec) * n,
+    # level 1 reads the two key columns and writes one record per row (the
+    # tile-local form needs no separate histogram pass over privacy ids)
+    out = {"k_scatter_l1": (16.0 + rec) * n,
            "k_scatter_l2": 2.0 * rec * n,
-           # B1 streams the keys, B2 the whole records; kept rows' values
+           # B1 streams the level-2 keys; kept rows' indices and values are
            # gathered; one record per kept pair out
-           "k_bucket_bound": kb * n + rec * n + 8.0 * kept_rows + pair_rec * kept_pairs,
+           "k_bucket_bound": (4.0 if plan.key_format != N.KEYS_WIDE else 8.0) * n + 12.0 * kept_rows
+                             + pair_rec * kept_pairs,
            "k_range_reduce": 2.0 * pair_rec * kept_pairs}
     return out
 
