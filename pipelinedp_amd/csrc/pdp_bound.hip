@@ -134,6 +134,15 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #ifndef PDP_L1_LOCAL
 #define PDP_L1_LOCAL 1
 #endif
+// tile-local level 2: all 16 loads per thread in flight (1) or two halves (0)
+#ifndef PDP_L2L_ALL
+#define PDP_L2L_ALL 0
+#endif
+// minimum waves per SIMD of the tile-local level 2 (4: two 512-thread
+// workgroups per CU within 128 VGPRs)
+#ifndef PDP_L2L_WAVES
+#define PDP_L2L_WAVES 4
+#endif
 #ifndef PDP_GATHER_VALUES
 #define PDP_GATHER_VALUES 1
 #endif
@@ -778,10 +787,14 @@ __device__ __forceinline__ uint64_t packed_key(const KP& kp, int64_t u, int64_t 
 // records are u32 (bit 31 dead), WIDE records u64 (bit 63 dead); both keep
 // the bucket-within-super bits above the local pid, which the key drops.
 __device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, uint32_t v) {
+  // COMPACT records have rand_shift = pk_bits + bucket_bits <= 31, so the
+  // pair key is the 32-bit pair hash above the record's (local pid,
+  // partition) bits -- the bucket-within-super bits above them dropped -- and
+  // pair_key_from's all-ones guard cannot fire
   if (v >> 31) return kEmpty;
-  const uint64_t local = (uint64_t)(v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1);
-  return pair_key_from(hpid[local], kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask), local << kp.pk_bits,
-                       kp.rand_shift);
+  const uint32_t local = (v >> kp.pk_bits) & ((1u << kp.bucket_bits) - 1);
+  return ((uint64_t)pair_hash_from(hpid[local], kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask)) << 32) |
+         (v & ((1u << kp.rand_shift) - 1));
 }
 __device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, unsigned long long v) {
   if (v >> 63) return kEmpty;
@@ -1177,7 +1190,7 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
 // records, so all of a thread's loads go out together.  Cursors as in
 // k_scatter_l2; PACKED rows are (stage / kStagesPerTile) * 65,536 + tile row.
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+__global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
                                                                    const unsigned* __restrict__ bucket_start,
                                                                    const unsigned* __restrict__ gcur,
                                                                    const L1Key<FMT>* __restrict__ keys1,
@@ -1244,6 +1257,49 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
       for (unsigned v = a + lane; v < e; v += 64) s.dest[v - base] = (D)(j - j0);
     }
     __syncthreads();
+#if PDP_L2L_ALL
+    // all of a thread's records in flight together; PACKED rows take their
+    // tile from the run map again after the loads (no per-item tile register)
+    KO x[kL2Items];
+    unsigned r[kL2Items];
+    int d[kL2Items];
+    KI raw[kL2Items];
+    unsigned rr[ROWS1 ? kL2Items : 1];
+    uint32_t live = 0;
+    static_assert(kL2Items <= 32, "item mask");
+#pragma unroll
+    for (int q = 0; q < kL2Items; ++q) {
+      const unsigned v = base + threadIdx.x + (unsigned)q * blockDim.x;
+      if (v < wend) {
+        const int j = j0 + (int)s.dest[v - base];
+        const unsigned i = rsrc[j] + (v - rbeg[j]);
+        live |= 1u << q;
+        raw[q] = keys1[i];
+        if constexpr (ROWS1) rr[q] = rows1[i];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kL2Items; ++q) {
+      d[q] = -1;
+      x[q] = 0;
+      r[q] = 0;
+      if (!((live >> q) & 1u)) continue;
+      if constexpr (PACKED) {
+        const unsigned v = base + threadIdx.x + (unsigned)q * blockDim.x;
+        const int j = j0 + (int)s.dest[v - base];
+        const uint64_t w = raw[q];
+        const uint32_t mid = (uint32_t)((w >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
+        d[q] = (int)(mid >> bb);
+        const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
+        x[q] = (KO)((w >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(w & kp.pk_mask)));
+        r[q] = (unsigned)(((S0 + j) / kStagesPerTile) * kTileRows) + (uint32_t)((w >> kPackedRowShift) & (kTileRows - 1));
+      } else {
+        x[q] = (KO)raw[q];
+        r[q] = rr[q];
+        d[q] = (int)((raw[q] >> sub_shift) & sub_mask);
+      }
+    }
+#else
     // records in two halves of loads in flight (register budget of two
     // workgroups per CU), unpacked into the counting sort's items
     KO x[kL2Items];
@@ -1287,6 +1343,7 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
         }
       }
     }
+#endif
     __syncthreads();  // the destination tags are rewritten by the counting sort
     unsigned rank[kL2Items];
     stage_count(s, nsub, d, rank);
