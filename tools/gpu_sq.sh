@@ -17,7 +17,7 @@ python3 tools/pmc_summary.py $OUT $OUT/sq.json "$TAG" > /dev/null
 python3 - $OUT/sq.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))["kernels"]
-for k in ("k_bucket_bound", "k_scatter_l1", "k_scatter_l2", "k_part_hist", "k_range_reduce"):
+for k in ("k_bucket_bound", "k_scatter_l1", "k_scatter_l2", "k_part_hist", "k_range_reduce"):  # (pmc_summary maps the _local kernels)
     if k in d:
         print(k, {c: "%.4g" % v for c, v in sorted(d[k]["counters_avg_per_launch"].items())})
 PY
