@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 6
+#define PDP_ABI_VERSION 7
 
 /* error codes */
 #define PDP_OK 0
@@ -99,10 +99,14 @@ typedef struct pdp_bound_config {
 #define PDP_KEYS_COMPACT 2 /* u32 (bucket-local pid, partition) + u32 row: 8 B per row and pass;
                               needs super/bucket/partition bits <= 31 (AUTO picks it then) */
 #define PDP_KEYS_PACKED 3  /* level 1: one u64 (row within its 65,536-row tile | bucket-local pid |
-                              partition), the tile recovered from the record's position; level 2
-                              on: the COMPACT pair.  8 B per row and pass where COMPACT does not
-                              fit: needs bucket + partition bits <= 31 and super + bucket +
-                              partition bits <= 47 (AUTO's second choice) */
+                              partition), the tile known from the stage block it was read from;
+                              level 2 on: the COMPACT pair.  8 B per row and pass: needs bucket +
+                              partition bits <= 31 and super + bucket + partition bits <= 47
+                              (AUTO's first choice with the tile-local level 1) */
+#define PDP_KEYS_PACKED_WIDE 4 /* level 1 PACKED (8 B), level 2 on WIDE (u64 key + u32 row):
+                              partition counts whose bucket + partition bits exceed 31 (C4/C5:
+                              P = 1e7) with super + bucket + partition bits <= 47; tile-local
+                              level 1 only (AUTO picks it there before WIDE) */
 
 /* per-partition merge of the kept pairs (BUCKETED; identical sums up to fp
  * summation order) */

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 6
+ABI_VERSION = 7
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 SELECT_ALL_NONEMPTY = 0
@@ -29,7 +29,7 @@ OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID 
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
 ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED, ALGO_PAIR_TABLE = 0, 1, 2, 3
 MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
-KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED = 0, 1, 2, 3
+KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED, KEYS_PACKED_WIDE = 0, 1, 2, 3, 4
 MAX_L0 = 2**31 - 1            # pipelinedp_amd.h PDP_MAX_*
 MAX_LINF = 2**31 - 1
 MAX_CONTRIBUTIONS = 2**31 - 1

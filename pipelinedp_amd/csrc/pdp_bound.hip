@@ -155,9 +155,15 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
-constexpr int64_t kL1HistMax = 8192;         // tile-local level 1: buckets counted in its LDS
-constexpr int64_t kL1LocalLds = 80 * 1024;   // ... and its LDS cap (two workgroups per CU)
+constexpr int64_t kL1LocalLds = 80 * 1024;   // tile-local level 1: LDS cap (two workgroups per CU)
 size_t l1_stage_bytes(int key_format);       // LDS of one level-1 stage (after StageLds)
+// tile-local level 1 bucket counts in LDS: u32 per bucket when they fit,
+// else two u16 per word, flushed every half tile (32,768 rows: no carry) to
+// counts_tm (first half) and counts_tm2 (second half)
+inline int64_t l1_hist_bytes(int64_t n_buckets, bool u16) { return ((u16 ? 2 : 4) * n_buckets + 15) / 16 * 16; }
+inline bool l1_hist_u16(int key_format, int64_t n_buckets) {
+  return (int64_t)l1_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) > kL1LocalLds;
+}
 
 struct Plan {
   int algorithm;   // PDP_ALGO_*
@@ -241,29 +247,36 @@ Plan make_plan(const pdp_bound_config* c) {
   const bool compact_ok = p.super_bits + p.bucket_bits + p.pk_bits <= 31;
   const bool packed_ok = p.bucket_bits + p.pk_bits <= 31 &&
                          p.super_bits + p.bucket_bits + p.pk_bits <= 64 - 1 - kTileRowBits;
+  // PACKED level 1 with WIDE records from level 2 on (tile-local level 1 only)
+  const bool packed_wide_ok = p.super_bits + p.bucket_bits + p.pk_bits <= 64 - 1 - kTileRowBits;
   p.key_format = 0;
-  if (p.algorithm == PDP_ALGO_BUCKETED) {
-    const int want = c->key_format;
-    if ((want == PDP_KEYS_COMPACT && !compact_ok) || (want == PDP_KEYS_PACKED && !packed_ok))
-      p.algorithm = -1;  // infeasible
-    else if (want != PDP_KEYS_AUTO)
-      p.key_format = want;
-    else
-      p.key_format = compact_ok ? PDP_KEYS_COMPACT : (packed_ok ? PDP_KEYS_PACKED : PDP_KEYS_WIDE);
-    // one super-bucket (no level 2): PACKED degenerates to COMPACT, which then fits
-    if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
-  }
   p.n_stages = (c->n_rows + kL1Rows - 1) / kL1Rows;
   p.l1_local = 0;
-  if (PDP_L1_LOCAL && p.algorithm == PDP_ALGO_BUCKETED && p.super_bits > 0 && p.n_buckets <= kL1HistMax) {
-    // tile-local level 1 prefers PACKED records to COMPACT ones: one u64
-    // array, so level 2 reads each run as one span
-    const int fmt = (c->key_format == PDP_KEYS_AUTO && p.key_format == PDP_KEYS_COMPACT && packed_ok)
-                        ? PDP_KEYS_PACKED : p.key_format;
-    if ((int64_t)l1_stage_bytes(fmt) + 4 * p.n_buckets <= kL1LocalLds) {
-      p.l1_local = 1;
-      p.key_format = fmt;
+  if (p.algorithm == PDP_ALGO_BUCKETED) {
+    // tile-local level 1: two levels, and the bucket counts in its LDS
+    auto local_fits = [&](int fmt) {
+      return PDP_L1_LOCAL && p.super_bits > 0 &&
+             (int64_t)l1_stage_bytes(fmt) + l1_hist_bytes(p.n_buckets, true) <= kL1LocalLds;
+    };
+    const int want = c->key_format;
+    if (want == PDP_KEYS_AUTO) {
+      // tile-local: PACKED (one u64 array at level 1, so level 2 reads each
+      // run as one span), else PACKED_WIDE; else COMPACT / PACKED / WIDE
+      if (packed_ok && local_fits(PDP_KEYS_PACKED))
+        p.key_format = PDP_KEYS_PACKED;
+      else if (!packed_ok && packed_wide_ok && local_fits(PDP_KEYS_PACKED_WIDE))
+        p.key_format = PDP_KEYS_PACKED_WIDE;
+      else
+        p.key_format = compact_ok ? PDP_KEYS_COMPACT : (packed_ok ? PDP_KEYS_PACKED : PDP_KEYS_WIDE);
+    } else if ((want == PDP_KEYS_COMPACT && !compact_ok) || (want == PDP_KEYS_PACKED && !packed_ok) ||
+               (want == PDP_KEYS_PACKED_WIDE && !(packed_wide_ok && local_fits(PDP_KEYS_PACKED_WIDE)))) {
+      p.algorithm = -1;  // infeasible
+    } else {
+      p.key_format = want;
     }
+    // one super-bucket (no level 2): PACKED degenerates to COMPACT, which then fits
+    if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
+    if (p.algorithm == PDP_ALGO_BUCKETED) p.l1_local = local_fits(p.key_format) ? 1 : 0;
   }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
@@ -296,6 +309,7 @@ struct Ws {
   uint64_t csum, gcur;  // level-2 cursor scans: per tile chunk, per tile group (x n_buckets)
   uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, record index)
   uint64_t soff;                // tile-local level 1: per stage, super-bucket run starts (u16)
+  uint64_t counts_tm2;          // tile-local level 1, u16 counts: second half-tile bucket counts
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -326,6 +340,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
+    if (p.l1_local && l1_hist_u16(p.key_format, p.n_buckets)) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     const uint64_t n_sc = ((uint64_t)p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
@@ -335,9 +350,9 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
     w.super_tm = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
     w.super_off = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
-    const bool packed = p.key_format == PDP_KEYS_PACKED && p.super_bits > 0;
+    const bool packed = (p.key_format == PDP_KEYS_PACKED || p.key_format == PDP_KEYS_PACKED_WIDE) && p.super_bits > 0;
     const uint64_t kb1 = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;  // level-1 key
-    const uint64_t kb2 = p.key_format == PDP_KEYS_WIDE ? 8 : 4;     // level-2 key
+    const uint64_t kb2 = (p.key_format == PDP_KEYS_WIDE || p.key_format == PDP_KEYS_PACKED_WIDE) ? 8 : 4;  // level-2 key
     const uint64_t n1 = p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n;  // level-1 records (stage blocks)
     w.keys1 = off; off = align256(off + n1 * (packed ? 8 : kb1));
     if (!packed) { w.rows1 = off; off = align256(off + n1 * 4); }
@@ -400,7 +415,7 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad algorithm");
   if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
     return set_error(PDP_E_INVALID, "bad merge");
-  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED)
+  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED_WIDE)
     return set_error(PDP_E_INVALID, "bad key_format");
   if (pairs_mode(c)) return pairs_validate(c);
   if (make_plan(c).algorithm < 0)
@@ -595,26 +610,34 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
 // (which also gives the bucket totals), and the cursors at group starts.
 // Level 2 then needs no atomics and writes every bucket's rows in tile order.
 
-__device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ counts_tm, int64_t n_tiles,
+// counts_tm2 (nullable): the tile-local level 1's second half-tile counts
+__device__ __forceinline__ unsigned tile_count(const unsigned* __restrict__ counts_tm,
+                                               const unsigned* __restrict__ counts_tm2, int64_t i) {
+  return counts_tm[i] + (counts_tm2 != nullptr ? counts_tm2[i] : 0u);
+}
+
+__device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ counts_tm,
+                                                  const unsigned* __restrict__ counts_tm2, int64_t n_tiles,
                                                   int64_t n_buckets, int64_t b, int64_t t0) {
   unsigned v = 0;
 #pragma unroll
   for (int j = 0; j < kScanTiles; ++j) {
     const int64_t t = t0 + j;
-    if (t < n_tiles && b < n_buckets) v += counts_tm[t * n_buckets + b];
+    if (t < n_tiles && b < n_buckets) v += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
   }
   return v;
 }
 
 // csum[chunk][b] = rows of bucket b in the chunk's tiles
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* __restrict__ counts_tm,
+                                                                 const unsigned* __restrict__ counts_tm2,
                                                                  int64_t n_tiles, int64_t n_buckets,
                                                                  unsigned* __restrict__ csum) {
   __shared__ unsigned part[kScanWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * 64 + lane;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  part[w][lane] = tile_slab_sum(counts_tm, n_tiles, n_buckets, b, t0);
+  part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
   __syncthreads();
   if (w == 0 && b < n_buckets) {
     unsigned v = 0;
@@ -639,6 +662,7 @@ __global__ void __launch_bounds__(kBlock) k_gscan_chunks(unsigned* __restrict__ 
 
 // gcur[g][b] = rows of bucket b in tiles < g * kL2GroupTiles
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigned* __restrict__ counts_tm,
+                                                                    const unsigned* __restrict__ counts_tm2,
                                                                     int64_t n_tiles, int64_t n_buckets,
                                                                     const unsigned* __restrict__ cpre,
                                                                     unsigned* __restrict__ gcur) {
@@ -646,7 +670,7 @@ __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigne
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * 64 + lane;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  part[w][lane] = tile_slab_sum(counts_tm, n_tiles, n_buckets, b, t0);
+  part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
   __syncthreads();
   if (b >= n_buckets || t0 >= n_tiles) return;
   unsigned run = cpre[(int64_t)blockIdx.y * n_buckets + b];
@@ -655,7 +679,7 @@ __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigne
     const int64_t t = t0 + j;
     if (t >= n_tiles) break;
     if (t % kL2GroupTiles == 0) gcur[(t / kL2GroupTiles) * n_buckets + b] = run;
-    run += counts_tm[t * n_buckets + b];
+    run += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
   }
 }
 
@@ -682,9 +706,11 @@ using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>:
 // level-1 record key per format (PACKED: the u64 packed record, no row array)
 template <int FMT>
 using L1Key = typename std::conditional<FMT == PDP_KEYS_COMPACT, uint32_t, unsigned long long>::type;
+template <int FMT>
+constexpr bool kPackedL1 = FMT == PDP_KEYS_PACKED || FMT == PDP_KEYS_PACKED_WIDE;  // no level-1 row array
 // level-2 (bucket-order) record key per format
 template <int FMT>
-using L2Key = RecKey<FMT != PDP_KEYS_WIDE>;
+using L2Key = RecKey<FMT != PDP_KEYS_WIDE && FMT != PDP_KEYS_PACKED_WIDE>;
 
 // MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
 // fits four workgroups per CU with compact keys instead of three.  ROWS:
@@ -704,7 +730,8 @@ constexpr int kSmallDest = 256;  // u8 tags; 39.9 KB with compact keys: four wor
 size_t l1_stage_bytes(int key_format) {
   switch (key_format) {
     case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kL1Items, kL1Threads>);
-    case PDP_KEYS_PACKED: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kL1Items, kL1Threads>);
+    case PDP_KEYS_PACKED:
+    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kL1Items, kL1Threads>);
     default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kL1Items, kL1Threads>);
   }
 }
@@ -1081,22 +1108,38 @@ __device__ __forceinline__ void copy_block(K* __restrict__ dst, const K* src, un
   for (unsigned k = nv * V + threadIdx.x; k < total; k += blockDim.x) dst[k] = src[k];
 }
 
-template <int FMT>
+template <int FMT, bool U16>
 __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP kp, const int64_t* __restrict__ pid,
                                                                    const int64_t* __restrict__ pk,
                                                                    const uint8_t* __restrict__ allowed,
                                                                    unsigned* __restrict__ counts_tm,
+                                                                   unsigned* __restrict__ counts_tm2,
                                                                    uint16_t* __restrict__ soff,
                                                                    L1Key<FMT>* __restrict__ keys1,
                                                                    unsigned* __restrict__ rows1, unsigned* err) {
   using K = L1Key<FMT>;
-  constexpr bool ROWS = FMT != PDP_KEYS_PACKED;
+  constexpr bool ROWS = !kPackedL1<FMT>;
   extern __shared__ unsigned long long stage_raw[];
   using SL = StageLds<K, kSmallDest, ROWS, kL1Items, kL1Threads>;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
-  unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);  // [n_buckets] rows per bucket
-  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) bh[b] = 0;
+  // rows per bucket: u32 each, or (U16) two u16 per word, flushed every half
+  // tile so that no count carries into its neighbour
+  unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);
+  const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
+  for (int64_t b = threadIdx.x; b < n_words; b += blockDim.x) bh[b] = 0;
   __syncthreads();
+  auto flush = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
+    for (int64_t wd = threadIdx.x; wd < n_words; wd += blockDim.x) {
+      const unsigned v = bh[wd];
+      bh[wd] = 0;
+      if constexpr (U16) {
+        dst[2 * wd] = v & 0xFFFFu;
+        if (2 * wd + 1 < kp.n_buckets) dst[2 * wd + 1] = v >> 16;
+      } else {
+        dst[wd] = v;
+      }
+    }
+  };
   const int64_t t = blockIdx.x;
   const int nd = (int)kp.n_supers;
   const int64_t t0 = t * kTileRows;
@@ -1123,6 +1166,8 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
     }
   };
   int64_t u[kL1Items], k[kL1Items];
+  // U16: the tile's counts in two halves (counts_tm, counts_tm2)
+  const bool split = U16 && t1 - t0 > (kStagesPerTile / 2 - 1) * kL1Rows;
   if (t0 < t1) load(t0, u, k);
   for (int64_t c0 = t0; c0 < t1; c0 += kL1Rows) {
     const int64_t st = c0 / kL1Rows;  // global stage index
@@ -1140,7 +1185,9 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
         atomicOr(err, 1u);
         continue;
       }
-      atomicAdd(bh + (u[q] >> kp.bucket_bits), 1u);
+      const int64_t bkt = u[q] >> kp.bucket_bits;
+      if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+      else atomicAdd(bh + bkt, 1u);
       d[q] = (int)(u[q] >> mid_bits);
       bool is_dead = false;
       if (k[q] < 0 || k[q] >= kp.P) {
@@ -1151,7 +1198,7 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
       }
       if constexpr (FMT == PDP_KEYS_COMPACT) {
         x[q] = (K)compact_key(kp, u[q], k[q], is_dead);
-      } else if constexpr (FMT == PDP_KEYS_PACKED) {
+      } else if constexpr (kPackedL1<FMT>) {
         x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), is_dead);
       } else {
         const uint64_t midv = ((uint64_t)u[q] & mid_mask) << kp.pk_bits;
@@ -1175,10 +1222,20 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
       soff[st * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] : total);
     __syncthreads();
     if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
+    if (split && c0 - t0 == (kStagesPerTile / 2 - 1) * kL1Rows) {  // first half tile done
+      flush(counts_tm + t * kp.n_buckets);
+      __syncthreads();
+    }
   }
   __syncthreads();
-  unsigned* row = counts_tm + t * kp.n_buckets;  // tile-major: coalesced
-  for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) row[b] = bh[b];
+  // tile-major rows: coalesced.  Counts of a half tile never reach 2^16
+  if (split) {
+    flush(counts_tm2 + t * kp.n_buckets);
+  } else {
+    flush(counts_tm + t * kp.n_buckets);
+    if constexpr (U16)
+      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.n_buckets + b] = 0;
+  }
 }
 
 // Level 2 over tile-local level-1 blocks: workgroup (group g of kL2GroupTiles
@@ -1189,8 +1246,21 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
 // before the counting sort reuses it) lets each thread address its own
 // records, so all of a thread's loads go out together.  Cursors as in
 // k_scatter_l2; PACKED rows are (stage / kStagesPerTile) * 65,536 + tile row.
+// level-2 key of a packed level-1 record w (bit 63 dead): COMPACT u32
+// (bit 31 dead | local pid | partition) or, PACKED_WIDE, the same fields in a u64
+template <typename KO>
+__device__ __forceinline__ KO unpacked_key(const KP& kp, uint32_t local, uint64_t w) {
+  if constexpr (sizeof(KO) == 4) {
+    const uint32_t lpk = local << kp.pk_bits;
+    return (KO)((w >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(w & kp.pk_mask)));
+  } else {
+    const uint64_t lpk = (uint64_t)local << kp.pk_bits;
+    return (KO)((w >> 63) ? ((1ULL << 63) | lpk) : (lpk | (w & kp.pk_mask)));
+  }
+}
+
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+__global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
                                                                    const unsigned* __restrict__ bucket_start,
                                                                    const unsigned* __restrict__ gcur,
                                                                    const L1Key<FMT>* __restrict__ keys1,
@@ -1199,7 +1269,7 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
                                                                    unsigned* __restrict__ rows2) {
   using KI = L1Key<FMT>;
   using KO = L2Key<FMT>;
-  constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
+  constexpr bool PACKED = kPackedL1<FMT>;  // PACKED / PACKED_WIDE level-1 records
   constexpr bool ROWS1 = !PACKED;
   extern __shared__ unsigned long long stage_raw[];
   using SL = StageLds<KO, MAXD, true, kL2Items, kL2Threads>;
@@ -1290,8 +1360,7 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
         const uint64_t w = raw[q];
         const uint32_t mid = (uint32_t)((w >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
         d[q] = (int)(mid >> bb);
-        const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
-        x[q] = (KO)((w >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(w & kp.pk_mask)));
+        x[q] = unpacked_key<KO>(kp, mid & local_mask, w);
         r[q] = (unsigned)(((S0 + j) / kStagesPerTile) * kTileRows) + (uint32_t)((w >> kPackedRowShift) & (kTileRows - 1));
       } else {
         x[q] = (KO)raw[q];
@@ -1333,8 +1402,7 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
           const uint64_t v = raw[q];
           const uint32_t mid = (uint32_t)((v >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
           d[h + q] = (int)(mid >> bb);
-          const uint32_t lpk = ((mid & local_mask) << kp.pk_bits);
-          x[h + q] = (KO)((v >> 63) ? (0x80000000u | lpk) : (lpk | (uint32_t)(v & kp.pk_mask)));
+          x[h + q] = unpacked_key<KO>(kp, mid & local_mask, v);
           r[h + q] = rr[q] + (uint32_t)((v >> kPackedRowShift) & (kTileRows - 1));
         } else {
           x[h + q] = (KO)raw[q];
@@ -2295,7 +2363,8 @@ template <int VK, bool KA>
 int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w, const void* value,
                   const pdp_partition_accumulators& acc) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
-  const bool compact = p.key_format != PDP_KEYS_WIDE;  // PACKED: COMPACT records from level 2 on
+  // PACKED: COMPACT records from level 2 on; PACKED_WIDE: WIDE ones
+  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
   const void* kern = compact ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, true>
                                        : (const void*)k_bucket_bound<VK, KA, false, true>)
                              : (ranges ? (const void*)k_bucket_bound<VK, KA, true, false>
@@ -2425,18 +2494,21 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
                  const uint8_t* allowed, char* ws, const Ws& w, unsigned* err) {
   using K1 = L1Key<FMT>;
   using K2 = L2Key<FMT>;
-  constexpr bool ROWS1 = FMT != PDP_KEYS_PACKED;
+  constexpr bool ROWS1 = !kPackedL1<FMT>;
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
+  const bool u16 = l1_hist_u16(FMT, p.n_buckets);
+  unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
   K1* keys1 = (K1*)(ws + w.keys1);
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
-  const size_t lds1 = l1_stage_bytes(FMT) + ((size_t)p.n_buckets * 4 + 7) / 8 * 8 + 8;
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter_l1_local<FMT>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+  const size_t lds1 = (l1_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
+  const void* l1 = u16 ? (const void*)k_scatter_l1_local<FMT, true> : (const void*)k_scatter_l1_local<FMT, false>;
+  PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+  void* args1[] = {(void*)&kp,         (void*)&pid,  (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
+                   (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err};
   PDP_PROF_BEGIN("k_scatter_l1", st);
-  hipLaunchKernelGGL(k_scatter_l1_local<FMT>, dim3((unsigned)p.n_tiles), dim3(kL1Threads), lds1, st, kp, pid, pk,
-                     allowed, counts_tm, soff, keys1, rows1, err);
+  PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   const int64_t n_bblk = (p.n_buckets + 63) / 64;
@@ -2445,7 +2517,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
   hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     p.n_tiles, p.n_buckets, csum);
+                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, csum);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -2455,7 +2527,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_cursors", st);
   hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
-                     counts_tm, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+                     counts_tm, (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   const int rc = scan_u32(counts, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);
@@ -2611,6 +2683,8 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
       return launch_local<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
     if (p.key_format == PDP_KEYS_PACKED)
       return launch_local<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    if (p.key_format == PDP_KEYS_PACKED_WIDE)
+      return launch_local<PDP_KEYS_PACKED_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
     return launch_local<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   }
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
@@ -2636,7 +2710,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
   hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     p.n_tiles, p.n_buckets, csum);
+                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -2647,7 +2721,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   if (p.super_bits > 0) {
     PDP_PROF_BEGIN("k_gscan_cursors", st);
     hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
-                       counts_tm, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+                       counts_tm, (const unsigned*)nullptr, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }

@@ -146,7 +146,7 @@ def test_workspace_bytes(lib):
     ("max_contributions", -1, -4, b"max_contributions"),
     ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
     ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
-    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 4, -1, b"key_format"),
+    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 5, -1, b"key_format"),
 ])
 def test_invalid_configs_are_rejected(lib, field, value, code, msg):
     info = N.BoundPlanInfo()

@@ -276,6 +276,25 @@ def test_c4_shape_matches_oracle_with_selection_and_noise(device):
     np.testing.assert_allclose(out.cpu().numpy()[:, :n_kept], wm, rtol=1e-9, atol=1e-9)
 
 
+def test_c4_bucketing_packed_wide_records_match_oracle(device):
+    """C4's per-GPU bucketing (U = 1.25e7 privacy ids -> 12,208 buckets of
+    1,024, P = 1e7): PACKED level-1 records and WIDE ones from level 2 on
+    (bucket + partition bits > 31), the tile-local level 1 counting buckets in
+    u16 halves; 2e7 rows against the oracle, sampling firing."""
+    rng = np.random.default_rng(44)
+    n, U, P = 20_000_000, 12_500_000, 10_000_000
+    pid = rng.integers(0, U, n)
+    pid[:300_000] = rng.integers(0, 2_000, 300_000)  # a few heavy privacy ids
+    pk = rng.integers(0, P, n)
+    val = rng.random(n) * 10.0
+    spec = _spec(4, 2, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2)
+    plan = _plan(n, U, P, spec)
+    assert plan.algorithm == 2 and plan.key_format == 4 and plan.n_buckets > 10_000
+    got = _gpu(device, pid, pk, val, U, P, spec, 0x4C4)
+    want = _oracle(pid, pk, val, U, P, spec, 0x4C4, plan.rand_shift)
+    _compare(got, want, _scale(pk, val, P, spec))
+
+
 # ---------------------------------------------------------------------- C5 --
 @pytest.mark.timeout(900)
 def test_c5_shape_heavy_tailed_privacy_ids_match_oracle(device):
