@@ -31,6 +31,7 @@
 //  GLOBAL (fallback for large l0 * linf)
 //    k_pair_sketch / k_pair_rows / k_reduce_pairs: the same sketches in HBM,
 //    updated with device-scope atomics.
+#include <algorithm>
 #include <type_traits>
 
 #include "pdp_internal.h"
@@ -47,7 +48,7 @@ constexpr int kPartThreads = 512;
 #define PDP_L2_ITEMS 16
 #endif
 #ifndef PDP_L1_THREADS
-#define PDP_L1_THREADS 512
+#define PDP_L1_THREADS 1024
 #endif
 constexpr int kL1Threads = PDP_L1_THREADS;
 constexpr int kL1Items = PDP_L1_ITEMS;
@@ -87,7 +88,11 @@ constexpr int kBucketThreads = PDP_BUCKET_THREADS;
 constexpr int64_t kLdsBudget = PDP_LDS_BUDGET_KB * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
-constexpr int kMaxSupers = 64;               // destinations of a level-1 scatter
+#ifndef PDP_MAX_SUPERS
+#define PDP_MAX_SUPERS 128
+#endif
+constexpr int kMaxSupers = PDP_MAX_SUPERS;   // destinations of a level-1 scatter
+constexpr int64_t kSingleLevelMax = 64;      // buckets partitioned by one level
 constexpr int kRangeBits = 11;                // partitions per merge range = 2048
 constexpr int kRangeParts = 1 << kRangeBits;
 constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= one block scan
@@ -155,7 +160,10 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
-constexpr int64_t kL1LocalLds = 80 * 1024;   // tile-local level 1: LDS cap (two workgroups per CU)
+#ifndef PDP_L1_LOCAL_LDS_KB
+#define PDP_L1_LOCAL_LDS_KB 150
+#endif
+constexpr int64_t kL1LocalLds = PDP_L1_LOCAL_LDS_KB * 1024;  // tile-local level 1: LDS cap (one 1,024-thread workgroup per CU)
 size_t l1_stage_bytes(int key_format);       // LDS of one level-1 stage (after StageLds)
 // tile-local level 1 bucket counts in LDS: u32 per bucket when they fit,
 // else two u16 per word, flushed every half tile (32,768 rows: no carry) to
@@ -206,7 +214,23 @@ Plan make_plan(const pdp_bound_config* c) {
     const int u_bits = bits_for(c->n_privacy_ids);
     if (s > u_bits) s = u_bits;                          // one bucket covers all pids
     const int64_t nb = (c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s;
-    while (((nb + ((int64_t)1 << s2) - 1) >> s2) > kMaxSupers) ++s2;
+    if (nb > kSingleLevelMax) {
+      // two levels: level 2's input runs are a stage's rows of one
+      // super-bucket (kL1Rows / supers), its output runs a window's rows of
+      // one bucket (kL2Rows / 2^s2); take the s2 whose shorter run is longest
+      // (C3: 77 supers x 64 buckets, C2: 62 x 32)
+      int lo = 1;
+      while (((nb + ((int64_t)1 << lo) - 1) >> lo) > kMaxSupers) ++lo;
+      double best = -1.0;
+      for (int c = lo; c <= lo + 3 && ((int64_t)1 << c) < nb; ++c) {
+        const double supers = (double)((nb + ((int64_t)1 << c) - 1) >> c);
+        const double score = std::min((double)kL1Rows / supers, (double)kL2Rows / (double)((int64_t)1 << c));
+        if (score > best) {
+          best = score;
+          s2 = c;
+        }
+      }
+    }
     // pair keys: random bits above rand_shift = pk_bits + bucket_bits
     if (nb > kMaxBuckets || 64 - p.pk_bits - s < kMinRandomBits) s = -1;
   }
