@@ -72,7 +72,10 @@ constexpr int kL2Rows = kL2Threads * kL2Items;  // records per level-2 LDS stage
 #endif
 constexpr int kL2GroupTiles = PDP_L2_GROUP;
 constexpr int kScanWaves = 16;
-constexpr int kScanTiles = 16;  // tiles per wave in the level-2 cursor scans; multiple of kL2GroupTiles
+#ifndef PDP_SCAN_TILES
+#define PDP_SCAN_TILES 16
+#endif
+constexpr int kScanTiles = PDP_SCAN_TILES;  // tiles per wave in the level-2 cursor scans; multiple of kL2GroupTiles
 constexpr int kScanChunkTiles = kScanWaves * kScanTiles;
 static_assert(kScanTiles % kL2GroupTiles == 0, "group starts must fall inside a wave's tiles");
 constexpr int kTileRowBits = 16;
@@ -147,6 +150,11 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 // workgroups per CU within 128 VGPRs)
 #ifndef PDP_L2L_WAVES
 #define PDP_L2L_WAVES 4
+#endif
+// B1 candidate test against a per-pid 32-bit threshold kept beside the pid
+// hash (one LDS read per record) instead of the 64-bit sketch maximum
+#ifndef PDP_B1_THR
+#define PDP_B1_THR 1
 #endif
 #ifndef PDP_GATHER_VALUES
 #define PDP_GATHER_VALUES 1
@@ -304,7 +312,7 @@ Plan make_plan(const pdp_bound_config* c) {
   }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
-    p.lds_bytes += ((int64_t)4 << p.bucket_bits);
+    p.lds_bytes += ((int64_t)8 << p.bucket_bits);  // {pid hash, sketch-maximum high half} per pid
   }
   if (p.merge == PDP_MERGE_RANGES) {
     // range r yields ceil(records_r / C) items + 1 sentinel, and a bucket
@@ -837,20 +845,38 @@ __device__ __forceinline__ uint64_t packed_key(const KP& kp, int64_t u, int64_t 
 // holds pid_hash of the bucket's 2^bucket_bits privacy ids (LDS).  COMPACT
 // records are u32 (bit 31 dead), WIDE records u64 (bit 63 dead); both keep
 // the bucket-within-super bits above the local pid, which the key drops.
-__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, uint32_t v) {
+__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint2* hpid, uint32_t v) {
   // COMPACT records have rand_shift = pk_bits + bucket_bits <= 31, so the
   // pair key is the 32-bit pair hash above the record's (local pid,
   // partition) bits -- the bucket-within-super bits above them dropped -- and
   // pair_key_from's all-ones guard cannot fire
   if (v >> 31) return kEmpty;
   const uint32_t local = (v >> kp.pk_bits) & ((1u << kp.bucket_bits) - 1);
-  return ((uint64_t)pair_hash_from(hpid[local], kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask)) << 32) |
+  return ((uint64_t)pair_hash_from(hpid[local].x, kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask)) << 32) |
          (v & ((1u << kp.rand_shift) - 1));
 }
-__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint32_t* hpid, unsigned long long v) {
+__device__ __forceinline__ uint64_t expand_key(const KP& kp, const uint2* hpid, unsigned long long v) {
   if (v >> 63) return kEmpty;
   const uint64_t local = (v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1);
-  return pair_key_from(hpid[local], kp.seed, (int64_t)(v & kp.pk_mask), local << kp.pk_bits, kp.rand_shift);
+  return pair_key_from(hpid[local].x, kp.seed, (int64_t)(v & kp.pk_mask), local << kp.pk_bits, kp.rand_shift);
+}
+
+// B1's candidate test in one LDS read: hpid[local] = {pid hash, high 32 bits
+// of the pid's sketch maximum (or above it: the maximum only decreases)}; a
+// record whose key's high half exceeds that cannot be at or below the
+// maximum.  Returns the pair key of a candidate, kEmpty otherwise.
+__device__ __forceinline__ uint64_t b1_candidate(const KP& kp, const uint2* hpid, uint32_t v) {
+  if (v >> 31) return kEmpty;
+  const uint32_t local = (v >> kp.pk_bits) & ((1u << kp.bucket_bits) - 1);
+  const uint2 e = hpid[local];
+  const uint32_t h = pair_hash_from(e.x, kp.seed, (int64_t)(v & (uint32_t)kp.pk_mask));
+  return h <= e.y ? (((uint64_t)h << 32) | (v & ((1u << kp.rand_shift) - 1))) : kEmpty;
+}
+__device__ __forceinline__ uint64_t b1_candidate(const KP& kp, const uint2* hpid, unsigned long long v) {
+  const uint64_t x = expand_key(kp, hpid, v);
+  if (x == kEmpty) return kEmpty;
+  const uint32_t local = (uint32_t)((v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1));
+  return (uint32_t)(x >> 32) <= hpid[local].y ? x : kEmpty;
 }
 
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
@@ -1666,9 +1692,11 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int wave = threadIdx.x >> 6;
   const WaveQueue wq{qbase + wave * kQueueCap,
                      (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
-  // pid_hash of the bucket's privacy ids, after the queues (expand_key)
-  uint32_t* hpid = (uint32_t*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap;
-  for (int64_t t = threadIdx.x; t < S; t += blockDim.x) hpid[t] = pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t);
+  // per privacy id of the bucket, after the queues: {pid_hash (expand_key),
+  // high half of its sketch maximum (b1_candidate)}
+  uint2* hpid = (uint2*)((unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap);
+  for (int64_t t = threadIdx.x; t < S; t += blockDim.x)
+    hpid[t] = make_uint2(pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t), 0xFFFFFFFFu);
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
@@ -1697,21 +1725,31 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   __syncthreads();
   const uint64_t lbits = ((uint64_t)1 << (kp.pk_bits + kp.bucket_bits)) - 1;  // local pid | partition
   stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, kRowIndex>(
-      keys, rowidx, begin, end, wq, conv,
+      keys, rowidx, begin, end, wq,
+#if PDP_B1_THR
+      // the candidate test rides on the pid-hash read (b1_candidate)
+      [&](RecKey<COMPACT> v) -> uint64_t { return b1_candidate(kp, hpid, v); },
+      [&](uint64_t x) { return x != kEmpty; },
+#else
+      conv,
       [&](uint64_t x) {
-#ifdef PDP_ABL_B1_NOPRED
-        return x == 0;
-#endif
         return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
       },
+#endif
       [&](uint64_t x, uint32_t i) PDP_WORK_ATTR {
-        unsigned long long* s = sk + ((x >> kp.pk_bits) & bmask);
+        const int64_t pl = (int64_t)((x >> kp.pk_bits) & bmask);
+        unsigned long long* s = sk + pl;
 #if PDP_INSERT_SKIP
         if (x < s[(l0 - 1) * S]) sketch_insert_strided_skip(s, l0, S, x);
 #else
         if (x < s[(l0 - 1) * S]) sketch_insert_strided(s, l0, S, x);
 #endif
-        const bool keep = x <= s[(l0 - 1) * S];
+        const unsigned long long smax = s[(l0 - 1) * S];
+#if PDP_B1_THR
+        // a maximum read after this insert: never below the current one
+        hpid[pl].y = (uint32_t)(smax >> 32);
+#endif
+        const bool keep = x <= smax;
         const unsigned long long active = __ballot(true);
         const unsigned long long m = __ballot(keep);
         const int leader = __ffsll((long long)active) - 1;
