@@ -258,6 +258,48 @@ def test_tile_local_partition_matches_oracle(device, keys, public):
     _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
 
 
+@pytest.mark.parametrize("n", [1, 1000, 65_535, 65_537, 8 * 65_536 + 8_191])
+def test_tile_local_partition_edge_sizes(device, n):
+    """Tile-local partition passes at sizes around their stage / tile /
+    level-2 group boundaries, with many more buckets than rows (empty runs)."""
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(n)
+    U, P = 300_000, 5_000
+    pid = rng.integers(0, U, n)
+    pk = rng.integers(0, P, n)
+    val = rng.normal(4.0, 3.0, n)
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM,
+                          min_value=0.0, max_value=9.0, middle=4.5)
+    info = X.bound_plan(n, U, P, spec)
+    assert info.algorithm == 2 and info.n_buckets > 64 and info.key_format == 3
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 5)
+    want = _oracle(pid, pk, val, U, P, spec, 5)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
+
+
+def test_tile_local_partition_unaligned_columns(device):
+    """Key columns that do not start on a 16-byte boundary (views one element
+    in) take the scalar-load path of level 1."""
+    import torch
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(17)
+    n, U, P = 700_001, 300_000, 5_000
+    pid = rng.integers(0, U, n + 1)
+    pk = rng.integers(0, P, n + 1)
+    val = rng.normal(4.0, 3.0, n + 1)
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_SUM | O.ACC_NSUM,
+                          min_value=0.0, max_value=9.0, middle=4.5)
+    tp = torch.as_tensor(pid).to(device)[1:]
+    tk = torch.as_tensor(pk).to(device)[1:]
+    tv = torch.as_tensor(val).to(device)[1:]
+    assert tp.data_ptr() % 16 != 0
+    acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=9)
+    torch.cuda.synchronize()
+    got = {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+    want = _oracle(pid[1:], pk[1:], val[1:], U, P, spec, 9)
+    _compare(got, want, _abs_scale(pid[1:], pk[1:], val[1:], P, 0.0, 9.0, 4.5))
+
+
 def test_compact_records_chosen_when_they_fit():
     """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records: PACKED
     (one u64 per row) through the tile-local level 1, then COMPACT pairs; at
