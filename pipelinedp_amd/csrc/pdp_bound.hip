@@ -1309,8 +1309,14 @@ __device__ __forceinline__ KO unpacked_key(const KP& kp, uint32_t local, uint64_
   }
 }
 
+// tile-local level 2 records per thread: half for 8-byte level-2 keys
+// (WIDE / PACKED_WIDE), so their LDS windows and registers leave room for two
+// workgroups per CU
+template <int FMT>
+constexpr int l2_items() { return sizeof(L2Key<FMT>) == 8 ? kL2Items / 2 : kL2Items; }
+
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+__global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
                                                                    const unsigned* __restrict__ bucket_start,
                                                                    const unsigned* __restrict__ gcur,
                                                                    const L1Key<FMT>* __restrict__ keys1,
@@ -1319,10 +1325,12 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
                                                                    unsigned* __restrict__ rows2) {
   using KI = L1Key<FMT>;
   using KO = L2Key<FMT>;
+  constexpr int NI = l2_items<FMT>();  // records per thread and window
+  constexpr int NR = kL2Threads * NI;
   constexpr bool PACKED = kPackedL1<FMT>;  // PACKED / PACKED_WIDE level-1 records
   constexpr bool ROWS1 = !PACKED;
   extern __shared__ unsigned long long stage_raw[];
-  using SL = StageLds<KO, MAXD, true, kL2Items, kL2Threads>;
+  using SL = StageLds<KO, MAXD, true, NI, kL2Threads>;
   using D = typename SL::D;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
   __shared__ unsigned rbeg[kL2Runs + 1];  // start of each run in the concatenation
@@ -1368,8 +1376,8 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
   const uint64_t sub_mask = (uint64_t)nsub - 1;
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   int j0 = 0;  // first run overlapping the window (block-uniform)
-  for (unsigned base = 0; base < total; base += kL2Rows) {
-    const unsigned wend = base + kL2Rows < total ? base + kL2Rows : total;
+  for (unsigned base = 0; base < total; base += NR) {
+    const unsigned wend = base + NR < total ? base + NR : total;
     while (rbeg[j0 + 1] <= base) ++j0;
     for (int j = j0 + (int)(threadIdx.x >> 6); j < nr && rbeg[j] < wend; j += nw) {
       const unsigned a = rbeg[j] > base ? rbeg[j] : base;
@@ -1380,15 +1388,15 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
 #if PDP_L2L_ALL
     // all of a thread's records in flight together; PACKED rows take their
     // tile from the run map again after the loads (no per-item tile register)
-    KO x[kL2Items];
-    unsigned r[kL2Items];
-    int d[kL2Items];
-    KI raw[kL2Items];
-    unsigned rr[ROWS1 ? kL2Items : 1];
+    KO x[NI];
+    unsigned r[NI];
+    int d[NI];
+    KI raw[NI];
+    unsigned rr[ROWS1 ? NI : 1];
     uint32_t live = 0;
-    static_assert(kL2Items <= 32, "item mask");
+    static_assert(NI <= 32, "item mask");
 #pragma unroll
-    for (int q = 0; q < kL2Items; ++q) {
+    for (int q = 0; q < NI; ++q) {
       const unsigned v = base + threadIdx.x + (unsigned)q * blockDim.x;
       if (v < wend) {
         const int j = j0 + (int)s.dest[v - base];
@@ -1399,7 +1407,7 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
       }
     }
 #pragma unroll
-    for (int q = 0; q < kL2Items; ++q) {
+    for (int q = 0; q < NI; ++q) {
       d[q] = -1;
       x[q] = 0;
       r[q] = 0;
@@ -1421,12 +1429,12 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
 #else
     // records in two halves of loads in flight (register budget of two
     // workgroups per CU), unpacked into the counting sort's items
-    KO x[kL2Items];
-    unsigned r[kL2Items];
-    int d[kL2Items];
-    constexpr int H = kL2Items / 2;
+    KO x[NI];
+    unsigned r[NI];
+    int d[NI];
+    constexpr int H = NI / 2;
 #pragma unroll
-    for (int h = 0; h < kL2Items; h += H) {
+    for (int h = 0; h < NI; h += H) {
       KI raw[H];
       unsigned rr[H];  // PACKED: the record's tile's first row; else its row
       bool live[H];
@@ -1463,7 +1471,7 @@ __global__ void __launch_bounds__(kL2Threads, sizeof(L2Key<FMT>) == 8 ? 1 : PDP_
     }
 #endif
     __syncthreads();  // the destination tags are rewritten by the counting sort
-    unsigned rank[kL2Items];
+    unsigned rank[NI];
     stage_count(s, nsub, d, rank);
     stage_write(s, nsub, d, rank, x, r, keys2, rows2);
     for (int t = threadIdx.x; t < nsub; t += blockDim.x) s.gcur[t] += s.hist[t];
@@ -2598,8 +2606,8 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
   const void* l2 = small ? (const void*)k_scatter_l2_local<FMT, kSmallDest>
                          : (const void*)k_scatter_l2_local<FMT, kMaxDest>;
-  const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, kL2Items, kL2Threads>)
-                            : sizeof(StageLds<K2, kMaxDest, true, kL2Items, kL2Threads>);
+  const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, l2_items<FMT>(), kL2Threads>)
+                            : sizeof(StageLds<K2, kMaxDest, true, l2_items<FMT>(), kL2Threads>);
   PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
   const uint16_t* soff_c = soff;
   const unsigned* counts_c = counts;
