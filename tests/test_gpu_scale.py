@@ -295,6 +295,25 @@ def test_c4_bucketing_packed_wide_records_match_oracle(device):
     _compare(got, want, _scale(pk, val, P, spec))
 
 
+def test_many_buckets_wide_level2_fanout_matches_oracle(device):
+    """34,180 buckets (U = 7e7 privacy ids, 2,048 per bucket): level 1 counts
+    them in u16 halves and level 2 fans each super-bucket out to 512 buckets
+    (the 1,024-destination LDS stage); 3e6 rows, mostly one per privacy id,
+    plus a heavy id, against the oracle."""
+    rng = np.random.default_rng(34)
+    n, U, P = 3_000_000, 70_000_000, 100_000
+    pid = rng.integers(0, U, n)
+    pid[:50_000] = 123_456_789 % U
+    pk = _zipf_pk(rng, n, P, 1.1)
+    val = rng.random(n) * 10.0
+    spec = _spec(2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM)
+    plan = _plan(n, U, P, spec)
+    assert plan.algorithm == 2 and plan.key_format == 3 and plan.n_buckets > 32_768
+    got = _gpu(device, pid, pk, val, U, P, spec, 0x34)
+    want = _oracle(pid, pk, val, U, P, spec, 0x34, plan.rand_shift)
+    _compare(got, want, _scale(pk, val, P, spec))
+
+
 # ---------------------------------------------------------------------- C5 --
 @pytest.mark.timeout(900)
 def test_c5_shape_heavy_tailed_privacy_ids_match_oracle(device):
