@@ -43,19 +43,24 @@ def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None):
         raise ValueError(f"accumulator length {padded} is not a multiple of world size {world}")
     slice_len = padded // world
     backend = dist.get_backend(group)
-    out = {}
+    # one collective per dtype: the fields of a dtype are interleaved rank-major
+    # ([rank][field][slice]) so that rank r's chunk of the sum is its slices of
+    # every field
+    out = {name: None for name in acc}
+    by_dtype = {}
     for name, t in acc.items():
-        if t is None:
-            out[name] = None
-            continue
+        if t is not None:
+            by_dtype.setdefault(t.dtype, []).append(name)
+    for dtype, names in by_dtype.items():
+        stacked = torch.stack([acc[n].reshape(world, slice_len) for n in names], dim=1).contiguous()
         if backend == "nccl":
-            part = torch.empty(slice_len, dtype=t.dtype, device=t.device)
-            dist.reduce_scatter_tensor(part, t.contiguous(), op=dist.ReduceOp.SUM, group=group)
-        else:  # gloo (CPU tests): all-reduce then keep the owned slice
-            full = t.clone()
-            dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
-            part = full[rank * slice_len:(rank + 1) * slice_len].clone()
-        out[name] = part
+            part = torch.empty((len(names), slice_len), dtype=dtype, device=stacked.device)
+            dist.reduce_scatter_tensor(part.view(-1), stacked.view(-1), op=dist.ReduceOp.SUM, group=group)
+        else:  # gloo (CPU tests): all-reduce then keep the owned chunk
+            dist.all_reduce(stacked, op=dist.ReduceOp.SUM, group=group)
+            part = stacked[rank].clone()
+        for i, n in enumerate(names):
+            out[n] = part[i]
     return out, rank * slice_len
 
 
