@@ -548,9 +548,18 @@ def main():
         cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
     import torch
     import torch.distributed as dist
+    # PDP_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
+    # the visible GPUs round-robin (e.g. two ranks on a one-GPU box); the
+    # measured configuration is RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("PDP_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local_rank)
 
     if args.workload in ("c4", "c5"):
