@@ -74,6 +74,9 @@ EPS, DELTA = 1.0, 1e-6
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--privacy-ids", type=int, default=0,
+                    help="C3 privacy ids in total (default: the config's 1e7); with --rows, one rank's "
+                         "share of an N-GPU run on one GPU")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5"), default="c3")
@@ -400,7 +403,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     if workload == "c3":
         total = args.rows or C3["rows"]
         n = total // world
-        U = C3["privacy_ids"] // world
+        U = (args.privacy_ids or C3["privacy_ids"]) // world
         P = C3["partitions"]
         bounding, selection, ops = build_plan(C3["l0"], C3["linf"])
         pid, pk, value = gen_c3(n, U, P, rank, world, device, 2000)
