@@ -142,10 +142,6 @@ constexpr int kQueueCap = 128;                // per-wave candidate queue (bucke
 #ifndef PDP_L1_LOCAL
 #define PDP_L1_LOCAL 1
 #endif
-// tile-local level 2: all 16 loads per thread in flight (1) or two halves (0)
-#ifndef PDP_L2L_ALL
-#define PDP_L2L_ALL 0
-#endif
 // minimum waves per SIMD of the tile-local level 2 (4: two 512-thread
 // workgroups per CU within 128 VGPRs)
 #ifndef PDP_L2L_WAVES
@@ -1385,48 +1381,6 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
       for (unsigned v = a + lane; v < e; v += 64) s.dest[v - base] = (D)(j - j0);
     }
     __syncthreads();
-#if PDP_L2L_ALL
-    // all of a thread's records in flight together; PACKED rows take their
-    // tile from the run map again after the loads (no per-item tile register)
-    KO x[NI];
-    unsigned r[NI];
-    int d[NI];
-    KI raw[NI];
-    unsigned rr[ROWS1 ? NI : 1];
-    uint32_t live = 0;
-    static_assert(NI <= 32, "item mask");
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      const unsigned v = base + threadIdx.x + (unsigned)q * blockDim.x;
-      if (v < wend) {
-        const int j = j0 + (int)s.dest[v - base];
-        const unsigned i = rsrc[j] + (v - rbeg[j]);
-        live |= 1u << q;
-        raw[q] = keys1[i];
-        if constexpr (ROWS1) rr[q] = rows1[i];
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NI; ++q) {
-      d[q] = -1;
-      x[q] = 0;
-      r[q] = 0;
-      if (!((live >> q) & 1u)) continue;
-      if constexpr (PACKED) {
-        const unsigned v = base + threadIdx.x + (unsigned)q * blockDim.x;
-        const int j = j0 + (int)s.dest[v - base];
-        const uint64_t w = raw[q];
-        const uint32_t mid = (uint32_t)((w >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
-        d[q] = (int)(mid >> bb);
-        x[q] = unpacked_key<KO>(kp, mid & local_mask, w);
-        r[q] = (unsigned)(((S0 + j) / kStagesPerTile) * kTileRows) + (uint32_t)((w >> kPackedRowShift) & (kTileRows - 1));
-      } else {
-        x[q] = (KO)raw[q];
-        r[q] = rr[q];
-        d[q] = (int)((raw[q] >> sub_shift) & sub_mask);
-      }
-    }
-#else
     // records in two halves of loads in flight (register budget of two
     // workgroups per CU), unpacked into the counting sort's items
     KO x[NI];
@@ -1469,7 +1423,6 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
         }
       }
     }
-#endif
     __syncthreads();  // the destination tags are rewritten by the counting sort
     unsigned rank[NI];
     stage_count(s, nsub, d, rank);
