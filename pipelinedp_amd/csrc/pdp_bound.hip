@@ -2329,6 +2329,29 @@ __global__ void __launch_bounds__(kBlock) k_scan_apply(unsigned* v, int64_t n,
   if (blockIdx.x == 0 && threadIdx.x == 0) v[n] = chunk_sums[n_chunks];
 }
 
+// the same scan in one launch for n <= kScanSmallMax (bucket offsets: C2 1,954
+// and C3 4,928 entries), 16 consecutive entries per thread
+constexpr int kScanSmallThreads = 1024;
+constexpr int64_t kScanSmallMax = (int64_t)kScanSmallThreads * kScanItems;
+__global__ void __launch_bounds__(kScanSmallThreads) k_scan_small(unsigned* v, int64_t n) {
+  __shared__ unsigned wsum[kScanSmallThreads / 64 + 1];
+  const int64_t base = (int64_t)threadIdx.x * kScanItems;
+  unsigned loc[kScanItems];
+  unsigned s = 0;
+#pragma unroll
+  for (int t = 0; t < kScanItems; ++t) {
+    loc[t] = base + t < n ? v[base + t] : 0u;
+    s += loc[t];
+  }
+  unsigned total;
+  unsigned run = block_excl_scan(s, wsum, &total);
+#pragma unroll
+  for (int t = 0; t < kScanItems; ++t) {
+    if (base + t < n) v[base + t] = run;
+    run += loc[t];
+  }
+  if (threadIdx.x == 0) v[n] = total;
+}
 
 }  // namespace
 
@@ -2337,6 +2360,13 @@ int64_t scan_chunk_sums_len(int64_t n) { return (n + kScanChunk - 1) / kScanChun
 int scan_u32(unsigned* v, int64_t n, unsigned* chunk_sums, hipStream_t st) {
   const int64_t n_chunks = (n + kScanChunk - 1) / kScanChunk;
   if (n_chunks == 0) return set_error(PDP_E_INVALID, "scan of an empty array");
+  if (n <= kScanSmallMax) {
+    PDP_PROF_BEGIN("k_scan_small", st);
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanSmallThreads), 0, st, v, n);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    return PDP_OK;
+  }
   PDP_PROF_BEGIN("k_scan_chunks", st);
   hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)n_chunks), dim3(kBlock), 0, st, v, n, chunk_sums);
   PDP_PROF_END(st);

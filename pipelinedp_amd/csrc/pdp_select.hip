@@ -190,7 +190,17 @@ __device__ __forceinline__ void put(double* out, int64_t stride, int col, int64_
   if (col >= 0) out[(int64_t)col * stride + i] = v;
 }
 
-__global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops,
+// mechanism draws of an op (each its own Philox stream (seed, partition, o << 4 | m))
+__host__ __device__ inline int op_draws(int kind) {
+  return kind == PDP_OP_MEAN ? 2 : (kind == PDP_OP_VARIANCE ? 3 : 1);  // THRESHOLDED_PID: a copy
+}
+
+// One lane per (kept partition, draw): a secure sample is a serial bisection
+// of ~60 fp64 steps, so the draws of one partition run on G neighbouring lanes
+// (G = draws per partition rounded up to a power of two) and the lane of each
+// op's first draw combines the op's draws by __shfl and writes its columns.
+// Same streams and arithmetic as one thread per partition.
+__global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops, int log2_g,
                                                           const int64_t* __restrict__ index,
                                                           int64_t n_kept, const int64_t* __restrict__ n_kept_dev,
                                                           int64_t partition_offset,
@@ -203,65 +213,96 @@ __global__ void __launch_bounds__(kBlock) k_noise_metrics(OpsPack ops, int n_ops
     const int64_t d = *n_kept_dev;
     n = d < n ? d : n;
   }
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const int G = 1 << log2_g;
+  const int lane = (int)(threadIdx.x & 63);
+  const int d = lane & (G - 1);
+  // this lane's draw: op o, mechanism m (o < 0: a padding lane)
+  int o = -1, m = 0;
+  for (int q = 0, c = 0; q < n_ops; ++q) {
+    const int k = op_draws(ops.op[q].kind);
+    if (d >= c && d < c + k) {
+      o = q;
+      m = d - c;
+    }
+    c += k;
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;  // a multiple of 64: groups stay whole
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; (t >> log2_g) < n; t += stride) {
+    const int64_t i = t >> log2_g;
     const int64_t p = index[i];
     const int64_t g = partition_offset + p;
-    for (int o = 0; o < n_ops; ++o) {
+    double v = 0.0;
+    if (o >= 0) {
       const pdp_metric_op& op = ops.op[o];
-      const uint32_t slot = (uint32_t)o << 4;
+      const uint32_t slot = ((uint32_t)o << 4) + (uint32_t)m;
       switch (op.kind) {
-        case PDP_OP_COUNT: {
-          const double v = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
-          put(out, out_stride, op.out_col[0], i, v);
+        case PDP_OP_COUNT:
+          v = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
           break;
-        }
-        case PDP_OP_SUM: {
-          const double s = sum_is_int ? (double)((const long long*)acc.sum)[p] : ((const double*)acc.sum)[p];
-          put(out, out_stride, op.out_col[0], i, secure_add_noise(op.noise[0], s, seed, g, slot));
+        case PDP_OP_SUM:
+          v = secure_add_noise(op.noise[0],
+                               sum_is_int ? (double)((const long long*)acc.sum)[p] : ((const double*)acc.sum)[p],
+                               seed, g, slot);
           break;
-        }
-        case PDP_OP_PRIVACY_ID_COUNT: {
-          const double v = secure_add_noise(op.noise[0], (double)acc.privacy_id_count[p], seed, g, slot);
-          put(out, out_stride, op.out_col[0], i, v);
+        case PDP_OP_PRIVACY_ID_COUNT:
+          v = secure_add_noise(op.noise[0], (double)acc.privacy_id_count[p], seed, g, slot);
           break;
-        }
-        case PDP_OP_MEAN: {
-          const double dp_count = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
-          const double denom = fmax(1.0, dp_count);
-          const double dp_nsum = secure_add_noise(op.noise[1], acc.normalized_sum[p], seed, g, slot + 1);
-          const double mean = op.middle + dp_nsum / denom;
-          put(out, out_stride, op.out_col[0], i, mean);
-          put(out, out_stride, op.out_col[1], i, dp_count);
-          put(out, out_stride, op.out_col[2], i, mean * dp_count);
+        case PDP_OP_MEAN:
+          v = secure_add_noise(op.noise[m], m == 0 ? (double)acc.count[p] : acc.normalized_sum[p], seed, g, slot);
           break;
-        }
-        case PDP_OP_VARIANCE: {
-          const double dp_count = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
-          double dp_mean, dp_mean_sq;
-          if (op.degenerate) {
-            dp_mean = op.min_value;
-            dp_mean_sq = op.sq_min_value;
-          } else {
-            const double denom = fmax(1.0, dp_count);
-            dp_mean = secure_add_noise(op.noise[1], acc.normalized_sum[p], seed, g, slot + 1) / denom;
-            dp_mean_sq = secure_add_noise(op.noise[2], acc.normalized_sum_sq[p], seed, g, slot + 2) / denom;
-          }
-          const double dp_var = dp_mean_sq - dp_mean * dp_mean;
-          if (!op.degenerate) dp_mean += op.middle;
-          put(out, out_stride, op.out_col[0], i, dp_var);
-          put(out, out_stride, op.out_col[1], i, dp_count);
-          put(out, out_stride, op.out_col[2], i, dp_mean * dp_count);
-          put(out, out_stride, op.out_col[3], i, dp_mean);
+        case PDP_OP_VARIANCE:
+          if (m == 0) v = secure_add_noise(op.noise[0], (double)acc.count[p], seed, g, slot);
+          else if (!op.degenerate)  // a degenerate variance draws the count only
+            v = secure_add_noise(op.noise[m], m == 1 ? acc.normalized_sum[p] : acc.normalized_sum_sq[p], seed, g, slot);
           break;
-        }
-        case PDP_OP_THRESHOLDED_PID: {
-          put(out, out_stride, op.out_col[0], i, noised_count[p]);
+        case PDP_OP_THRESHOLDED_PID:
+          v = noised_count[p];
           break;
-        }
         default:
           break;
       }
+    }
+    // every lane takes part in the shuffles (the op's later draws sit on lanes + 1, + 2)
+    const double v1 = __shfl(v, (lane + 1) & 63, 64);
+    const double v2 = __shfl(v, (lane + 2) & 63, 64);
+    if (o < 0 || m != 0) continue;
+    const pdp_metric_op& op = ops.op[o];
+    switch (op.kind) {
+      case PDP_OP_COUNT:
+      case PDP_OP_SUM:
+      case PDP_OP_PRIVACY_ID_COUNT:
+      case PDP_OP_THRESHOLDED_PID:
+        put(out, out_stride, op.out_col[0], i, v);
+        break;
+      case PDP_OP_MEAN: {
+        const double dp_count = v;
+        const double mean = op.middle + v1 / fmax(1.0, dp_count);
+        put(out, out_stride, op.out_col[0], i, mean);
+        put(out, out_stride, op.out_col[1], i, dp_count);
+        put(out, out_stride, op.out_col[2], i, mean * dp_count);
+        break;
+      }
+      case PDP_OP_VARIANCE: {
+        const double dp_count = v;
+        double dp_mean, dp_mean_sq;
+        if (op.degenerate) {
+          dp_mean = op.min_value;
+          dp_mean_sq = op.sq_min_value;
+        } else {
+          const double denom = fmax(1.0, dp_count);
+          dp_mean = v1 / denom;
+          dp_mean_sq = v2 / denom;
+        }
+        const double dp_var = dp_mean_sq - dp_mean * dp_mean;
+        if (!op.degenerate) dp_mean += op.middle;
+        put(out, out_stride, op.out_col[0], i, dp_var);
+        put(out, out_stride, op.out_col[1], i, dp_count);
+        put(out, out_stride, op.out_col[2], i, dp_mean * dp_count);
+        put(out, out_stride, op.out_col[3], i, dp_mean);
+        break;
+      }
+      default:
+        break;
     }
   }
 }
@@ -378,9 +419,13 @@ int pdp_noise_metrics(const pdp_metric_op* ops, int32_t n_ops, const int64_t* in
     }
     pack.op[i] = o;
   }
+  int draws = 0;
+  for (int i = 0; i < n_ops; ++i) draws += op_draws(ops[i].kind);
+  int log2_g = 0;
+  while ((1 << log2_g) < draws) ++log2_g;  // <= 24 draws: groups of at most 32 lanes
   PDP_PROF_BEGIN("k_noise_metrics", (hipStream_t)stream);
-  hipLaunchKernelGGL(k_noise_metrics, dim3(grid_for(n_kept)), dim3(kBlock), 0, (hipStream_t)stream, pack,
-                     n_ops, index, n_kept, n_kept_dev, partition_offset, *acc, sum_is_int, noised_count,
+  hipLaunchKernelGGL(k_noise_metrics, dim3(grid_for(n_kept << log2_g)), dim3(kBlock), 0, (hipStream_t)stream, pack,
+                     n_ops, log2_g, index, n_kept, n_kept_dev, partition_offset, *acc, sum_is_int, noised_count,
                      out, out_stride, seed);
   PDP_PROF_END((hipStream_t)stream);
   PDP_HIP_CHECK(hipGetLastError());

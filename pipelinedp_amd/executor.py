@@ -168,19 +168,23 @@ def _mark(timer, name):
 def new_accumulators(n_partitions: int, bounding: BoundingSpec, device) -> Dict[str, "torch.Tensor"]:
     torch = _torch()
     P = int(n_partitions)
-    acc = {
-        "privacy_id_count": torch.zeros(P, dtype=torch.int64, device=device),
-        "count": torch.zeros(P, dtype=torch.int64, device=device),
-        "sum": None,
-        "normalized_sum": None,
-        "normalized_sum_sq": None,
-    }
+    names = ["privacy_id_count", "count"]
     if bounding.flags & (N.ACC_SUM | N.SUM_PER_PARTITION):
-        acc["sum"] = torch.zeros(P, dtype=torch.int64 if bounding.sum_is_int else torch.float64, device=device)
+        names.append("sum")
     if bounding.flags & N.ACC_NSUM:
-        acc["normalized_sum"] = torch.zeros(P, dtype=torch.float64, device=device)
+        names.append("normalized_sum")
     if bounding.flags & N.ACC_NSUM2:
-        acc["normalized_sum_sq"] = torch.zeros(P, dtype=torch.float64, device=device)
+        names.append("normalized_sum_sq")
+    # one zero fill for every field: 8-byte fields side by side, each starting
+    # on a 256-byte boundary (all-zero bits are 0 as int64 and 0.0 as float64)
+    stride = (P + 31) // 32 * 32
+    block = torch.zeros(len(names) * stride, dtype=torch.int64, device=device)
+    acc = {"privacy_id_count": None, "count": None, "sum": None, "normalized_sum": None,
+           "normalized_sum_sq": None}
+    for k, name in enumerate(names):
+        field = block[k * stride:k * stride + P]
+        is_int = name in ("privacy_id_count", "count") or (name == "sum" and bounding.sum_is_int)
+        acc[name] = field if is_int else field.view(torch.float64)
     return acc
 
 
