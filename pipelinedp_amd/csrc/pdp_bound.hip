@@ -656,16 +656,34 @@ __device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ c
   return v;
 }
 
-// csum[chunk][b] = rows of bucket b in the chunk's tiles
+// csum[chunk][b] = rows of bucket b in the chunk's tiles; gsum (nullable):
+// gsum[g][b] = rows of bucket b in the kL2GroupTiles tiles of group g
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* __restrict__ counts_tm,
                                                                  const unsigned* __restrict__ counts_tm2,
                                                                  int64_t n_tiles, int64_t n_buckets,
-                                                                 unsigned* __restrict__ csum) {
+                                                                 unsigned* __restrict__ csum,
+                                                                 unsigned* __restrict__ gsum) {
   __shared__ unsigned part[kScanWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * 64 + lane;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
+  if (gsum == nullptr) {
+    part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
+  } else {
+    unsigned v = 0, gv = 0;
+#pragma unroll
+    for (int j = 0; j < kScanTiles; ++j) {
+      const int64_t t = t0 + j;
+      if (t < n_tiles && b < n_buckets) gv += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
+      if ((j + 1) % kL2GroupTiles == 0) {
+        if (t0 + j + 1 - kL2GroupTiles < n_tiles && b < n_buckets)
+          gsum[((t0 + j + 1) / kL2GroupTiles - 1) * n_buckets + b] = gv;
+        v += gv;
+        gv = 0;
+      }
+    }
+    part[w][lane] = v;
+  }
   __syncthreads();
   if (w == 0 && b < n_buckets) {
     unsigned v = 0;
@@ -686,6 +704,26 @@ __global__ void __launch_bounds__(kBlock) k_gscan_chunks(unsigned* __restrict__ 
     run += v;
   }
   total[b] = run;
+}
+
+// gcur[g][b] in place: the group sums of k_gscan_sums -> rows of bucket b in
+// tiles < g * kL2GroupTiles (cpre: k_gscan_chunks' exclusive chunk sums)
+__global__ void __launch_bounds__(kBlock) k_gscan_groups(const unsigned* __restrict__ cpre, int64_t n_tiles,
+                                                         int64_t n_buckets, unsigned* __restrict__ gcur) {
+  const int64_t n_sc = (n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
+  const int64_t n_grp = (n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
+  constexpr int kGroups = kScanChunkTiles / kL2GroupTiles;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_sc * n_buckets) return;
+  const int64_t c = i / n_buckets, b = i % n_buckets;
+  unsigned run = cpre[i];
+  for (int k = 0; k < kGroups; ++k) {
+    const int64_t g = c * kGroups + k;
+    if (g >= n_grp) break;
+    const unsigned v = gcur[g * n_buckets + b];
+    gcur[g * n_buckets + b] = run;
+    run += v;
+  }
 }
 
 // gcur[g][b] = rows of bucket b in tiles < g * kL2GroupTiles
@@ -2570,7 +2608,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
   hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, csum);
+                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, csum, gcur);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -2578,9 +2616,10 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
                      counts);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_gscan_cursors", st);
-  hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
-                     counts_tm, (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+  // level-2 cursors from the group sums (one pass over counts_tm in all)
+  PDP_PROF_BEGIN("k_gscan_groups", st);
+  hipLaunchKernelGGL(k_gscan_groups, dim3(grid_for(n_sc * p.n_buckets, (int64_t)1 << 30)), dim3(kBlock), 0, st,
+                     (const unsigned*)csum, p.n_tiles, p.n_buckets, gcur);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   const int rc = scan_u32(counts, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);
@@ -2763,7 +2802,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
   hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum);
+                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum, (unsigned*)nullptr);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
