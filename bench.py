@@ -58,8 +58,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
 # wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for
 # the workload and tree named in the file; None otherwise.
-PMC_SUMMARY = {"c3": os.path.join(HERE, "profiles", "r02", "c3_pmc.json"),
-               "c2": os.path.join(HERE, "profiles", "r02", "c2_pmc.json")}
+PMC_SUMMARY = {"c3": os.path.join(HERE, "profiles", "r03", "c3_pmc.json"),
+               "c2": os.path.join(HERE, "profiles", "r03", "c2_pmc.json")}
 
 # workload constants
 C2 = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000, l0=8, linf=2)
@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
+    ap.add_argument("--sieve", type=int, default=0,
+                    help="threshold sieve t * 2^16 (0 auto, -1 off; pdp_bound_config.sieve)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the "
                          "n_gpus it sees (tests/test_bench_launcher.py)")
@@ -337,22 +339,31 @@ def run_api_workload(args, workload, world, rank, device):
     }
 
 
-def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields):
+def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
     """Algorithmic bytes of each kernel of one step: every
-    input it must read once plus every output it must write once."""
+    input it must read once plus every output it must write once.  `stats`
+    (BoundWorkspace.stats): rows through the partition passes (the sieve's
+    candidates) and the sieve's fix-up rows."""
     from pipelinedp_amd import _native as N
-    kb, rb = {N.KEYS_COMPACT: (4, 4), N.KEYS_WIDE: (8, 4), N.KEYS_PACKED: (8, 0)}.get(plan.key_format, (8, 4))
-    rec = kb + rb
+    rec1 = {N.KEYS_COMPACT: 8, N.KEYS_WIDE: 12}.get(plan.key_format, 8)        # level-1 record
+    rec2 = {N.KEYS_WIDE: 12, N.KEYS_PACKED_WIDE: 12}.get(plan.key_format, 8)   # level-2 key + row
+    key2 = rec2 - 4
     pair_rec = 8 + 8 * n_fields
-    # level 1 reads the two key columns and writes one record per row (the
-    # tile-local form needs no separate histogram pass over privacy ids)
-    out = {"k_scatter_l1": (16.0 + rec) * n,
-           "k_scatter_l2": 2.0 * rec * n,
-           # B1 streams the level-2 keys; kept rows' indices and values are
-           # gathered; one record per kept pair out
-           "k_bucket_bound": (4.0 if plan.key_format != N.KEYS_WIDE else 8.0) * n + 12.0 * kept_rows
-                             + pair_rec * kept_pairs,
-           "k_range_reduce": 2.0 * pair_rec * kept_pairs}
+    cand = stats["rows_partitioned"]
+    fix = stats["fixup_rows"]
+    out = {}
+    # level 1 reads the two key columns once and writes one record per row
+    # that goes on (the tile-local form needs no histogram pass over ids)
+    out["k_sieve_l1" if plan.sieve else "k_scatter_l1"] = 16.0 * n + rec1 * cand
+    out["k_scatter_l2"] = (rec1 + rec2) * cand
+    # B1 streams the level-2 keys; kept rows' indices and values are
+    # gathered; one record per kept pair out
+    out["k_bucket_bound"] = key2 * cand + 12.0 * kept_rows + pair_rec * kept_pairs
+    if plan.sieve:
+        out["k_sieve_rescan"] = 8.0 * n + 8.0 * fix         # privacy ids in, (id, row) per fix-up row out
+        out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * fix      # list in, partition gathered, record out
+        out["k_bucket_fix"] = key2 * fix
+    out["k_range_reduce"] = 2.0 * pair_rec * kept_pairs
     return out
 
 
@@ -417,7 +428,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
 
     P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
-    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format)
+    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format, sieve=args.sieve)
     acc = X.new_accumulators(P_pad, bounding, device)
     seed_base = parallel.broadcast_seeds((int.from_bytes(os.urandom(8), "little"),))[0]
 
@@ -427,7 +438,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                 t.zero_()
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
-                           check_keys=False, key_format=args.key_format)
+                           check_keys=False, key_format=args.key_format, sieve=args.sieve)
         mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
@@ -452,7 +463,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     # key-error check of the data once (outside the timed region)
     X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding, seed=1,
                        row_offset=rank * n, acc=acc, workspace=ws, check_keys=True,
-                       key_format=args.key_format)
+                       key_format=args.key_format, sieve=args.sieve)
     # per-kernel times from a second, untimed pass of the same steps: the HIP
     # events the profiler records around every launch (on its launch stream)
     # would otherwise sit inside the timed region
@@ -463,6 +474,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     N.profiler_enable(False)
     kept_pairs = int(acc["privacy_id_count"].sum().item())  # last step, this rank
     kept_rows = int(acc["count"].sum().item())
+    stats = ws.stats()
     api = api_timing(args, workload, pid, pk, value, U, P, ws) if (world == 1 and args.api) else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -481,7 +493,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         if pmc.get("workload", "").startswith(f"{workload} n={n} ") and world == 1:
             traffic = {k: v["hbm_bytes"] for k, v in pmc["kernels"].items() if "hbm_bytes" in v}
             traffic_src = os.path.relpath(pmc_file, HERE)
-    alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2)
+    alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2, stats)
     table = {}
     for k, ms in kernel_ms.items():
         e = {"ms": ms, "launches_per_step": launches[k]}
@@ -523,8 +535,9 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         "kernels": table,
         "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
                        "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
-                       "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(plan.key_format,
-                                                                               plan.key_format)},
+                       "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(
+                           plan.key_format, plan.key_format),
+                       "sieve": plan.sieve / 65536.0, "stats": stats},
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api,
     }

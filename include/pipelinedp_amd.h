@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 7
+#define PDP_ABI_VERSION 8
 
 /* error codes */
 #define PDP_OK 0
@@ -46,6 +46,10 @@ extern "C" {
 #define PDP_ACC_NSUM2 0x4          /* Variance: sum of (clip(v) - middle)^2 */
 #define PDP_SUM_PER_PARTITION 0x8  /* SumCombiner bounds_per_partition: clip(sum_pair) */
 #define PDP_SUM_INT 0x10           /* SUM accumulator is int64 (int values, int bounds) */
+#define PDP_DEBUG_CORRUPT_RECORDS 0x40000000 /* tests only: overwrite the level-2 records of buckets 0
+                                                and 1 with an out-of-range partition / row before the
+                                                bucket kernel, which must flag them in the error word
+                                                (pdp_bound_error_flags) instead of reading out of bounds */
 
 /* One shard's contribution-bounding configuration. */
 typedef struct pdp_bound_config {
@@ -72,7 +76,11 @@ typedef struct pdp_bound_config {
   int32_t rows_are_units;    /* != 0: contribution_bounds_already_enforced — every row is
                                 its own accumulator; privacy_id may be NULL */
   int32_t key_format;        /* PDP_KEYS_*: row record format of the BUCKETED partition passes */
-  int32_t reserved;
+  int32_t sieve;             /* BUCKETED threshold sieve (identical results): 0 = auto, < 0 = off,
+                                1..32768 = keep rows whose 32-bit pair hash is below sieve * 2^16
+                                (candidate fraction t = sieve / 2^16 <= 1/2) through the partition
+                                passes; privacy ids with < l0 candidate pairs are finished from a
+                                re-read of the privacy-id column */
 } pdp_bound_config;
 
 /* bounds up to int32; above 256 (l0, linf) the pair-table algorithm runs, and
@@ -126,7 +134,7 @@ typedef struct pdp_bound_plan_info {
   int32_t n_ranges;    /* PDP_MERGE_RANGES: partition ranges of 2^11 keys */
   int64_t range_group; /* PDP_MERGE_RANGES: records per range-reduce work item */
   int32_t key_format;  /* resolved PDP_KEYS_* (BUCKETED) */
-  int32_t reserved;
+  int32_t sieve;       /* resolved threshold sieve, t = sieve / 2^16 (0 = off) */
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */
@@ -162,7 +170,10 @@ int pdp_bound_workspace_bytes(const pdp_bound_config* cfg, uint64_t* bytes);
  * branch ("Wrap values into accumulators", dp_engine.py:143-150).
  * `pk_allowed` (nullable, u8[n_partitions]) drops rows of non-public
  * partitions first (DPEngine._drop_partitions, dp_engine.py:290-296).
- * The workspace is fully (re)initialised on `stream` by this call. */
+ * The workspace is fully (re)initialised on `stream` by this call.  With
+ * PDP_MERGE_RANGES (the default) the whole sampling runs here and leaves
+ * per-pair records in the workspace; with PDP_MERGE_ATOMIC the per-bucket
+ * sampling runs in pdp_reduce_partitions. */
 int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_id,
                             const int64_t* partition_key, const void* value,
                             const uint8_t* pk_allowed, void* workspace,
@@ -172,7 +183,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
  * values, combiners.py:749-753) merged per partition key
  * (LocalBackend.combine_accumulators_per_key, pipeline_backend.py:555-565).
  * Must follow pdp_bound_contributions on the same workspace and stream
- * (BUCKETED: the per-bucket sampling itself runs here, in LDS).
+ * (BUCKETED + PDP_MERGE_ATOMIC: the per-bucket sampling itself runs here).
  * `acc` arrays are ADDED to (zero them first, or chain shards). */
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value,
                           void* workspace, uint64_t workspace_bytes,
@@ -295,6 +306,23 @@ int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, const pdp_n
  * of bounds).  Reads it from the workspace of pdp_bound_contributions
  * (synchronises `stream`). */
 int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
+
+/* What the last pdp_bound_contributions (BUCKETED) moved, read from its
+ * workspace (synchronises `stream`): rows that entered the partition passes
+ * (every live row, or the sieve's candidates), privacy ids the sieve left
+ * unresolved and the rows of those ids its fix-up re-read.  Diagnostics for
+ * the measurement (bench.py's algorithmic bytes); zeros for other
+ * algorithms. */
+typedef struct pdp_bound_stats {
+  int64_t rows_partitioned;
+  int64_t unresolved_ids;
+  int64_t fixup_rows;
+  int32_t sieve;        /* resolved sieve (pdp_bound_plan_info.sieve) */
+  uint32_t error_flags; /* pdp_bound_error_flags */
+} pdp_bound_stats;
+
+int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,
+                         pdp_bound_stats* out, void* stream);
 
 /* Dataset histograms: compute_dataset_histograms
  * (pipeline_dp/dataset_histograms/computing_histograms.py:456-513) over one

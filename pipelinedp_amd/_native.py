@@ -17,9 +17,10 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 7
+ABI_VERSION = 8
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
+DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
 SELECT_ALL_NONEMPTY = 0
 SELECT_TRUNCATED_GEOMETRIC = 1
 SELECT_LAPLACE_THRESHOLDING = 2
@@ -58,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "pdp_dataset_histograms_preaggregated_exchange_offsets",
     "pdp_dataset_histograms_preaggregated_finish",
     "pdp_bound_error_flags",
+    "pdp_bound_stats_read",
     "pdp_profiler_enable",
     "pdp_profiler_report",
 )
@@ -89,7 +91,7 @@ class BoundConfig(ctypes.Structure):
         ("max_contributions", ctypes.c_int32),
         ("rows_are_units", ctypes.c_int32),
         ("key_format", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("sieve", ctypes.c_int32),
     ]
 
 
@@ -106,7 +108,17 @@ class BoundPlanInfo(ctypes.Structure):
         ("n_ranges", ctypes.c_int32),
         ("range_group", ctypes.c_int64),
         ("key_format", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("sieve", ctypes.c_int32),
+    ]
+
+
+class BoundStats(ctypes.Structure):
+    _fields_ = [
+        ("rows_partitioned", ctypes.c_int64),
+        ("unresolved_ids", ctypes.c_int64),
+        ("fixup_rows", ctypes.c_int64),
+        ("sieve", ctypes.c_int32),
+        ("error_flags", ctypes.c_uint32),
     ]
 
 
@@ -215,6 +227,7 @@ def _declare(lib):
         "pdp_dataset_histograms_preaggregated_finish": (ctypes.c_int, [vp, i64, i64, i32, P(HistogramBins),
                                                                        vp, u64, vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
+        "pdp_bound_stats_read": (ctypes.c_int, [P(BoundConfig), vp, u64, P(BoundStats), vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),
     }

@@ -41,60 +41,31 @@ namespace {
 
 constexpr int kPartThreads = 512;
 // rows per thread and LDS stage of the level-1 scatter / level-2 window
-#ifndef PDP_L1_ITEMS
-#define PDP_L1_ITEMS 8
-#endif
-#ifndef PDP_L2_ITEMS
-#define PDP_L2_ITEMS 16
-#endif
-#ifndef PDP_L1_THREADS
-#define PDP_L1_THREADS 1024
-#endif
-constexpr int kL1Threads = PDP_L1_THREADS;
-constexpr int kL1Items = PDP_L1_ITEMS;
+constexpr int kL1Threads = 1024;
+constexpr int kL1Items = 8;
 constexpr int kL1Rows = kL1Threads * kL1Items;  // rows per level-1 LDS stage
-constexpr int kL2Items = PDP_L2_ITEMS;
-#ifndef PDP_L2_THREADS
-#define PDP_L2_THREADS 512
-#endif
-// level-2 occupancy attribute (A/B knob).  Two 8-wave workgroups per CU
-// need <= 128 VGPRs (MI355X_MICROARCH.md register table): the kernel as
-// written takes 121-123 with 16 records per thread; loading a stage ahead
-// (157 VGPRs, one workgroup per CU) cost 1 ms at C3
-#ifndef PDP_L2_OCC
-#define PDP_L2_OCC
-#endif
-constexpr int kL2Threads = PDP_L2_THREADS;
+constexpr int kL2Items = 16;
+// level 2: two 8-wave workgroups per CU need <= 128 VGPRs (MI355X_MICROARCH.md
+// register table): the kernel takes 121-123 with 16 records per thread;
+// loading a stage ahead (157 VGPRs, one workgroup per CU) cost 1 ms at C3
+constexpr int kL2Threads = 512;
 constexpr int kL2Rows = kL2Threads * kL2Items;  // records per level-2 LDS stage
 // tiles per level-2 workgroup (k_scatter_l2, k_gscan_cursors)
-#ifndef PDP_L2_GROUP
-#define PDP_L2_GROUP 16
-#endif
-constexpr int kL2GroupTiles = PDP_L2_GROUP;
+constexpr int kL2GroupTiles = 16;
 constexpr int kScanWaves = 16;
-#ifndef PDP_SCAN_TILES
-#define PDP_SCAN_TILES 16
-#endif
-constexpr int kScanTiles = PDP_SCAN_TILES;  // tiles per wave in the level-2 cursor scans; multiple of kL2GroupTiles
+constexpr int kScanTiles = 16;  // tiles per wave in the level-2 cursor scans; multiple of kL2GroupTiles
 constexpr int kScanChunkTiles = kScanWaves * kScanTiles;
 static_assert(kScanTiles % kL2GroupTiles == 0, "group starts must fall inside a wave's tiles");
 constexpr int kTileRowBits = 16;
 constexpr int64_t kTileRows = (int64_t)1 << kTileRowBits;
+constexpr int kStagesPerTile = (int)(kTileRows / kL1Rows);  // level-1 blocks per tile
+constexpr int kL2Runs = kL2GroupTiles * kStagesPerTile;  // level-1 runs per level-2 workgroup
 constexpr int kUnroll = 8;
-#ifndef PDP_BUCKET_THREADS
-#define PDP_BUCKET_THREADS 1024
-#endif
-#ifndef PDP_LDS_BUDGET_KB
-#define PDP_LDS_BUDGET_KB 124
-#endif
-constexpr int kBucketThreads = PDP_BUCKET_THREADS;
-constexpr int64_t kLdsBudget = PDP_LDS_BUDGET_KB * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
+constexpr int kBucketThreads = 1024;
+constexpr int64_t kLdsBudget = 124 * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
-#ifndef PDP_MAX_SUPERS
-#define PDP_MAX_SUPERS 128
-#endif
-constexpr int kMaxSupers = PDP_MAX_SUPERS;   // destinations of a level-1 scatter
+constexpr int kMaxSupers = 128;   // destinations of a level-1 scatter
 constexpr int64_t kSingleLevelMax = 64;      // buckets partitioned by one level
 constexpr int kRangeBits = 11;                // partitions per merge range = 2048
 constexpr int kRangeParts = 1 << kRangeBits;
@@ -113,61 +84,10 @@ constexpr int64_t kRangeChunk = 8192;
 constexpr unsigned kRangeDirect = 256;        // records below which a workgroup adds them directly
 constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
-// 16-byte key loads in flight per lane in the bucket kernel's B1 / B2 passes
-#ifndef PDP_B1_KU_COMPACT
-#define PDP_B1_KU_COMPACT 4
-#endif
-#ifndef PDP_PIPE
-#define PDP_PIPE 1
-#endif
-// attribute of the bucket kernel's per-candidate work lambdas (A/B: noinline
-// keeps one copy of the sketch code instead of one per unrolled push)
-#ifndef PDP_WORK_ATTR
-#define PDP_WORK_ATTR
-#endif
-#ifndef PDP_BATCH_PRED
-#define PDP_BATCH_PRED 0
-#endif
-// level-1 scatter: prefetch the next stage's columns during this stage's LDS
-// passes (+32 VGPRs: 2 instead of 4 workgroups per CU)
-#ifndef PDP_L1_PREFETCH
-#define PDP_L1_PREFETCH 0
-#endif
-// level-1 scatter occupancy attribute (A/B: amdgpu_waves_per_eu(8, 8) caps
-// VGPRs at 64 and spills: 0.64 -> 0.96 ms; left to the compiler)
-#ifndef PDP_L1_OCC
-#define PDP_L1_OCC
-#endif
-// tile-local level 1 when its LDS fits (A/B knob: 0 = histogram pass + global offsets)
-#ifndef PDP_L1_LOCAL
-#define PDP_L1_LOCAL 1
-#endif
-// minimum waves per SIMD of the tile-local level 2 (4: two 512-thread
-// workgroups per CU within 128 VGPRs)
-#ifndef PDP_L2L_WAVES
-#define PDP_L2L_WAVES 4
-#endif
-// B1 candidate test against a per-pid 32-bit threshold kept beside the pid
-// hash (one LDS read per record) instead of the 64-bit sketch maximum
-#ifndef PDP_B1_THR
-#define PDP_B1_THR 1
-#endif
-#ifndef PDP_GATHER_VALUES
-#define PDP_GATHER_VALUES 1
-#endif
-#ifndef PDP_INSERT_SKIP
-#define PDP_INSERT_SKIP 0
-#endif
-#ifndef PDP_B2_KU_COMPACT
-#define PDP_B2_KU_COMPACT 1
-#endif
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
 
-#ifndef PDP_L1_LOCAL_LDS_KB
-#define PDP_L1_LOCAL_LDS_KB 150
-#endif
-constexpr int64_t kL1LocalLds = PDP_L1_LOCAL_LDS_KB * 1024;  // tile-local level 1: LDS cap (one 1,024-thread workgroup per CU)
+constexpr int64_t kL1LocalLds = 150 * 1024;  // tile-local level 1: LDS cap (one 1,024-thread workgroup per CU)
 size_t l1_stage_bytes(int key_format);       // LDS of one level-1 stage (after StageLds)
 // tile-local level 1 bucket counts in LDS: u32 per bucket when they fit,
 // else two u16 per word, flushed every half tile (32,768 rows: no carry) to
@@ -175,6 +95,39 @@ size_t l1_stage_bytes(int key_format);       // LDS of one level-1 stage (after 
 inline int64_t l1_hist_bytes(int64_t n_buckets, bool u16) { return ((u16 ? 2 : 4) * n_buckets + 15) / 16 * 16; }
 inline bool l1_hist_u16(int key_format, int64_t n_buckets) {
   return (int64_t)l1_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) > kL1LocalLds;
+}
+
+// ---- threshold sieve (Plan.sieve) ----------------------------------------
+// With cross-partition sampling, a privacy id keeps the l0 pairs of smallest
+// pair key, and its other pairs (usually most of its rows) contribute
+// nothing.  The sieve keeps only rows whose 32-bit pair hash is below one
+// global threshold t32 = sieve << 16: if a privacy id has >= l0 distinct
+// pairs below it, its l0 smallest are among them, together with every row of
+// those pairs (a pair's rows share its hash), so the level-1 pass writes and
+// levels 2/3 read only those candidate rows.  Privacy ids with fewer than l0
+// candidate pairs ("unresolved": the bucket kernel marks them in a bitmap
+// and a list) are finished by a fix-up over ALL their rows: one streaming
+// re-read of the privacy-id column (k_sieve_rescan, an LDS Bloom filter of
+// the list in front of the exact bitmap), a scatter into bucket order and a
+// second bucket-kernel launch whose pair records follow the main ones.
+// Kept pairs and rows are exactly those of the unsieved path.
+constexpr int kSieveChunkItems = 4;                            // rows per thread and chunk
+constexpr int kSieveChunk = kL1Threads * kSieveChunkItems;     // rows filtered per chunk
+constexpr int kSieveCap = 12288;                               // candidate slots of the LDS stage
+constexpr int kSieveItems = kSieveCap / kL1Threads;            // per thread at a flush
+// a tile's flush blocks lie back to back from tile * kSieveTileStride
+constexpr int64_t kSieveTileStride = kTileRows;
+constexpr int kSieveMaxT16 = 1 << 15;                          // t <= 1/2
+constexpr int kBloomWords = 16384;                             // k_sieve_rescan: 64 KiB LDS Bloom filter
+constexpr int kRescanThreads = 512;                            // two workgroups per CU
+constexpr int kSieveL2Groups = 4;  // tile groups per level-2 workgroup with the sieve
+// every flush but a tile's last holds > kSieveCap - kSieveChunk records, so a
+// tile flushes at most kStagesPerTile times (its blocks fit the level-1 slots)
+static_assert(kTileRows / (kSieveCap - kSieveChunk + 1) + 1 <= kStagesPerTile, "sieve flushes per tile");
+static_assert(kSieveCap <= 65535, "u16 run offsets");
+size_t sieve_stage_bytes(int key_format);  // LDS of the sieve's level-1 stage (after StageLds)
+inline bool sieve_hist_u16(int key_format, int64_t n_buckets) {
+  return (int64_t)sieve_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) > kL1LocalLds;
 }
 
 struct Plan {
@@ -198,6 +151,9 @@ struct Plan {
   int key_format;       // PDP_KEYS_WIDE / PDP_KEYS_COMPACT (bucketed)
   int l1_local;         // tile-local level 1 (k_scatter_l1_local / k_scatter_l2_local), no histogram pass
   int64_t n_stages;     // level-1 stages of kL1Rows rows
+  int sieve;            // threshold sieve: t = sieve / 2^16 (0 = off); k_sieve_l1 instead of k_scatter_l1_local
+  int64_t n_slots1;     // level-1 blocks (stages, or sieve flush slots: n_tiles * kStagesPerTile)
+  int64_t buckets_out;  // buckets of pair records: n_buckets, 2 * n_buckets with the sieve (fix-up after)
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -283,7 +239,7 @@ Plan make_plan(const pdp_bound_config* c) {
   if (p.algorithm == PDP_ALGO_BUCKETED) {
     // tile-local level 1: two levels, and the bucket counts in its LDS
     auto local_fits = [&](int fmt) {
-      return PDP_L1_LOCAL && p.super_bits > 0 &&
+      return p.super_bits > 0 &&
              (int64_t)l1_stage_bytes(fmt) + l1_hist_bytes(p.n_buckets, true) <= kL1LocalLds;
     };
     const int want = c->key_format;
@@ -306,6 +262,27 @@ Plan make_plan(const pdp_bound_config* c) {
     if (p.key_format == PDP_KEYS_PACKED && p.super_bits == 0) p.key_format = PDP_KEYS_COMPACT;
     if (p.algorithm == PDP_ALGO_BUCKETED) p.l1_local = local_fits(p.key_format) ? 1 : 0;
   }
+  // threshold sieve: tile-local level 1, range merge, whole 64-pid bitmap
+  // words per bucket, and the sieve's larger LDS stage must fit
+  const bool sieve_ok = p.algorithm == PDP_ALGO_BUCKETED && p.l1_local && p.merge == PDP_MERGE_RANGES &&
+                        p.bucket_bits >= 6 && p.key_format != PDP_KEYS_WIDE &&
+                        (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) <= kL1LocalLds &&
+                        p.n_tiles * kSieveTileStride < ((int64_t)1 << 32);
+  int t16 = 0;
+  if (sieve_ok && c->sieve > 0) {
+    t16 = c->sieve < kSieveMaxT16 ? c->sieve : kSieveMaxT16;
+  } else if (sieve_ok && c->sieve == 0) {
+    // auto: a privacy id with d distinct partitions has ~d*t candidate pairs;
+    // ask for l0 + 3 sqrt(l0) + 3 of them, assuming d ~ 0.6 rows per id
+    // (C3: 100 rows over Zipf(1.1) keys, t = 0.15); no sieve above t = 0.35
+    const double rows_per_id = (double)c->n_rows / (double)c->n_privacy_ids;
+    const double want = c->l0 + 3.0 * std::sqrt((double)c->l0) + 3.0;
+    const double t = want / (0.6 * rows_per_id);
+    if (t <= 0.35) t16 = (int)std::ceil(t * 65536.0);
+  }
+  p.sieve = t16 > 0 ? t16 : 0;
+  p.n_slots1 = p.sieve ? p.n_tiles * kStagesPerTile : p.n_stages;
+  p.buckets_out = p.sieve ? 2 * p.n_buckets : p.n_buckets;
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
     p.lds_bytes += ((int64_t)8 << p.bucket_bits);  // {pid hash, sketch-maximum high half} per pid
@@ -313,7 +290,7 @@ Plan make_plan(const pdp_bound_config* c) {
   if (p.merge == PDP_MERGE_RANGES) {
     // range r yields ceil(records_r / C) items + 1 sentinel, and a bucket
     // emits at most l0 * 2^bucket_bits records in all
-    const int64_t recs = p.n_buckets * ((int64_t)c->l0 << p.bucket_bits);
+    const int64_t recs = p.buckets_out * ((int64_t)c->l0 << p.bucket_bits);
     p.range_group = kRangeChunk;
     p.n_groups = recs / kRangeChunk + 2 * (int64_t)p.n_ranges + 1;
     p.fine_items = p.two_level ? recs / kRangeChunk + p.n_fine + 1 : 0;
@@ -338,6 +315,11 @@ struct Ws {
   uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, record index)
   uint64_t soff;                // tile-local level 1: per stage, super-bucket run starts (u16)
   uint64_t counts_tm2;          // tile-local level 1, u16 counts: second half-tile bucket counts
+  // threshold sieve: flush-block starts (u32 per slot), unresolved privacy
+  // ids (bitmap + list), {unresolved count, fix-up rows}, fix-up rows per
+  // bucket (-> starts) and their write cursors; the fix-up row list itself
+  // reuses keys1 (dead after level 2), its bucket-ordered records keys2/rows2
+  uint64_t sbase, unres_bits, unres_list, sctl, fix_cnt, fix_cur;
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -368,7 +350,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
-    if (p.l1_local && l1_hist_u16(p.key_format, p.n_buckets)) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
+    const bool u16 = p.sieve ? sieve_hist_u16(p.key_format, p.n_buckets) : l1_hist_u16(p.key_format, p.n_buckets);
+    if (p.l1_local && u16) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     const uint64_t n_sc = ((uint64_t)p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
@@ -381,10 +364,21 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const bool packed = (p.key_format == PDP_KEYS_PACKED || p.key_format == PDP_KEYS_PACKED_WIDE) && p.super_bits > 0;
     const uint64_t kb1 = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;  // level-1 key
     const uint64_t kb2 = (p.key_format == PDP_KEYS_WIDE || p.key_format == PDP_KEYS_PACKED_WIDE) ? 8 : 4;  // level-2 key
-    const uint64_t n1 = p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n;  // level-1 records (stage blocks)
+    // level-1 records: stage blocks, or the sieve's per-tile flush blocks
+    const uint64_t n1 = p.sieve ? (uint64_t)p.n_tiles * kSieveTileStride
+                                : (p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n);
     w.keys1 = off; off = align256(off + n1 * (packed ? 8 : kb1));
     if (!packed) { w.rows1 = off; off = align256(off + n1 * 4); }
-    if (p.l1_local) { w.soff = off; off = align256(off + (uint64_t)p.n_stages * (p.n_supers + 1) * 2); }
+    if (p.l1_local) { w.soff = off; off = align256(off + (uint64_t)p.n_slots1 * (p.n_supers + 1) * 2); }
+    if (p.sieve) {
+      const uint64_t ids = (uint64_t)p.n_buckets << p.bucket_bits;
+      w.sbase = off; off = align256(off + (uint64_t)p.n_slots1 * 4);
+      w.unres_bits = off; off = align256(off + ids / 8);
+      w.unres_list = off; off = align256(off + ids * 4);
+      w.sctl = off; off = align256(off + 16);
+      w.fix_cnt = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
+      w.fix_cur = off; off = align256(off + (uint64_t)p.n_buckets * 4);
+    }
     if (p.super_bits > 0) {
       w.keys2 = off; off = align256(off + n * kb2);
       w.rows2 = off; off = align256(off + n * 4);
@@ -395,8 +389,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.cand_key = off; off = align256(off + n * kb2);
     w.cand_idx = off; off = align256(off + n * 4);
     if (p.merge == PDP_MERGE_RANGES) {
-      const uint64_t recs = (uint64_t)p.n_buckets * ((uint64_t)c->l0 << p.bucket_bits);
-      w.runs = off; off = align256(off + (uint64_t)p.n_buckets * (p.n_ranges + 1) * 4);
+      const uint64_t recs = (uint64_t)p.buckets_out * ((uint64_t)c->l0 << p.bucket_bits);
+      w.runs = off; off = align256(off + (uint64_t)p.buckets_out * (p.n_ranges + 1) * 4);
       w.rec_key = off; off = align256(off + recs * 8);
       if (c->flags & (PDP_ACC_SUM | PDP_SUM_PER_PARTITION)) { w.rec_f0 = off; off = align256(off + recs * 8); }
       if (c->flags & PDP_ACC_NSUM) { w.rec_f1 = off; off = align256(off + recs * 8); }
@@ -464,6 +458,10 @@ struct KP {  // kernel parameters
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
   ClipParams clip;
+  int64_t n_slots1;     // level-1 blocks read by level 2 (Plan.n_slots1)
+  int l2_group_mult;    // tile groups per level-2 workgroup
+  uint32_t sieve_t32;   // threshold sieve: candidate rows have pair_hash < sieve_t32 (0 = off)
+  int sieve_mark;       // bucket kernel: mark privacy ids with < l0 candidate pairs unresolved
 };
 
 KP make_kp(const pdp_bound_config* c, const Plan& p) {
@@ -484,6 +482,10 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.range_bits = p.range_bits;
   k.n_fine_ranges = p.n_fine;
   k.keys_vec = 0;
+  k.n_slots1 = p.n_slots1;
+  k.l2_group_mult = p.sieve ? kSieveL2Groups : 1;
+  k.sieve_t32 = (uint32_t)p.sieve << 16;
+  k.sieve_mark = p.sieve != 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -802,6 +804,15 @@ size_t l1_stage_bytes(int key_format) {
   }
 }
 
+size_t sieve_stage_bytes(int key_format) {
+  switch (key_format) {
+    case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kSieveItems, kL1Threads>);
+    case PDP_KEYS_PACKED:
+    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kSieveItems, kL1Threads>);
+    default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kSieveItems, kL1Threads>);
+  }
+}
+
 // phase 1: histogram + local rank (dest < 0 = drop the row)
 template <typename K, int MAXD, bool ROWS, int N, int TH>
 __device__ __forceinline__ void stage_count(StageLds<K, MAXD, ROWS, N, TH>& s, int ndest, const int (&d)[N],
@@ -915,7 +926,7 @@ __device__ __forceinline__ uint64_t b1_candidate(const KP& kp, const uint2* hpid
 
 // Level 1: tile rows -> super-bucket regions (<= 64 destinations per tile).
 template <int FMT>
-__global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
+__global__ void __launch_bounds__(kL1Threads)  k_scatter_l1(KP kp, const int64_t* __restrict__ pid,
                                                              const int64_t* __restrict__ pk,
                                                              const uint8_t* __restrict__ allowed,
                                                              const unsigned* __restrict__ super_off,
@@ -988,18 +999,12 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1(KP kp, con
         x[q] = (K)(is_dead ? ((1ULL << 63) | midv) : (midv | (uint64_t)k[q]));
       }
     }
-#if PDP_L1_PREFETCH
-    // next sub-chunk's column loads go out before this one's LDS passes
-    if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
-#endif
     unsigned rank[kL1Items];
     stage_count(s, nd, d, rank);
     stage_write(s, nd, d, rank, x, r, keys1, rows1);
     for (int B = threadIdx.x; B < nd; B += blockDim.x) s.gcur[B] += s.hist[B];
     __syncthreads();
-#if !PDP_L1_PREFETCH
     if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
-#endif
   }
 }
 
@@ -1013,7 +1018,7 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1(KP kp, con
 // u64 packed records are unpacked into COMPACT (key, row) pairs, the row =
 // tile * 65,536 + tile row, the tile found among the group's run starts.
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kL2Threads) PDP_L2_OCC k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
+__global__ void __launch_bounds__(kL2Threads)  k_scatter_l2(KP kp, const unsigned* __restrict__ super_base,
                                                              const unsigned* __restrict__ super_off,
                                                              const unsigned* __restrict__ bucket_start,
                                                              const unsigned* __restrict__ gcur,
@@ -1021,9 +1026,6 @@ __global__ void __launch_bounds__(kL2Threads) PDP_L2_OCC k_scatter_l2(KP kp, con
                                                              const unsigned* __restrict__ rows1,
                                                              L2Key<FMT>* __restrict__ keys2,
                                                              unsigned* __restrict__ rows2) {
-#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
-  return;  // ablation: only the level-1 pass is meaningful
-#endif
   using KI = L1Key<FMT>;
   using KO = L2Key<FMT>;
   constexpr bool PACKED = FMT == PDP_KEYS_PACKED;
@@ -1176,10 +1178,8 @@ __global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __
 // super-bucket B's run starts in that block.  The tile's rows per bucket
 // (counts_tm, the level-2 cursor input) are counted in LDS on the way, so the
 // privacy-id column is read once (k_part_hist + k_super_scan are not run).
-constexpr int kStagesPerTile = (int)(kTileRows / kL1Rows);
-constexpr int kL2Runs = kL2GroupTiles * kStagesPerTile;  // level-1 runs per level-2 workgroup
 static_assert(kTileRows % kL1Rows == 0, "a tile is a whole number of level-1 stages");
-static_assert(kL2Runs <= kL2Threads && kL2Runs <= 256, "one run per thread in the run scan; u8 run tags");
+static_assert(kL2Runs * kSieveL2Groups <= kL2Threads, "one level-1 slot per thread in the run scan");
 
 // the LDS stage block [0, total) -> dst, 16 bytes per lane
 template <typename K>
@@ -1193,7 +1193,7 @@ __device__ __forceinline__ void copy_block(K* __restrict__ dst, const K* src, un
 }
 
 template <int FMT, bool U16>
-__global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP kp, const int64_t* __restrict__ pid,
+__global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const int64_t* __restrict__ pid,
                                                                    const int64_t* __restrict__ pk,
                                                                    const uint8_t* __restrict__ allowed,
                                                                    unsigned* __restrict__ counts_tm,
@@ -1322,6 +1322,210 @@ __global__ void __launch_bounds__(kL1Threads) PDP_L1_OCC k_scatter_l1_local(KP k
   }
 }
 
+// Threshold-sieve level 1 (Plan.sieve): one 1,024-thread workgroup per
+// 65,536-row tile filters the tile in chunks of kSieveChunk rows.  A row is a
+// candidate when it is live (valid keys, public partition) and its pair hash
+// is below kp.sieve_t32; candidates' level-1 records are appended to an LDS
+// stage (wave-compacted: one LDS atomic per wave and chunk).  When the stage
+// cannot take another chunk, or the tile ends, it is counting-sorted by
+// super-bucket and written as one block right after the tile's previous
+// blocks (keys1 + tile * kSieveTileStride + sbase[slot]) with its run
+// offsets in soff[slot], as k_scatter_l1_local writes a stage;
+// the tile's unused slots get empty runs.  Rows with invalid keys set the
+// error word; dead rows (non-public partitions) are simply dropped.  The
+// tile's candidate counts per bucket feed the level-2 cursors as before.
+template <int FMT, bool U16>
+__global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
+                                                         const int64_t* __restrict__ pk,
+                                                         const uint8_t* __restrict__ allowed,
+                                                         unsigned* __restrict__ counts_tm,
+                                                         unsigned* __restrict__ counts_tm2,
+                                                         uint16_t* __restrict__ soff, unsigned* __restrict__ sbase,
+                                                         L1Key<FMT>* __restrict__ keys1,
+                                                         unsigned* __restrict__ rows1, unsigned* err) {
+  using K = L1Key<FMT>;
+  constexpr bool ROWS = !kPackedL1<FMT>;
+  constexpr int Q = kSieveChunkItems;
+  extern __shared__ unsigned long long stage_raw[];
+  using SL = StageLds<K, kSmallDest, ROWS, kSieveItems, kL1Threads>;
+  SL& s = *reinterpret_cast<SL*>(stage_raw);
+  unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);
+  __shared__ unsigned fill;
+  const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
+  for (int64_t b = threadIdx.x; b < n_words; b += blockDim.x) bh[b] = 0;
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  auto flush_counts = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
+    for (int64_t wd = threadIdx.x; wd < n_words; wd += blockDim.x) {
+      const unsigned v = bh[wd];
+      bh[wd] = 0;
+      if constexpr (U16) {
+        dst[2 * wd] = v & 0xFFFFu;
+        if (2 * wd + 1 < kp.n_buckets) dst[2 * wd + 1] = v >> 16;
+      } else {
+        dst[wd] = v;
+      }
+    }
+  };
+  const int64_t t = blockIdx.x;
+  const int nd = (int)kp.n_supers;
+  const int64_t t0 = t * kTileRows;
+  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  const int mid_bits = kp.bucket_bits + kp.super_bits;
+  const uint32_t t32 = kp.sieve_t32;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  K* const blk = keys1 + t * kSieveTileStride;
+  unsigned* const rblk = ROWS ? rows1 + t * kSieveTileStride : nullptr;
+  unsigned written = 0;  // block-uniform: this tile's records already written
+  int slot = 0;
+  // the stage's `total` records -> counting sort by super-bucket -> block
+  auto flush = [&](unsigned total) {
+    // runs per super-bucket: LDS histogram, one-wave scan
+    for (int B = threadIdx.x; B < nd; B += blockDim.x) s.hist[B] = 0;
+    __syncthreads();
+    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) atomicAdd(s.hist + s.dest[e], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      unsigned carry = 0;
+      for (int base = 0; base < nd; base += 64) {
+        const unsigned v = base + lane < nd ? s.hist[base + lane] : 0;
+        unsigned incl = v;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned up = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += up;
+        }
+        if (base + lane < nd) s.start[base + lane] = s.gcur[base + lane] = carry + incl - v;
+        carry += __shfl(incl, 63, 64);
+      }
+    }
+    __syncthreads();
+    // every record straight to its run: the block (<= kSieveCap records) is
+    // written whole by this workgroup, so its partial lines merge in L2; no
+    // register holds a record across a barrier (the prefetched chunks stay
+    // in flight)
+    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) {
+      const unsigned pos = written + atomicAdd(s.gcur + s.dest[e], 1u);
+      blk[pos] = s.keys[e];
+      if (ROWS) rblk[pos] = s.rows[e];
+    }
+    const int64_t sl = t * kStagesPerTile + slot;
+    for (int B = threadIdx.x; B <= nd; B += blockDim.x)
+      soff[sl * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] : total);
+    if (threadIdx.x == 0) {
+      sbase[sl] = written;
+      fill = 0;
+    }
+    written += total;
+    ++slot;
+    __syncthreads();
+  };
+  auto load = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
+#pragma unroll
+    for (int q = 0; q < Q; q += 2) {
+      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+      if (kp.keys_vec && i + 1 < t1) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+        const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
+        u[q] = a.x;
+        u[q + 1] = a.y;
+        k[q] = c.x;
+        k[q + 1] = c.y;
+      } else {
+        u[q] = i < t1 ? pid[i] : 0;
+        k[q] = i < t1 ? pk[i] : 0;
+        u[q + 1] = i + 1 < t1 ? pid[i + 1] : 0;
+        k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
+      }
+    }
+  };
+  // U16: the tile's counts in two halves (counts_tm, counts_tm2)
+  const bool split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
+  // one chunk: filter, then (its registers free) the loads of the chunk two
+  // ahead go out, then append / flush -- two chunks of loads in flight
+  auto body = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
+    const bool more = c0 + kSieveChunk < t1;  // block-uniform
+    bool cand[Q];
+    int d[Q];
+    K x[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+      cand[q] = false;
+      d[q] = 0;
+      x[q] = 0;
+      if (i >= t1) continue;
+      if (u[q] < 0 || u[q] >= kp.U || k[q] < 0 || k[q] >= kp.P) {  // invalid key: flagged, dropped
+        atomicOr(err, 1u);
+        continue;
+      }
+      if (allowed != nullptr && allowed[k[q]] == 0) continue;  // non-public partition
+      if (pair_hash(kp.seed, u[q], k[q]) >= t32) continue;
+      cand[q] = true;
+      const int64_t bkt = u[q] >> kp.bucket_bits;
+      if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+      else atomicAdd(bh + bkt, 1u);
+      d[q] = (int)(u[q] >> mid_bits);
+      if constexpr (FMT == PDP_KEYS_COMPACT) {
+        x[q] = (K)compact_key(kp, u[q], k[q], false);
+      } else {  // PACKED / PACKED_WIDE
+        x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
+      }
+    }
+    if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
+    // append this wave's candidates at one reserved range of the stage
+    unsigned long long m[Q];
+    unsigned nw = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      m[q] = __ballot(cand[q]);
+      nw += (unsigned)__popcll(m[q]);
+    }
+    unsigned base = 0;
+    if (lane == 0 && nw) base = atomicAdd(&fill, nw);
+    base = __shfl(base, 0, 64);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (cand[q]) {
+        const unsigned pos = base + (unsigned)__popcll(m[q] & below);
+        s.keys[pos] = x[q];
+        s.dest[pos] = (typename SL::D)d[q];
+        if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
+      }
+      base += (unsigned)__popcll(m[q]);
+    }
+    __syncthreads();
+    const unsigned f = fill;
+    if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
+    else __syncthreads();  // every thread has read `fill` before the next chunk's appends
+    if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
+      flush_counts(counts_tm + t * kp.n_buckets);
+      __syncthreads();
+    }
+  };
+  int64_t ua[Q], ka[Q], ub[Q], kb[Q];
+  if (t0 < t1) load(t0, ua, ka);
+  if (t0 + kSieveChunk < t1) load(t0 + kSieveChunk, ub, kb);
+  for (int64_t c0 = t0; c0 < t1; c0 += 2 * kSieveChunk) {
+    body(c0, ua, ka);
+    if (c0 + kSieveChunk < t1) body(c0 + kSieveChunk, ub, kb);  // block-uniform
+  }
+  // the tile's unused slots: empty runs
+  for (int j = slot; j < kStagesPerTile; ++j) {
+    const int64_t sl = t * kStagesPerTile + j;
+    for (int B = threadIdx.x; B <= nd; B += blockDim.x) soff[sl * (nd + 1) + B] = 0;
+    if (threadIdx.x == 0) sbase[sl] = written;
+  }
+  __syncthreads();
+  if (split) {
+    flush_counts(counts_tm2 + t * kp.n_buckets);
+  } else {
+    flush_counts(counts_tm + t * kp.n_buckets);
+    if constexpr (U16)
+      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.n_buckets + b] = 0;
+  }
+}
+
 // Level 2 over tile-local level-1 blocks: workgroup (group g of kL2GroupTiles
 // tiles, super-bucket B) takes B's run from each of the group's stages
 // (kL2Runs runs: keys1[st * kL1Rows + soff[st][B], + soff[st][B + 1])),
@@ -1350,7 +1554,8 @@ template <int FMT>
 constexpr int l2_items() { return sizeof(L2Key<FMT>) == 8 ? kL2Items / 2 : kL2Items; }
 
 template <int FMT, int MAXD>
-__global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+__global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
+                                                                   const unsigned* __restrict__ sbase,
                                                                    const unsigned* __restrict__ bucket_start,
                                                                    const unsigned* __restrict__ gcur,
                                                                    const L1Key<FMT>* __restrict__ keys1,
@@ -1367,40 +1572,51 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
   using SL = StageLds<KO, MAXD, true, NI, kL2Threads>;
   using D = typename SL::D;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
-  __shared__ unsigned rbeg[kL2Runs + 1];  // start of each run in the concatenation
-  __shared__ unsigned rsrc[kL2Runs];      // its first record in keys1
-  __shared__ unsigned wsum[kL2Threads / 64 + 1];
+  // the workgroup's non-empty runs, in slot order
+  __shared__ unsigned rbeg[kL2Threads + 1];  // start of each run in the concatenation
+  __shared__ unsigned rsrc[kL2Threads];      // its first record in keys1
+  __shared__ unsigned rtile[kL2Threads];     // PACKED: first row of its tile
+  __shared__ unsigned wsum[kL2Threads / 64 + 1], wsum2[kL2Threads / 64 + 1];
   // XCD-aware order: a group's workgroups (all super-buckets) run one after
   // another on one XCD (blocks are placed round-robin, linear id % 8), so the
   // cache lines that two neighbouring runs of a stage block share are read
   // from that XCD's L2
+  // a workgroup takes kp.l2_group_mult tile groups (4 with the sieve, whose
+  // blocks hold a fraction of the rows; <= kL2Threads slots, one per thread)
   const int nd = (int)kp.n_supers;
-  const int64_t n_grp = (kp.n_tiles + kL2GroupTiles - 1) / kL2GroupTiles;
+  const int M = kp.l2_group_mult;
+  const int64_t n_grp = (kp.n_tiles + (int64_t)kL2GroupTiles * M - 1) / ((int64_t)kL2GroupTiles * M);
   const int64_t lin = blockIdx.x, kx = lin >> 3;
   const int64_t g = (kx / nd) * 8 + (lin & 7);
   const int B = (int)(kx % nd);
   if (g >= n_grp) return;  // block-uniform
-  const int64_t n_stages = (kp.n + kL1Rows - 1) / kL1Rows;
-  const int64_t S0 = g * kL2Runs;
-  const int nr = (int)(n_stages - S0 < kL2Runs ? n_stages - S0 : kL2Runs);
+  const int64_t S0 = g * kL2Runs * M;
+  const int64_t n_all = kp.n_slots1 - S0 < (int64_t)kL2Runs * M ? kp.n_slots1 - S0 : (int64_t)kL2Runs * M;
   unsigned len = 0, src = 0;
-  if ((int)threadIdx.x < nr) {
-    const uint16_t* o = soff + (S0 + threadIdx.x) * (nd + 1) + B;
+  if ((int64_t)threadIdx.x < n_all) {
+    // block sl starts at sl * kL1Rows, or (sieve, sbase != NULL) at its
+    // tile's region + sbase[sl]
+    const int64_t sl = S0 + threadIdx.x;
+    const uint16_t* o = soff + sl * (nd + 1) + B;
     len = (unsigned)o[1] - (unsigned)o[0];
-    src = (unsigned)((S0 + threadIdx.x) * kL1Rows) + o[0];
+    src = (sbase != nullptr ? (unsigned)((sl / kStagesPerTile) * kSieveTileStride) + sbase[sl]
+                            : (unsigned)(sl * kL1Rows)) + o[0];
   }
-  unsigned total;
+  unsigned total, nnz;
   const unsigned ex = block_excl_scan(len, wsum, &total);
-  if ((int)threadIdx.x < nr) {
-    rbeg[threadIdx.x] = ex;
-    rsrc[threadIdx.x] = src;
+  const unsigned idx = block_excl_scan(len > 0 ? 1u : 0u, wsum2, &nnz);
+  if (len > 0) {
+    rbeg[idx] = ex;
+    rsrc[idx] = src;
+    rtile[idx] = (unsigned)(((S0 + threadIdx.x) / kStagesPerTile) * kTileRows);
   }
-  if ((int)threadIdx.x == nr) rbeg[nr] = total;
+  if (threadIdx.x == 0) rbeg[nnz] = total;
+  const int nr = (int)nnz;
   const int nsub = 1 << kp.super_bits;
   const int64_t s_first = (int64_t)B << kp.super_bits;
   for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
     const int64_t b = s_first + t;
-    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * kp.n_buckets + b] : 0u;
+    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
   }
   __syncthreads();
   if (total == 0) return;  // block-uniform
@@ -1410,9 +1626,11 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
   const uint64_t sub_mask = (uint64_t)nsub - 1;
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   int j0 = 0;  // first run overlapping the window (block-uniform)
-  for (unsigned base = 0; base < total; base += NR) {
-    const unsigned wend = base + NR < total ? base + NR : total;
+  for (unsigned base = 0, wend = 0; base < total; base = wend) {
     while (rbeg[j0 + 1] <= base) ++j0;
+    wend = base + NR < total ? base + NR : total;
+    // at most 256 runs per window (u8 run tags): a cap only tiny runs reach
+    if (j0 + 256 < nr && rbeg[j0 + 256] < wend) wend = rbeg[j0 + 256];
     for (int j = j0 + (int)(threadIdx.x >> 6); j < nr && rbeg[j] < wend; j += nw) {
       const unsigned a = rbeg[j] > base ? rbeg[j] : base;
       const unsigned e = rbeg[j + 1] < wend ? rbeg[j + 1] : wend;
@@ -1439,7 +1657,7 @@ __global__ void __launch_bounds__(kL2Threads, PDP_L2L_WAVES) k_scatter_l2_local(
           const unsigned i = rsrc[j] + (v - rbeg[j]);
           raw[q] = keys1[i];
           if (ROWS1) rr[q] = rows1[i];
-          else rr[q] = (unsigned)(((S0 + j) / kStagesPerTile) * kTileRows);
+          else rr[q] = rtile[j];
         }
       }
 #pragma unroll
@@ -1585,41 +1803,12 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
         return 0u;
       }
     };
-#if PDP_PIPE
     // software pipeline: the next batch's loads are in flight while this
     // batch runs through the queue (LDS work only, no vector memory)
     KV nk[KU];
     RV nr[KU];
     const bool more = g0 + step < np;  // block-uniform
     if (more) load(g0 + step, nk, nr);
-#endif
-#if PDP_BATCH_PRED
-    // every record's key conversion and predicate first (their LDS reads issue
-    // back to back under one wait), then the wave-serial queue pushes; a
-    // predicate evaluated before earlier pushes' work ran is only weaker (the
-    // sketch maxima only decrease), and work() re-checks
-    uint64_t xs[KU * R];
-    bool ps[KU * R];
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-      if constexpr (R == 4) {
-        xs[u * 4 + 0] = conv(kx[u].x);
-        xs[u * 4 + 1] = conv(kx[u].y);
-        xs[u * 4 + 2] = conv(kx[u].z);
-        xs[u * 4 + 3] = conv(kx[u].w);
-      } else {
-        xs[u * 2 + 0] = conv(kx[u].x);
-        xs[u * 2 + 1] = conv(kx[u].y);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < KU * R; ++i) ps[i] = pred(xs[i]);
-#pragma unroll
-    for (int u = 0; u < KU; ++u) {
-#pragma unroll
-      for (int e = 0; e < R; ++e) push_p(xs[u * R + e], rowv(u, e), ps[u * R + e]);
-    }
-#else
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
       if constexpr (R == 4) {
@@ -1632,8 +1821,6 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
         push(conv(kx[u].y), rowv(u, 1));
       }
     }
-#endif
-#if PDP_PIPE
     if (more) {
 #pragma unroll
       for (int u = 0; u < KU; ++u) {
@@ -1641,9 +1828,6 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
         if (LOADR) rx[u] = nr[u];
       }
     }
-#else
-    if (g0 + step < np) load(g0 + step, kx, rx);
-#endif
   }
   if (n > 0) {  // partial wave
     wave_lds_fence();
@@ -1666,10 +1850,10 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
                                                                  const void* __restrict__ value,
                                                                  pdp_partition_accumulators acc, PairRecords rec,
                                                                  RecKey<COMPACT>* __restrict__ cand_key,
-                                                                 unsigned* __restrict__ cand_idx) {
-#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
-  return;  // ablation: only the level-1 pass is meaningful
-#endif
+                                                                 unsigned* __restrict__ cand_idx,
+                                                                 unsigned* __restrict__ unres_bits,
+                                                                 unsigned* __restrict__ unres_list,
+                                                                 unsigned* __restrict__ sctl, unsigned* __restrict__ err) {
   extern __shared__ unsigned long long smem[];
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
@@ -1723,31 +1907,18 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   if (threadIdx.x == 0) ccount = 0;
   __syncthreads();
   const uint64_t lbits = ((uint64_t)1 << (kp.pk_bits + kp.bucket_bits)) - 1;  // local pid | partition
-  stream_bucket<COMPACT ? PDP_B1_KU_COMPACT : kUnroll, kRowIndex>(
+  stream_bucket<COMPACT ? 4 : kUnroll, kRowIndex>(
       keys, rowidx, begin, end, wq,
-#if PDP_B1_THR
       // the candidate test rides on the pid-hash read (b1_candidate)
       [&](RecKey<COMPACT> v) -> uint64_t { return b1_candidate(kp, hpid, v); },
       [&](uint64_t x) { return x != kEmpty; },
-#else
-      conv,
-      [&](uint64_t x) {
-        return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
-      },
-#endif
-      [&](uint64_t x, uint32_t i) PDP_WORK_ATTR {
+      [&](uint64_t x, uint32_t i)  {
         const int64_t pl = (int64_t)((x >> kp.pk_bits) & bmask);
         unsigned long long* s = sk + pl;
-#if PDP_INSERT_SKIP
-        if (x < s[(l0 - 1) * S]) sketch_insert_strided_skip(s, l0, S, x);
-#else
         if (x < s[(l0 - 1) * S]) sketch_insert_strided(s, l0, S, x);
-#endif
         const unsigned long long smax = s[(l0 - 1) * S];
-#if PDP_B1_THR
         // a maximum read after this insert: never below the current one
         hpid[pl].y = (uint32_t)(smax >> 32);
-#endif
         const bool keep = x <= smax;
         const unsigned long long active = __ballot(true);
         const unsigned long long m = __ballot(keep);
@@ -1762,22 +1933,48 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
         }
       });
   __syncthreads();
+  if (kp.sieve_mark) {
+    // threshold sieve: a privacy id with fewer than l0 candidate pairs (its
+    // sketch not full) may have kept pairs among its sieved-out rows; mark it
+    // in the bitmap (a wave covers 64 ids = one u64 word; the bucket's ids
+    // are whole words) and list it, and emit nothing for it here (B2 skips
+    // it): the fix-up recomputes it from all of its rows
+    const int lane = threadIdx.x & 63;
+    const int64_t id0 = b << kp.bucket_bits;
+    for (int64_t p0 = (int64_t)(threadIdx.x >> 6) * 64; p0 < S; p0 += blockDim.x) {
+      const bool un = id0 + p0 + lane < kp.U && sk[(int64_t)(l0 - 1) * S + p0 + lane] == kEmpty;
+      const unsigned long long m = __ballot(un);
+      if (lane == 0) reinterpret_cast<uint2*>(unres_bits)[(id0 + p0) >> 6] = make_uint2((unsigned)m, (unsigned)(m >> 32));
+      if (m) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(sctl, (unsigned)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (un) unres_list[base + __popcll(m & ((1ULL << lane) - 1))] = (unsigned)(id0 + p0 + lane);
+      }
+    }
+  }
 #ifdef PDP_ABL_B1_ONLY
   return;
 #endif
   // B2: rows of kept pairs, from B1's candidate list (the row index gathered
   // for the rows of kept pairs only)
   const int flags = kp.clip.flags;
-  stream_bucket<COMPACT ? PDP_B2_KU_COMPACT : kUnroll / 2, kRowLoad>(
+  stream_bucket<COMPACT ? 1 : kUnroll / 2, kRowLoad>(
       cand_key, cand_idx, begin, begin + ccount, wq, conv,
       [&](uint64_t x) {
-        return !dead_key(x, kp.rand_shift) && x <= sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
+        if (dead_key(x, kp.rand_shift)) return false;
+        const unsigned long long smax = sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
+        return x <= smax && !(kp.sieve_mark && smax == kEmpty);  // sieve: unresolved ids are the fix-up's
       },
-      [&](uint64_t x, uint32_t ci) PDP_WORK_ATTR {
+      [&](uint64_t x, uint32_t ci)  {
       const int64_t pl = (x >> kp.pk_bits) & bmask;
       const int j = sketch_find_strided(sk + pl, l0, S, x);
       if (j < 0) return;
       const uint32_t r = rowidx[ci];
+      if (r >= (uint64_t)kp.n) {  // malformed record: flagged, never dereferenced
+        atomicOr(err, 1u);
+        return;
+      }
       const int64_t slot = j * S + pl;  // entry j of pid pl (structure of arrays)
       atomicAdd(cnt + slot, 1u);
       if (!KEEP_ALL_ROWS) {
@@ -1808,7 +2005,6 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
 #ifdef PDP_ABL_NO_B3
   return;
 #endif
-#if PDP_GATHER_VALUES
   if (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) {
     // B2.5: the kept rows' values replace their row keys in the row sketches,
     // all of a thread's gathers in flight together (B3 then reads LDS only;
@@ -1836,15 +2032,12 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     __syncthreads();
   }
   const void* const b3_value = (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) ? nullptr : value;
-#else
-  const void* const b3_value = value;
-#endif
   unsigned* run = nullptr;
   if (RANGES) {
     // B3a: kept pairs per partition range -> this bucket's run starts
     for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
       const uint64_t x = sk[slot];
-      if (x == kEmpty || cnt[slot] == 0) continue;
+      if (x == kEmpty || cnt[slot] == 0 || (int64_t)(x & kp.pk_mask) >= kp.P) continue;
       atomicAdd(rh + ((x & kp.pk_mask) >> kp.range_bits), 1u);
     }
     __syncthreads();
@@ -1866,6 +2059,10 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     const int64_t p = (int64_t)(x & kp.pk_mask);
     const unsigned c = cnt[slot];
     if (c == 0) continue;
+    if (p >= kp.P) {  // malformed record (pk_mask spans up to 2^pk_bits > P): flagged, skipped
+      atomicOr(err, 1u);
+      continue;
+    }
     PairSums ps;
     if (!KEEP_ALL_ROWS) {
       const long long m = c < (unsigned)kp.linf ? (long long)c : (long long)kp.linf;
@@ -1885,6 +2082,119 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     } else {
       add_pair_to_partition(acc, p, ps, flags);
     }
+  }
+}
+
+// ------------------------------------------------ threshold-sieve fix-up --
+// Bloom hash of a privacy id: word index from bits [0, 14), three bit
+// positions from bits [15, 30) (one LDS word per test)
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t id) { return fmix32(id * 0x9E3779B1u + 0x7F4A7C15u); }
+__device__ __forceinline__ unsigned bloom_bits(uint32_t h) {
+  return (1u << ((h >> 15) & 31)) | (1u << ((h >> 20) & 31)) | (1u << ((h >> 25) & 31));
+}
+
+// Fix-up step 1: every row of an unresolved privacy id.  One streaming read
+// of the privacy-id column (8 B per row); a row is tested against an LDS Bloom
+// filter of the unresolved list (one word, three bits; each workgroup builds
+// its own) and, on a hit, against the exact bitmap.  Rows of unresolved ids
+// are appended to fix_rec as (privacy id << 32 | row) -- one returning atomic
+// per wave and batch -- and counted per bucket.  No unresolved id: no work.
+__global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const int64_t* __restrict__ pid,
+                                                                 const unsigned* __restrict__ unres_bits,
+                                                                 const unsigned* __restrict__ unres_list,
+                                                                 unsigned* __restrict__ sctl,
+                                                                 unsigned* __restrict__ fix_cnt,
+                                                                 unsigned long long* __restrict__ fix_rec) {
+  __shared__ unsigned bloom[kBloomWords];
+  const unsigned n_unres = sctl[0];
+  if (n_unres == 0) return;  // grid-uniform
+  for (int i = threadIdx.x; i < kBloomWords; i += blockDim.x) bloom[i] = 0;
+  __syncthreads();
+  for (unsigned i = threadIdx.x; i < n_unres; i += blockDim.x) {
+    const uint32_t h = bloom_hash(unres_list[i]);
+    atomicOr(bloom + (h & (kBloomWords - 1)), bloom_bits(h));
+  }
+  __syncthreads();
+  constexpr int KU = 8;  // 16-byte loads (two rows) in flight per lane
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  const int64_t n_pairs = (kp.n + 1) / 2;
+  const int64_t step = (int64_t)gridDim.x * blockDim.x * KU;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x * KU; g0 < n_pairs; g0 += step) {  // block-uniform trips
+    int64_t u[2 * KU];
+#pragma unroll
+    for (int v = 0; v < KU; ++v) {
+      const int64_t i = 2 * (g0 + (int64_t)v * blockDim.x + threadIdx.x);
+      if (kp.keys_vec && i + 1 < kp.n) {
+        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+        u[2 * v] = a.x;
+        u[2 * v + 1] = a.y;
+      } else {
+        u[2 * v] = i < kp.n ? pid[i] : -1;
+        u[2 * v + 1] = i + 1 < kp.n ? pid[i + 1] : -1;
+      }
+    }
+    bool hit[2 * KU];
+#pragma unroll
+    for (int e = 0; e < 2 * KU; ++e) {
+      hit[e] = false;
+      if (u[e] < 0 || u[e] >= kp.U) continue;  // invalid ids were flagged by level 1
+      const uint32_t h = bloom_hash((uint32_t)u[e]);
+      const unsigned bits = bloom_bits(h);
+      if ((bloom[h & (kBloomWords - 1)] & bits) != bits) continue;
+      hit[e] = (unres_bits[u[e] >> 5] >> (u[e] & 31)) & 1u;
+    }
+    unsigned long long m[2 * KU];
+    unsigned nw = 0;
+#pragma unroll
+    for (int e = 0; e < 2 * KU; ++e) {
+      m[e] = __ballot(hit[e]);
+      nw += (unsigned)__popcll(m[e]);
+    }
+    if (nw == 0) continue;  // wave-uniform
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(sctl + 1, nw);
+    base = __shfl(base, 0, 64);
+#pragma unroll
+    for (int e = 0; e < 2 * KU; ++e) {
+      if (hit[e]) {
+        const int64_t i = 2 * (g0 + (int64_t)(e / 2) * blockDim.x + threadIdx.x) + (e & 1);
+        fix_rec[base + __popcll(m[e] & below)] = ((unsigned long long)u[e] << 32) | (unsigned long long)(uint32_t)i;
+        atomicAdd(fix_cnt + (u[e] >> kp.bucket_bits), 1u);
+      }
+      base += (unsigned)__popcll(m[e]);
+    }
+  }
+}
+
+// Fix-up step 2: the listed rows -> bucket order (fix_start = exclusive scan
+// of the per-bucket counts; a slot per row from the bucket's cursor), as the
+// bucket kernel's records: (bucket-local pid << pk_bits | partition), dead
+// bit for a non-public or invalid partition, and the row.
+template <bool COMPACT>
+__global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __restrict__ pk,
+                                                        const uint8_t* __restrict__ allowed,
+                                                        const unsigned long long* __restrict__ fix_rec,
+                                                        const unsigned* __restrict__ sctl,
+                                                        const unsigned* __restrict__ fix_start,
+                                                        unsigned* __restrict__ fix_cur,
+                                                        RecKey<COMPACT>* __restrict__ keys, unsigned* __restrict__ rows) {
+  const int64_t total = sctl[1];
+  const uint64_t lmask = ((uint64_t)1 << kp.bucket_bits) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t e = fix_rec[i];
+    const uint64_t u = e >> 32;
+    const uint32_t r = (uint32_t)e;
+    const int64_t k = pk[r];
+    const bool dead = k < 0 || k >= kp.P || (allowed != nullptr && allowed[k] == 0);
+    const uint64_t lpk = (u & lmask) << kp.pk_bits;
+    const int64_t b = (int64_t)(u >> kp.bucket_bits);
+    const unsigned pos = fix_start[b] + atomicAdd(fix_cur + b, 1u);
+    if constexpr (COMPACT)
+      keys[pos] = (uint32_t)(dead ? (0x80000000ull | lpk) : (lpk | (uint64_t)k));
+    else
+      keys[pos] = dead ? ((1ull << 63) | lpk) : (lpk | (uint64_t)k);
+    rows[pos] = r;
   }
 }
 
@@ -1947,10 +2257,7 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
 // directly).
 __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec, const uint4* __restrict__ items,
                                                                const unsigned* __restrict__ n_items,
-                                                               pdp_partition_accumulators acc) {
-#if defined(PDP_ABL_L1_NOPRO) || defined(PDP_ABL_L1_NOSTAGE)
-  return;  // ablation: only the level-1 pass is meaningful
-#endif
+                                                               pdp_partition_accumulators acc, unsigned* err) {
   extern __shared__ unsigned long long smem[];
   double* s0 = (double*)smem;               // [kRangeParts] sum
   double* s1 = s0 + kRangeParts;            // normalized sum
@@ -2029,6 +2336,11 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
 #pragma unroll
       for (int u = 0; u < RR; ++u) {
         if (!ok[u]) continue;
+        // a record outside this item's range (malformed workspace): flagged, skipped
+        if ((int64_t)(key[u] >> 32) >= kp.P || (key[u] >> 32) - (uint64_t)p0 >= (uint64_t)kRangeParts) {
+          atomicOr(err, 1u);
+          continue;
+        }
         if (direct) {
           const int64_t p = (int64_t)(key[u] >> 32);
           atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
@@ -2141,8 +2453,11 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecord
   item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
               [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (ok[u]) atomicAdd(lh + (int)((rec.key[idx[u]] >> (32 + kRangeBits)) - f0), 1u);
+                for (int u = 0; u < 4; ++u) {
+                  if (!ok[u]) continue;
+                  const uint64_t f = (rec.key[idx[u]] >> (32 + kRangeBits)) - (uint64_t)f0;
+                  if (f < (uint64_t)F) atomicAdd(lh + (int)f, 1u);  // else malformed: k_split_scatter skips it too
+                }
               },
               [] {});
   __syncthreads();
@@ -2175,11 +2490,14 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairReco
                 unsigned long long key[4];
                 int f[4];
                 unsigned rank[4];
+                bool live[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                   key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
-                  f[u] = (int)((key[u] >> (32 + kRangeBits)) - f0);
-                  rank[u] = ok[u] ? atomicAdd(lh + f[u], 1u) : 0u;
+                  const uint64_t fu = (key[u] >> (32 + kRangeBits)) - (uint64_t)f0;
+                  live[u] = ok[u] && fu < (uint64_t)F;  // a malformed record is skipped (k_split_count too)
+                  f[u] = live[u] ? (int)fu : 0;
+                  rank[u] = live[u] ? atomicAdd(lh + f[u], 1u) : 0u;
                 }
                 __syncthreads();
                 // reserve: lh[t] -> this round's base of fine range t (then 0)
@@ -2190,7 +2508,7 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairReco
                 __syncthreads();
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                  if (!ok[u]) continue;
+                  if (!live[u]) continue;
                   const uint64_t o = (uint64_t)lh[f[u]] + rank[u];
                   stg.key[o] = key[u];
                   if (stg.f0) stg.f0[o] = rec.f0[idx[u]];
@@ -2224,7 +2542,7 @@ __global__ void __launch_bounds__(kBlock) k_fine_plan(KP kp, const unsigned* __r
 // summed in LDS (or added directly when few), then coalesced atomics
 __global__ void __launch_bounds__(kRangeThreads) k_fine_reduce(KP kp, PairRecords stg, const uint4* __restrict__ items,
                                                               const unsigned* __restrict__ n_items,
-                                                              pdp_partition_accumulators acc) {
+                                                              pdp_partition_accumulators acc, unsigned* err) {
   extern __shared__ unsigned long long smem[];
   double* s0 = (double*)smem;
   double* s1 = s0 + kRangeParts;
@@ -2253,6 +2571,10 @@ __global__ void __launch_bounds__(kRangeThreads) k_fine_reduce(KP kp, PairRecord
   for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
     const uint64_t o = a + i;
     const unsigned long long key = stg.key[o];
+    if ((int64_t)(key >> 32) >= kp.P || (key >> 32) - (uint64_t)p0 >= (uint64_t)kRangeParts) {  // malformed
+      atomicOr(err, 1u);
+      continue;
+    }
     const double v0 = f0 ? stg.f0[o] : 0.0, v1 = f1 ? stg.f1[o] : 0.0, v2 = f2 ? stg.f2[o] : 0.0;
     if (direct) {
       const int64_t p = (int64_t)(key >> 32);
@@ -2451,8 +2773,9 @@ int launch_global_reduce(const KP& kp, hipStream_t st, const void* value, const 
 }
 
 template <int VK, bool KA>
-int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w, const void* value,
-                  const pdp_partition_accumulators& acc) {
+int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void* keys, const unsigned* rows,
+                         const unsigned* offsets, const void* value, const pdp_partition_accumulators& acc,
+                         PairRecords rec, char* ws, const Ws& w, const char* name) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
   // PACKED: COMPACT records from level 2 on; PACKED_WIDE: WIDE ones
   const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
@@ -2460,27 +2783,94 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
                                        : (const void*)k_bucket_bound<VK, KA, false, true>)
                              : (ranges ? (const void*)k_bucket_bound<VK, KA, true, false>
                                        : (const void*)k_bucket_bound<VK, KA, false, false>);
+  PDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes));
+  void* cand_key = ws + w.cand_key;
+  unsigned* cand_idx = (unsigned*)(ws + w.cand_idx);
+  unsigned* unres_bits = w.unres_bits ? (unsigned*)(ws + w.unres_bits) : nullptr;
+  unsigned* unres_list = w.unres_list ? (unsigned*)(ws + w.unres_list) : nullptr;
+  unsigned* sctl = w.sctl ? (unsigned*)(ws + w.sctl) : nullptr;
+  unsigned* err = (unsigned*)(ws + w.err);
+  void* args[] = {(void*)&kp,       (void*)&keys,       (void*)&rows,       (void*)&offsets,
+                  (void*)&value,    (void*)&acc,        (void*)&rec,        (void*)&cand_key,
+                  (void*)&cand_idx, (void*)&unres_bits, (void*)&unres_list, (void*)&sctl,
+                  (void*)&err};
+  PDP_PROF_BEGIN(name, st);
+  PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+PairRecords pair_records(char* ws, const Ws& w) {
   PairRecords rec{};
-  if (ranges) {
+  if (w.runs) {
     rec.runs = (unsigned*)(ws + w.runs);
     rec.key = (unsigned long long*)(ws + w.rec_key);
     rec.f0 = w.rec_f0 ? (double*)(ws + w.rec_f0) : nullptr;
     rec.f1 = w.rec_f1 ? (double*)(ws + w.rec_f1) : nullptr;
     rec.f2 = w.rec_f2 ? (double*)(ws + w.rec_f2) : nullptr;
   }
-  PDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes));
-  const void* keys2 = ws + w.keys2;
-  const unsigned* rows2 = (const unsigned*)(ws + w.rows2);
-  const unsigned* counts = (const unsigned*)(ws + w.counts);
-  void* cand_key = ws + w.cand_key;
-  unsigned* cand_idx = (unsigned*)(ws + w.cand_idx);
-  void* args[] = {(void*)&kp,  (void*)&keys2, (void*)&rows2,    (void*)&counts,  (void*)&value,
-                  (void*)&acc, (void*)&rec,   (void*)&cand_key, (void*)&cand_idx};
-  PDP_PROF_BEGIN("k_bucket_bound", st);
-  PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
+  return rec;
+}
+
+// Sampling (every bucket kernel): the main launch over the level-2 records;
+// with the sieve, the fix-up of the unresolved privacy ids (rescan of the
+// privacy-id column, scatter into bucket order, a second launch whose pair
+// records follow the main ones: buckets [n_buckets, 2 n_buckets) of `rec`).
+template <int VK, bool KA>
+int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
+                   const uint8_t* allowed, const void* value, const pdp_partition_accumulators& acc, char* ws,
+                   const Ws& w) {
+  const PairRecords rec = pair_records(ws, w);
+  int rc = launch_bucket_kernel<VK, KA>(kp, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
+                                        (const unsigned*)(ws + w.counts), value, acc, rec, ws, w, "k_bucket_bound");
+  if (rc != PDP_OK || !p.sieve) return rc;
+  unsigned* sctl = (unsigned*)(ws + w.sctl);
+  unsigned* fix_cnt = (unsigned*)(ws + w.fix_cnt);
+  unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
+  PDP_PROF_BEGIN("k_sieve_rescan", st);
+  hipLaunchKernelGGL(k_sieve_rescan, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
+                     (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
+                     fix_rec);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  if (ranges) {
+  rc = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts
+  if (rc != PDP_OK) return rc;
+  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
+  const unsigned fix_grid = grid_for(kp.n, 2048);
+  PDP_PROF_BEGIN("k_fix_scatter", st);
+  if (compact)
+    hipLaunchKernelGGL(k_fix_scatter<true>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                       (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt,
+                       (unsigned*)(ws + w.fix_cur), (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+  else
+    hipLaunchKernelGGL(k_fix_scatter<false>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                       (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt,
+                       (unsigned*)(ws + w.fix_cur), (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  KP kf = kp;
+  kf.sieve_mark = 0;  // every row of these privacy ids is here
+  PairRecords fr = rec;
+  const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
+  fr.runs += p.n_buckets * (p.n_ranges + 1);
+  fr.key += p.n_buckets * n_slots;
+  if (fr.f0) fr.f0 += p.n_buckets * n_slots;
+  if (fr.f1) fr.f1 += p.n_buckets * n_slots;
+  if (fr.f2) fr.f2 += p.n_buckets * n_slots;
+  return launch_bucket_kernel<VK, KA>(kf, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
+                                      (const unsigned*)fix_cnt, value, acc, fr, ws, w, "k_bucket_fix");
+}
+
+// PDP_MERGE_RANGES: the pair records of every bucket (p.buckets_out of them)
+// summed per partition
+int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const Ws& w,
+                 const pdp_partition_accumulators& acc) {
+  KP kp = kp0;
+  kp.n_buckets = p.buckets_out;
+  const PairRecords rec = pair_records(ws, w);
+  unsigned* err = (unsigned*)(ws + w.err);
+  {
     PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_range_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kRangeLds));
     uint4* items = (uint4*)(ws + w.rr_items);
@@ -2494,7 +2884,7 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
     if (!p.two_level) {
       PDP_PROF_BEGIN("k_range_reduce", st);
       hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kRangeThreads), kRangeLds, st, kp, rec,
-                         (const uint4*)items, (const unsigned*)n_items, acc);
+                         (const uint4*)items, (const unsigned*)n_items, acc, err);
       PDP_PROF_END(st);
       PDP_HIP_CHECK(hipGetLastError());
       return PDP_OK;
@@ -2534,7 +2924,7 @@ int launch_bucket(const KP& kp, const Plan& p, hipStream_t st, char* ws, const W
                                       (int)kFineLds));
     PDP_PROF_BEGIN("k_fine_reduce", st);
     hipLaunchKernelGGL(k_fine_reduce, dim3((unsigned)p.fine_items), dim3(kRangeThreads), kFineLds, st, kp, stg,
-                       (const uint4*)fitems, (const unsigned*)n_fitems, acc);
+                       (const uint4*)fitems, (const unsigned*)n_fitems, acc, err);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
@@ -2587,21 +2977,37 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = !kPackedL1<FMT>;
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
-  const bool u16 = l1_hist_u16(FMT, p.n_buckets);
+  const bool u16 = p.sieve ? sieve_hist_u16(FMT, p.n_buckets) : l1_hist_u16(FMT, p.n_buckets);
   unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
+  unsigned* sbase = p.sieve ? (unsigned*)(ws + w.sbase) : nullptr;
   K1* keys1 = (K1*)(ws + w.keys1);
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
-  const size_t lds1 = (l1_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
-  const void* l1 = u16 ? (const void*)k_scatter_l1_local<FMT, true> : (const void*)k_scatter_l1_local<FMT, false>;
-  PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
-  void* args1[] = {(void*)&kp,         (void*)&pid,  (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
-                   (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err};
-  PDP_PROF_BEGIN("k_scatter_l1", st);
-  PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
+  if constexpr (FMT != PDP_KEYS_WIDE) {
+    if (p.sieve) {
+      const size_t lds1 = (sieve_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
+      const void* l1 = u16 ? (const void*)k_sieve_l1<FMT, true> : (const void*)k_sieve_l1<FMT, false>;
+      PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+      void* args1[] = {(void*)&kp,   (void*)&pid,   (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
+                       (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err};
+      PDP_PROF_BEGIN("k_sieve_l1", st);
+      PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
+      PDP_PROF_END(st);
+      PDP_HIP_CHECK(hipGetLastError());
+    }
+  }
+  if (!p.sieve) {
+    const size_t lds1 = (l1_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
+    const void* l1 = u16 ? (const void*)k_scatter_l1_local<FMT, true> : (const void*)k_scatter_l1_local<FMT, false>;
+    PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+    void* args1[] = {(void*)&kp,         (void*)&pid,  (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
+                     (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err};
+    PDP_PROF_BEGIN("k_scatter_l1", st);
+    PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
   const int64_t n_bblk = (p.n_buckets + 63) / 64;
   const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
   unsigned* csum = (unsigned*)(ws + w.csum);
@@ -2632,20 +3038,111 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
                             : sizeof(StageLds<K2, kMaxDest, true, l2_items<FMT>(), kL2Threads>);
   PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
   const uint16_t* soff_c = soff;
+  const unsigned* sbase_c = sbase;
   const unsigned* counts_c = counts;
   const unsigned* gcur_c = gcur;
   const K1* keys1_c = keys1;
   const unsigned* rows1_c = rows1;
   K2* keys2 = (K2*)(ws + w.keys2);
   unsigned* rows2 = (unsigned*)(ws + w.rows2);
-  void* args[] = {(void*)&kp, (void*)&soff_c, (void*)&counts_c, (void*)&gcur_c, (void*)&keys1_c, (void*)&rows1_c,
-                  (void*)&keys2, (void*)&rows2};
+  void* args[] = {(void*)&kp,       (void*)&soff_c,  (void*)&sbase_c, (void*)&counts_c, (void*)&gcur_c,
+                  (void*)&keys1_c, (void*)&rows1_c, (void*)&keys2,   (void*)&rows2};
   PDP_PROF_BEGIN("k_scatter_l2", st);
-  const int64_t n_blk = (n_grp + 7) / 8 * 8 * p.n_supers;  // k_scatter_l2_local maps ids to (group, super)
+  const int64_t n_mgrp = (n_grp + kp.l2_group_mult - 1) / kp.l2_group_mult;  // tile groups per workgroup
+  const int64_t n_blk = (n_mgrp + 7) / 8 * 8 * p.n_supers;  // k_scatter_l2_local maps ids to (group, super)
   PDP_HIP_CHECK(hipLaunchKernel(l2, dim3((unsigned)n_blk), dim3(kL2Threads), args, lds2, st));
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
+}
+
+// PDP_DEBUG_CORRUPT_RECORDS (tests only): every level-2 record of bucket 0
+// gets the all-ones partition (>= P when P is not a power of two) and every
+// record of bucket 1 an out-of-range row, as a malformed workspace would
+// carry; the bucket kernel must flag them in the error word, not fault
+template <bool COMPACT>
+__global__ void __launch_bounds__(kBlock) k_debug_corrupt(KP kp, const unsigned* __restrict__ starts,
+                                                          RecKey<COMPACT>* __restrict__ keys,
+                                                          unsigned* __restrict__ rows) {
+  const int64_t nb = kp.n_buckets < 2 ? kp.n_buckets : 2;
+  for (int64_t i = (int64_t)starts[0] + blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)starts[nb];
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < (int64_t)starts[1]) keys[i] = keys[i] | (RecKey<COMPACT>)kp.pk_mask;
+    else rows[i] = 0xFFFFFFF0u;
+  }
+}
+
+int launch_debug_corrupt(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w) {
+  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
+  const unsigned* starts = (const unsigned*)(ws + w.counts);
+  if (compact)
+    hipLaunchKernelGGL(k_debug_corrupt<true>, dim3(64), dim3(kBlock), 0, st, kp, starts, (uint32_t*)(ws + w.keys2),
+                       (unsigned*)(ws + w.rows2));
+  else
+    hipLaunchKernelGGL(k_debug_corrupt<false>, dim3(64), dim3(kBlock), 0, st, kp, starts,
+                       (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
+// histogram pass over the privacy ids -> global offsets -> level 1 -> level 2
+// (plans whose tile-local level 1 does not fit)
+int launch_offsets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* privacy_id,
+                   const int64_t* partition_key, const uint8_t* pk_allowed, char* ws, const Ws& w, unsigned* err) {
+  unsigned* counts = (unsigned*)(ws + w.counts);
+  unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
+  unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);
+  const size_t hist_lds = (size_t)p.n_buckets * 4;
+  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)hist_lds));
+  PDP_PROF_BEGIN("k_part_hist", st);
+  unsigned* super_tm = (unsigned*)(ws + w.super_tm);
+  unsigned* super_off = (unsigned*)(ws + w.super_off);
+  hipLaunchKernelGGL(k_part_hist, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
+                     counts_tm, super_tm, err);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_super_scan", st);
+  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  // rows per bucket (and, with two levels, the level-2 cursors at tile-group starts)
+  const int64_t n_bblk = (p.n_buckets + 63) / 64;
+  const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
+  unsigned* csum = (unsigned*)(ws + w.csum);
+  unsigned* gcur = (unsigned*)(ws + w.gcur);
+  PDP_PROF_BEGIN("k_gscan_sums", st);
+  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
+                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum, (unsigned*)nullptr);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_gscan_chunks", st);
+  hipLaunchKernelGGL(k_gscan_chunks, dim3(grid_for(p.n_buckets)), dim3(kBlock), 0, st, csum, n_sc, p.n_buckets,
+                     counts);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  if (p.super_bits > 0) {
+    PDP_PROF_BEGIN("k_gscan_cursors", st);
+    hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
+                       counts_tm, (const unsigned*)nullptr, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
+  const int rc = scan_u32(counts, p.n_buckets, chunk_sums, st);
+  if (rc != PDP_OK) return rc;
+  unsigned* super_base = (unsigned*)(ws + w.super_base);
+  PDP_PROF_BEGIN("k_super_bases", st);
+  hipLaunchKernelGGL(k_super_bases, dim3(grid_for(p.n_supers + 1)), dim3(kBlock), 0, st, kp, counts, super_base);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  if (p.key_format == PDP_KEYS_COMPACT)
+    return launch_scatter<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                            counts, gcur, ws, w, err);
+  if (p.key_format == PDP_KEYS_PACKED)
+    return launch_scatter<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                           counts, gcur, ws, w, err);
+  return launch_scatter<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
+                                       counts, gcur, ws, w, err);
 }
 
 template <template <int, bool> class F, typename... A>
@@ -2671,9 +3168,9 @@ struct GlobalReduce {
   static int run(A&&... a) { return launch_global_reduce<VK, KA>(a...); }
 };
 template <int VK, bool KA>
-struct Bucket {
+struct Buckets {
   template <typename... A>
-  static int run(A&&... a) { return launch_bucket<VK, KA>(a...); }
+  static int run(A&&... a) { return launch_buckets<VK, KA>(a...); }
 };
 
 int check_ws(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes, Plan* p, Ws* w) {
@@ -2720,6 +3217,7 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->n_ranges = p.n_ranges;
   info->range_group = p.range_group;
   info->key_format = p.key_format;
+  info->sieve = p.sieve;
   return PDP_OK;
 }
 
@@ -2742,6 +3240,9 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     return set_error(PDP_E_INVALID, "key columns are NULL");
   if (cfg->value_kind != PDP_VALUE_NONE && cfg->n_rows > 0 && value == nullptr)
     return set_error(PDP_E_INVALID, "value column is NULL");
+  if (cfg->value_kind == PDP_VALUE_NONE &&
+      (cfg->flags & (PDP_ACC_SUM | PDP_ACC_NSUM | PDP_ACC_NSUM2 | PDP_SUM_PER_PARTITION)))
+    return set_error(PDP_E_INVALID, "value sums requested without a value column");
   hipStream_t st = (hipStream_t)stream;
   char* ws = (char*)workspace;
   if (pairs_mode(cfg)) return pairs_bound(cfg, privacy_id, partition_key, value, pk_allowed, ws, st);
@@ -2770,68 +3271,58 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (p.n_buckets + 1) * 4, st));
     return PDP_OK;
   }
+  int rc2 = PDP_OK;
   if (p.l1_local) {
     if (p.key_format == PDP_KEYS_COMPACT)
-      return launch_local<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
-    if (p.key_format == PDP_KEYS_PACKED)
-      return launch_local<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
-    if (p.key_format == PDP_KEYS_PACKED_WIDE)
-      return launch_local<PDP_KEYS_PACKED_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
-    return launch_local<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+      rc2 = launch_local<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    else if (p.key_format == PDP_KEYS_PACKED)
+      rc2 = launch_local<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    else if (p.key_format == PDP_KEYS_PACKED_WIDE)
+      rc2 = launch_local<PDP_KEYS_PACKED_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    else
+      rc2 = launch_local<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+  } else {
+    rc2 = launch_offsets(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   }
-  unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
-  unsigned* chunk_sums = (unsigned*)(ws + w.chunk_sums);
-  const size_t hist_lds = (size_t)p.n_buckets * 4;
-  PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_part_hist, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)hist_lds));
-  PDP_PROF_BEGIN("k_part_hist", st);
-  unsigned* super_tm = (unsigned*)(ws + w.super_tm);
-  unsigned* super_off = (unsigned*)(ws + w.super_off);
-  hipLaunchKernelGGL(k_part_hist, dim3((unsigned)p.n_tiles), dim3(kPartThreads), hist_lds, st, kp, privacy_id,
-                     counts_tm, super_tm, err);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_super_scan", st);
-  hipLaunchKernelGGL(k_super_scan, dim3((unsigned)p.n_supers), dim3(kBlock), 0, st, kp, super_tm, super_off);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  // rows per bucket (and, with two levels, the level-2 cursors at tile-group starts)
-  const int64_t n_bblk = (p.n_buckets + 63) / 64;
-  const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
-  unsigned* csum = (unsigned*)(ws + w.csum);
-  unsigned* gcur = (unsigned*)(ws + w.gcur);
-  PDP_PROF_BEGIN("k_gscan_sums", st);
-  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum, (unsigned*)nullptr);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_gscan_chunks", st);
-  hipLaunchKernelGGL(k_gscan_chunks, dim3(grid_for(p.n_buckets)), dim3(kBlock), 0, st, csum, n_sc, p.n_buckets,
-                     counts);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  if (p.super_bits > 0) {
-    PDP_PROF_BEGIN("k_gscan_cursors", st);
-    hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
-                       counts_tm, (const unsigned*)nullptr, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
-    PDP_PROF_END(st);
-    PDP_HIP_CHECK(hipGetLastError());
+  if (rc2 != PDP_OK) return rc2;
+  // PDP_MERGE_ATOMIC: the bucket kernel adds into the accumulators, so it
+  // runs in pdp_reduce_partitions; PDP_MERGE_RANGES: all sampling runs here
+  if (p.merge != PDP_MERGE_RANGES) return PDP_OK;
+  if (cfg->flags & PDP_DEBUG_CORRUPT_RECORDS) {
+    rc2 = launch_debug_corrupt(kp, p, st, ws, w);
+    if (rc2 != PDP_OK) return rc2;
   }
-  rc = scan_u32(counts, p.n_buckets, chunk_sums, st);
+  if (p.sieve) {
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.sctl, 0, 16, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cnt, 0, ((uint64_t)p.n_buckets + 1) * 4, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cur, 0, (uint64_t)p.n_buckets * 4, st));
+  }
+  const pdp_partition_accumulators none{};
+  return dispatch<Buckets>(cfg->value_kind, cfg->linf == 0, kp, p, st, privacy_id, partition_key, pk_allowed, value,
+                           none, ws, w);
+}
+
+int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,
+                         pdp_bound_stats* out, void* stream) {
+  if (out == nullptr) return set_error(PDP_E_INVALID, "out is NULL");
+  Plan p;
+  Ws w;
+  const int rc = check_ws(cfg, workspace, workspace_bytes, &p, &w);
   if (rc != PDP_OK) return rc;
-  unsigned* super_base = (unsigned*)(ws + w.super_base);
-  PDP_PROF_BEGIN("k_super_bases", st);
-  hipLaunchKernelGGL(k_super_bases, dim3(grid_for(p.n_supers + 1)), dim3(kBlock), 0, st, kp, counts, super_base);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  if (p.key_format == PDP_KEYS_COMPACT)
-    return launch_scatter<PDP_KEYS_COMPACT>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
-                                            counts, gcur, ws, w, err);
-  if (p.key_format == PDP_KEYS_PACKED)
-    return launch_scatter<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
-                                           counts, gcur, ws, w, err);
-  return launch_scatter<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, super_off, super_base,
-                                       counts, gcur, ws, w, err);
+  *out = pdp_bound_stats{};
+  hipStream_t st = (hipStream_t)stream;
+  const char* ws = (const char*)workspace;
+  PDP_HIP_CHECK(hipMemcpyAsync(&out->error_flags, ws + w.err, 4, hipMemcpyDeviceToHost, st));
+  unsigned rows = 0, ctl[2] = {0, 0};
+  const bool bucketed = !pairs_mode(cfg) && p.algorithm == PDP_ALGO_BUCKETED && cfg->n_rows > 0;
+  if (bucketed) PDP_HIP_CHECK(hipMemcpyAsync(&rows, ws + w.counts + (uint64_t)p.n_buckets * 4, 4, hipMemcpyDeviceToHost, st));
+  if (bucketed && p.sieve) PDP_HIP_CHECK(hipMemcpyAsync(ctl, ws + w.sctl, 8, hipMemcpyDeviceToHost, st));
+  PDP_HIP_CHECK(hipStreamSynchronize(st));
+  out->rows_partitioned = rows;
+  out->unresolved_ids = ctl[0];
+  out->fixup_rows = ctl[1];
+  out->sieve = bucketed ? p.sieve : 0;
+  return PDP_OK;
 }
 
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,
@@ -2860,7 +3351,14 @@ int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* 
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH)
     return dispatch<GlobalReduce>(cfg->value_kind, cfg->linf == 0, kp, st, value, ws, w, *acc);
   if (cfg->n_rows == 0) return PDP_OK;
-  return dispatch<Bucket>(cfg->value_kind, cfg->linf == 0, kp, p, st, ws, w, value, *acc);
+  if (p.merge == PDP_MERGE_RANGES) return launch_merge(kp, p, st, ws, w, *acc);
+  if (cfg->flags & PDP_DEBUG_CORRUPT_RECORDS) {
+    rc = launch_debug_corrupt(kp, p, st, ws, w);
+    if (rc != PDP_OK) return rc;
+  }
+  // PDP_MERGE_ATOMIC (never sieved: the key columns are not needed here)
+  return dispatch<Buckets>(cfg->value_kind, cfg->linf == 0, kp, p, st, (const int64_t*)nullptr,
+                           (const int64_t*)nullptr, (const uint8_t*)nullptr, value, *acc, ws, w);
 }
 
 }  // extern "C"

@@ -68,27 +68,8 @@ __host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, int64_t pid
   return fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^ (uint32_t)seed);
 }
 
-#ifndef PDP_PAIR_HASH_VARIANT
-#define PDP_PAIR_HASH_VARIANT 0
-#endif
-__host__ __device__ __forceinline__ uint32_t umul24(uint32_t a, uint32_t b) {
-  return (a & 0xFFFFFFu) * (b & 0xFFFFFFu);
-}
 __host__ __device__ __forceinline__ uint32_t pair_hash_from(uint32_t hpid, uint64_t seed, int64_t pk) {
-#if PDP_PAIR_HASH_VARIANT == 1
-  return fmix32(hpid ^ (uint32_t)pk ^ (uint32_t)(seed >> 32));
-#elif PDP_PAIR_HASH_VARIANT == 2
-  return hpid ^ (uint32_t)pk;
-#elif PDP_PAIR_HASH_VARIANT == 3
-  uint32_t h = hpid ^ umul24((uint32_t)pk ^ ((uint32_t)pk >> 24), 0x2B2AE3u) ^ (uint32_t)(seed >> 32);
-  h ^= h >> 16;
-  h = umul24(h, 0xEBCA6Bu);
-  h ^= h >> 13;
-  h = umul24(h, 0xB2AE35u);
-  return h ^ (h >> 16);
-#else
   return fmix32(hpid ^ ((uint32_t)pk * 0xC2B2AE3DU + (uint32_t)(seed >> 32)));
-#endif
 }
 
 __host__ __device__ __forceinline__ uint32_t pair_hash(uint64_t seed, int64_t pid, int64_t pk) {
@@ -285,24 +266,6 @@ __device__ __forceinline__ void sketch_insert(unsigned long long* s, int k, uint
 // wave touching different sketches hit different LDS banks).
 __device__ __forceinline__ void sketch_insert_strided(unsigned long long* s, int k, int64_t stride, uint64_t x) {
   for (int j = 0; j < k; ++j) {
-    const uint64_t old = atomicMin(s + j * stride, (unsigned long long)x);
-    if (old == x) return;
-    if (old > x) {
-      if (old == kEmpty) return;
-      x = old;
-    }
-  }
-}
-
-// As sketch_insert_strided, but the atomic chain starts at the first entry
-// not below x in a plain (non-atomic) read of the sketch: entries only ever
-// decrease, so an entry already below x stays below it and atomicMin there
-// would leave it unchanged and carry x on.  Saves the leading atomics (LDS
-// 64-bit atomics with return are the expensive part of an insert).
-__device__ __forceinline__ void sketch_insert_strided_skip(unsigned long long* s, int k, int64_t stride, uint64_t x) {
-  int j = 0;
-  while (j < k && s[j * stride] < x) ++j;
-  for (; j < k; ++j) {
     const uint64_t old = atomicMin(s + j * stride, (unsigned long long)x);
     if (old == x) return;
     if (old > x) {

@@ -42,7 +42,7 @@
 // A cap above PDP_SKETCH_MAX (l0, linf or max_contributions) does not use an
 // atomicMin cascade of that length: the heavy group stores ALL its keys in
 // the pool (its length is the group's count) and one workgroup per heavy
-// group finds the cap-th smallest key by radix select (k_select, 8-bit digits,
+// group finds the cap-th smallest key by radix select (k_radix_select, 8-bit digits,
 // the candidates moved to LDS once they fit) and writes it where a sketch
 // keeps its maximum (pool[offset + cap - 1]), so membership is the same test
 // `key <= pool[offset + cap - 1]` in both modes; Linf's kept rows of heavy
@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) k_sketch_len(const unsigned* __restric
 // candidates sharing the chosen prefix move to LDS once they fit.
 constexpr int kSelBlock = 256;
 constexpr int kSelLds = 4096;
-__global__ void __launch_bounds__(kSelBlock) k_select(const unsigned* __restrict__ list,
+__global__ void __launch_bounds__(kSelBlock) k_radix_select(const unsigned* __restrict__ list,
                                                       const unsigned* __restrict__ n_list,
                                                       const unsigned* __restrict__ off,
                                                       const unsigned* __restrict__ cnt, unsigned cap,
@@ -580,7 +580,7 @@ struct RunBound {
     auto run_select = [&](unsigned* n_list, const unsigned* off, const unsigned* cnt, int cap,
                           unsigned long long* pool) -> int {
       const int64_t ub = t.n / ((int64_t)cap + 1) + 1;
-      PDP_LAUNCH("k_select", st, k_select, dim3((unsigned)ub), dim3(kSelBlock), 0, st, hlist, n_list, off, cnt,
+      PDP_LAUNCH("k_radix_select", st, k_radix_select, dim3((unsigned)ub), dim3(kSelBlock), 0, st, hlist, n_list, off, cnt,
                  (unsigned)cap, pool);
       return PDP_OK;
     };

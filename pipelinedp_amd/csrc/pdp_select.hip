@@ -21,7 +21,12 @@ int check_noise(const pdp_noise_params* np) {
   if (np->kind != PDP_NOISE_LAPLACE && np->kind != PDP_NOISE_GAUSSIAN) return set_error(PDP_E_INVALID, "bad noise kind");
   if (!(np->granularity >= 0.0) || !std::isfinite(np->granularity))
     return set_error(PDP_E_INVALID, "noise granularity must be finite and >= 0");
-  if (np->granularity == 0.0) return PDP_OK;  // no noise
+  if (!(np->scale >= 0.0) || !std::isfinite(np->scale))
+    return set_error(PDP_E_INVALID, "noise scale must be finite and >= 0");
+  if (np->granularity == 0.0) {  // no noise: only for a scale of exactly 0 (fail closed)
+    if (np->scale != 0.0) return set_error(PDP_E_INVALID, "noise granularity 0 with a nonzero scale");
+    return PDP_OK;
+  }
   if (np->kind == PDP_NOISE_LAPLACE && !(np->lambda > 0.0 && std::isfinite(np->lambda)))
     return set_error(PDP_E_INVALID, "Laplace noise needs a finite lambda > 0");
   if (np->kind == PDP_NOISE_GAUSSIAN &&

@@ -182,17 +182,28 @@ NO_NOISE = NoiseParams(kind=0, scale=0.0, granularity=0.0)
 def laplace_noise_params(eps: float, l1_sensitivity: float) -> NoiseParams:
     """Google LaplaceDistribution(epsilon, sensitivity) constants."""
     b = laplace_diversity(eps, l1_sensitivity)
-    if not math.isfinite(b) or b <= 0:
-        return NoiseParams(kind=0, scale=max(b, 0.0) if math.isfinite(b) else b, granularity=0.0)
+    # fail closed: granularity 0 means "no noise", which only a scale of
+    # exactly 0 (zero sensitivity) may produce
+    if not math.isfinite(b) or b < 0:
+        raise ValueError(f"Laplace scale l1/eps = {l1_sensitivity}/{eps} must be finite and >= 0")
+    if b == 0:
+        return NoiseParams(kind=0, scale=0.0, granularity=0.0)
     g = _next_power_of_two(b / _GRANULARITY_PARAM)
-    return NoiseParams(kind=0, scale=b, granularity=g, lam=g * eps / (l1_sensitivity + g))
+    lam = g * eps / (l1_sensitivity + g) if g > 0 else 0.0
+    if not (g > 0 and math.isfinite(g) and lam > 0 and math.isfinite(lam)):
+        raise ValueError(f"Laplace scale {b} has no representable noise grid")
+    return NoiseParams(kind=0, scale=b, granularity=g, lam=lam)
 
 
 def gaussian_noise_params(sigma: float) -> NoiseParams:
     """Google GaussianDistribution(stddev) constants (binomial sampler)."""
+    if not math.isfinite(sigma) or sigma < 0:
+        raise ValueError(f"Gaussian sigma {sigma} must be finite and >= 0")
+    if sigma == 0:
+        return NoiseParams(kind=1, scale=0.0, granularity=0.0)
     g = _next_power_of_two(2.0 * sigma / math.sqrt(_BINOMIAL_BOUND))
     if g == 0.0 or not math.isfinite(g):
-        return NoiseParams(kind=1, scale=sigma, granularity=0.0)
+        raise ValueError(f"Gaussian sigma {sigma} has no representable noise grid")
     sqrt_n = 2.0 * sigma / g
     n = sqrt_n * sqrt_n
     return NoiseParams(kind=1, scale=sigma, granularity=g,

@@ -21,6 +21,7 @@ STRUCTS = {
     "pdp_select_config": N.SelectConfig,
     "pdp_metric_op": N.MetricOp,
     "pdp_histogram_bins": N.HistogramBins,
+    "pdp_bound_stats": N.BoundStats,
 }
 
 
@@ -122,6 +123,36 @@ def test_abi_version_and_plan(lib):
     for merge in (N.MERGE_AUTO, N.MERGE_RANGES):
         assert lib.pdp_bound_plan(ctypes.byref(_cfg(n_partitions=10_000_000, merge=merge)), ctypes.byref(info)) == 0
         assert info.merge == N.MERGE_RANGES and info.n_ranges == 153
+
+
+def test_sieve_plan(lib):
+    """Threshold sieve (Plan.sieve): AUTO picks t = (l0 + 3 sqrt(l0) + 3) / (0.6 rows per id)
+    up to 0.35 (C3: 0.154, C2: 0.325; C4 with 10 rows per id: off), a forced value is
+    clamped to 1/2, < 0 is off, and small (one-level) plans never sieve."""
+    info = N.BoundPlanInfo()
+    c3 = dict(n_rows=1_000_000_000, n_privacy_ids=10_000_000, n_partitions=1_000_000, l0=2, linf=1)
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3)), ctypes.byref(info)) == 0
+    assert abs(info.sieve / 65536 - (2 + 3 * 2 ** 0.5 + 3) / 60) < 1e-4
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg()), ctypes.byref(info)) == 0  # C2
+    assert abs(info.sieve / 65536 - (8 + 3 * 8 ** 0.5 + 3) / 60) < 1e-4
+    c4 = dict(n_rows=125_000_000, n_privacy_ids=12_500_000, n_partitions=10_000_000, l0=4, linf=2)
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c4)), ctypes.byref(info)) == 0
+    assert info.sieve == 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c4, sieve=4096)), ctypes.byref(info)) == 0
+    assert info.sieve == 4096 and info.key_format == N.KEYS_PACKED_WIDE
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=-1)), ctypes.byref(info)) == 0
+    assert info.sieve == 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=1 << 20)), ctypes.byref(info)) == 0
+    assert info.sieve == 1 << 15
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(n_privacy_ids=5000, sieve=4096)), ctypes.byref(info)) == 0
+    assert info.sieve == 0  # one bucket level: no tile-local level 1
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(merge=N.MERGE_ATOMIC, sieve=4096)), ctypes.byref(info)) == 0
+    assert info.sieve == 0  # the fix-up appends pair records: range merge only
+    # the sieve's workspace holds the fix-up state and twice the pair records
+    on, off = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(**c3)), ctypes.byref(on)) == 0
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(**c3, sieve=-1)), ctypes.byref(off)) == 0
+    assert on.value > off.value
 
 
 def test_workspace_bytes(lib):

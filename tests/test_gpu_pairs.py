@@ -160,7 +160,7 @@ def test_pair_table_at_scale_count_identity(device):
 # ------------------------------------------------ bounds above 256 -------
 # (l0, linf, max_contributions, value_kind, flags): l0 or linf > 256 run the
 # pair-table path with L0 over its distinct pairs; a cap > 256 selects by
-# radix select (k_select) instead of a sorted sketch.
+# radix select (k_radix_select) instead of a sorted sketch.
 BIG = {
     "linf_300": (0, 300, 0, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM),
     "linf_1000_int": (0, 1000, 0, O.VALUE_I64, O.ACC_SUM | O.SUM_INT),

@@ -1,0 +1,160 @@
+"""GPU parity of the threshold sieve (pdp_bound.hip, Plan.sieve) against the oracle.
+
+The sieve changes data movement only: k_sieve_l1 keeps the rows whose pair
+hash is below t = sieve / 2^16, the bucket kernel marks privacy ids with
+fewer than l0 candidate pairs, and the fix-up (k_sieve_rescan ->
+k_fix_scatter -> k_bucket_fix) recomputes those ids from all of their rows.
+Kept pairs and rows must therefore equal the oracle's exactly (the oracle has
+no sieve: oracle/columnar.py bound_and_reduce follows
+contribution_bounders.py:72-111 with the kernels' priorities), at every t:
+t ~ 0 (nearly every id unresolved: the fix-up does all the work, the Bloom
+filter saturates), intermediate t, and t = 1/2.  Integer outputs bit-exact;
+fp64 sums within 1e-9 of the sum of |terms| (FLOAT_RTOL).
+"""
+import numpy as np
+import pytest
+
+from oracle import columnar as O
+from tests.test_gpu_kernels import _abs_scale, _compare, _gen, _rand_shift
+
+pytestmark = pytest.mark.gpu
+
+SIEVES = [1, 64, 4096, 16384, 32768]  # t = sieve / 2^16
+
+# (l0, linf, value_kind, flags, lo, hi, per-partition bounds, U): U large
+# enough for two partition levels (the sieve's precondition)
+CASES = [
+    (2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 200_000),
+    (4, 2, O.VALUE_I64, O.ACC_SUM | O.SUM_INT, 0, 7, None, 90_000),
+    (16, 4, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM | O.ACC_NSUM2, 1.0, 6.0, None, 20_000),
+    (3, 0, O.VALUE_F64, O.SUM_PER_PARTITION, 0, 0, (-3.0, 20.0), 120_000),
+    (1, 1, O.VALUE_NONE, 0, 0, 0, None, 300_000),
+]
+
+
+def _spec(case):
+    from pipelinedp_amd import executor as X
+    l0, linf, vk, flags, lo, hi, pp, _ = case
+    mid = lo + (hi - lo) / 2 if vk != O.VALUE_NONE else 0.0
+    return X.BoundingSpec(l0=l0, linf=linf, value_kind=vk, flags=flags, min_value=lo, max_value=hi,
+                          middle=mid, min_sum=pp[0] if pp else 0.0, max_sum=pp[1] if pp else 0.0)
+
+
+def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format=0, row_offset=0):
+    import torch
+    from pipelinedp_amd import executor as X
+    tv = None if val is None else torch.as_tensor(val).to(device)
+    ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
+    acc = X.bound_and_reduce(torch.as_tensor(pid).to(device), torch.as_tensor(pk).to(device), tv,
+                             n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, allowed=ta,
+                             key_format=key_format, sieve=sieve, row_offset=row_offset)
+    torch.cuda.synchronize()
+    return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+
+
+def _want(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+    return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0, linf=spec.linf,
+                              value_kind=spec.value_kind, flags=spec.flags, min_value=spec.min_value,
+                              max_value=spec.max_value, middle=spec.middle, min_sum=spec.min_sum,
+                              max_sum=spec.max_sum, seed=seed, allowed=allowed, row_offset=row_offset,
+                              rand_shift=_rand_shift(len(pid), U, P, spec))
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
+def test_sieve_matches_oracle_at_every_threshold(device, case):
+    from pipelinedp_amd import executor as X
+    spec = _spec(case)
+    U, P = case[7], 3001
+    n = 2_000_000 + 12_345  # a ragged last tile
+    pid, pk, val = _gen(77 + spec.l0, n, U, P, spec.value_kind, skew=True)
+    seed = 0xA5A5_0000_1111 + spec.l0
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    for sieve in SIEVES:
+        plan = X.bound_plan(n, U, P, spec, sieve=sieve)
+        assert plan.sieve == sieve, (sieve, plan.sieve)
+        got = _run(device, pid, pk, val, U, P, spec, seed, sieve)
+        _compare(got, want, scale)
+    off = _run(device, pid, pk, val, U, P, spec, seed, -1)
+    assert X.bound_plan(n, U, P, spec, sieve=-1).sieve == 0
+    _compare(off, want, scale)
+
+
+@pytest.mark.parametrize("key_format", [2, 3])  # COMPACT, PACKED
+def test_sieve_key_formats_public_filter_and_offset(device, key_format):
+    """Dead (non-public) rows are dropped by the sieve and marked dead in the
+    fix-up; row priorities follow row_offset in both."""
+    spec = _spec(CASES[0])
+    U, P, n = 200_000, 1000, 1_500_000
+    pid, pk, val = _gen(5, n, U, P, spec.value_kind, skew=True)
+    allowed = np.random.default_rng(3).random(P) < 0.7
+    seed, off = 991, 123_456_789
+    want = _want(pid, pk, val, U, P, spec, seed, allowed=allowed, row_offset=off)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    for sieve in (64, 8192):
+        got = _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=allowed, key_format=key_format,
+                   row_offset=off)
+        _compare(got, want, scale)
+        assert (got["privacy_id_count"][~allowed] == 0).all()
+
+
+def test_sieve_packed_wide(device):
+    """P = 1e7 (bucket + partition bits > 31): PACKED_WIDE records, 8-byte
+    fix-up keys, rand_shift > 32 (the threshold is a multiple of the masked
+    hash grain)."""
+    from pipelinedp_amd import _native as N
+    from pipelinedp_amd import executor as X
+    spec = _spec((4, 2, O.VALUE_F64, O.ACC_NSUM, 0.0, 20.0, None, 0))
+    U, P, n = 400_000, 10_000_000, 2_000_000
+    rng = np.random.default_rng(8)
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.1, n) - 1, P - 1).astype(np.int64)
+    val = np.clip(rng.lognormal(1.0, 1.0, n), 0, 20)
+    plan = X.bound_plan(n, U, P, spec, sieve=4096)
+    assert plan.key_format == N.KEYS_PACKED_WIDE and plan.rand_shift > 32 and plan.sieve == 4096
+    seed = 4242
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    for sieve in (64, 4096, 32768):
+        _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve), want, scale)
+
+
+def test_sieve_c3_shape_slice(device):
+    """A C3-shaped slice (uniform ids, ~100 rows each, Zipf(1.1) keys folded
+    into 1e6, L0 = 2, Linf = 1, COUNT+SUM+MEAN) with the AUTO threshold."""
+    from pipelinedp_amd import executor as X
+    spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    U, P = 150_000, 1_000_000
+    n = 100 * U
+    rng = np.random.default_rng(2)
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.1, n) - 1, P - 1).astype(np.int64)
+    val = rng.random(n) * 10.0
+    plan = X.bound_plan(n, U, P, spec)
+    assert 0 < plan.sieve < 16384  # auto: t ~ 0.15
+    seed = 77
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 0), want, scale)
+
+
+@pytest.mark.parametrize("sieve", [-1, 4096])
+def test_malformed_records_are_flagged_not_read(device, sieve):
+    """PDP_DEBUG_CORRUPT_RECORDS overwrites bucket 0's level-2 records with
+    the all-ones partition (>= P) and bucket 1's with an out-of-range row: the
+    bucket kernel sets the error word (bound_and_reduce raises) instead of
+    dereferencing them (the r02 illegal-address fault)."""
+    import torch
+    from pipelinedp_amd import _native as N
+    from pipelinedp_amd import executor as X
+    base = _spec(CASES[0])
+    spec = X.BoundingSpec(l0=base.l0, linf=base.linf, value_kind=base.value_kind,
+                          flags=base.flags | N.DEBUG_CORRUPT_RECORDS, min_value=base.min_value,
+                          max_value=base.max_value, middle=base.middle)
+    U, P, n = 200_000, 3001, 1_000_000
+    pid, pk, val = _gen(1, n, U, P, spec.value_kind)
+    with pytest.raises(ValueError, match="outside the dense key range"):
+        _run(device, pid, pk, val, U, P, spec, 5, sieve)
+    torch.cuda.synchronize()  # the device is still healthy
+    ok = _run(device, pid, pk, val, U, P, base, 5, sieve)
+    assert ok["privacy_id_count"].sum() > 0

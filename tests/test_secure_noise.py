@@ -51,6 +51,34 @@ def test_zero_scale_is_no_noise():
     np.testing.assert_array_equal(O.secure_add_noise(pydp.laplace_params(1.0, 0.0), x, 1, np.arange(3), 5), x)
 
 
+@pytest.mark.parametrize("make", [lambda: dpc.laplace_noise_params(1.0, math.inf),
+                                  lambda: dpc.laplace_noise_params(5e-324, 1.0),
+                                  lambda: dpc.laplace_noise_params(1.0, math.nan),
+                                  lambda: dpc.gaussian_noise_params(math.inf),
+                                  lambda: dpc.gaussian_noise_params(math.nan),
+                                  lambda: dpc.gaussian_noise_params(-1.0)])
+def test_non_finite_scale_fails_closed(make):
+    """A scale that is not finite must raise, never become granularity 0
+    (which the kernels read as "no noise" and release raw values)."""
+    with pytest.raises(ValueError):
+        make()
+
+
+def test_abi_rejects_zero_granularity_with_scale():
+    """check_noise (pdp_select.hip) refuses granularity 0 unless the scale is
+    exactly 0; runs before any device work, so it needs no GPU."""
+    import ctypes
+    from pipelinedp_amd import _native as N
+    lib = N.lib()
+    bad = dpc.NoiseParams(kind=0, scale=2.0, granularity=0.0).to_c()
+    rc = lib.pdp_add_noise(None, N.VALUE_F64, 0, ctypes.byref(bad), 1, 0, None, None)
+    assert rc == -1 and b"granularity 0" in lib.pdp_last_error()
+    inf = dpc.NoiseParams(kind=1, scale=math.inf, granularity=0.0).to_c()
+    assert lib.pdp_add_noise(None, N.VALUE_F64, 0, ctypes.byref(inf), 1, 0, None, None) == -1
+    ok = dpc.NoiseParams(kind=0, scale=0.0, granularity=0.0).to_c()
+    assert lib.pdp_add_noise(None, N.VALUE_F64, 0, ctypes.byref(ok), 1, 0, None, None) == 0
+
+
 def test_round_to_multiple_ties_toward_zero():
     g = 0.5
     xs = np.array([0.25, -0.25, 0.26, -0.26, 1.0, 0.74, 0.75, -0.75])
