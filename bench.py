@@ -172,7 +172,9 @@ def cpu_baselines(workload, sample_rows):
 
 
 def gen_c3(n, U, P, rank, world, device, seed):
-    """This rank's shard: privacy ids r + k*world (k < U), Zipf(1.1) pk."""
+    """This rank's shard: its U privacy ids as local codes k in [0, U) --
+    the dataset-wide id of code k on rank r is r * U + k (privacy_id_identity),
+    so ranks hold disjoint ids -- and Zipf(1.1) pk."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed + rank)
@@ -192,6 +194,7 @@ def gen_c3(n, U, P, rank, world, device, seed):
 
 
 def gen_c2(n, U, P, rank, device, seed):
+    """Local privacy-id codes as in gen_c3 (dataset-wide id r * U + k)."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed + rank)
@@ -245,6 +248,23 @@ def gen_c5(n, U, P, rank, device, seed):
     return pid, pk, value
 
 
+def verify_sharding(ids, world, base=0):
+    """The library's default privacy_id_sharding="verify" on this rank's
+    dataset-wide ids base + ids (ColumnarBackend._shard_privacy_ids: the distinct ids,
+    one all-to-all to their owner ranks, ValueError on an id held by two
+    ranks), run once before the timed region; returns its wall time in ms
+    (None at N = 1, where there is nothing to verify)."""
+    import torch
+    from pipelinedp_amd import parallel
+    if world == 1:
+        return None
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    parallel.check_privacy_ids_disjoint(torch.unique(ids) + base)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
 def run_api_workload(args, workload, world, rank, device):
     """c4 / c5: one step = DPEngine.aggregate (the public API) over this
     rank's device-resident rows on ColumnarBackend, compute_budgets(), and
@@ -261,6 +281,9 @@ def run_api_workload(args, workload, world, rank, device):
     pid, pk, value = gen(n, U, P, rank, device, 4000 if workload == "c4" else 5000)
     pid += rank * U  # privacy ids of different ranks are different people
     torch.cuda.synchronize()
+    # the default privacy_id_sharding="verify", once, before timing (the
+    # steps below pass "trusted": the check does not change between steps)
+    verify_ms = verify_sharding(pid, world)
     table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U * world, n_partitions=P)
     if workload == "c4":
         params = pdp.AggregateParams(metrics=[pdp.Metrics.VARIANCE, pdp.Metrics.PRIVACY_ID_COUNT],
@@ -336,6 +359,7 @@ def run_api_workload(args, workload, world, rank, device):
             "lds_bytes": info.lds_bytes,
             "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(info.key_format, info.key_format)},
         "partitions_kept": kept,
+        "privacy_id_verify_ms": verify_ms,
     }
 
 
@@ -425,6 +449,10 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         bounding, selection, ops = build_plan(C2["l0"], C2["linf"])
         pid, pk, value = gen_c2(n, U, P, rank, device, 1000)
     torch.cuda.synchronize()
+    # rank r holds the dataset-wide ids r * U + [0, U): checked once with the
+    # library's default verify (it raises on an id held by two ranks); the
+    # kernels take the local codes (ids relative to the rank's base)
+    verify_ms = verify_sharding(pid, world, rank * U)
 
     P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
@@ -539,7 +567,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                            plan.key_format, plan.key_format),
                        "sieve": plan.sieve / 65536.0, "stats": stats},
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
-        "api": api,
+        "api": api, "privacy_id_verify_ms": verify_ms,
     }
 
 
@@ -608,6 +636,7 @@ def main():
         "kernels": r["kernels"],
         "bound_plan": r["bound_plan"],
         "partitions_kept": r["partitions_kept"],
+        "privacy_id_verify_ms": r.get("privacy_id_verify_ms"),
         "api": r["api"],
         "cpu_baseline": cpu[0] if cpu else None,
         "cpu_baseline_strong": cpu[1] if cpu else None,

@@ -193,10 +193,13 @@ _lock = threading.Lock()
 _lib = None
 
 
-def _declare(lib):
+def signatures():
+    """{symbol: (restype, argtypes)} of every exported function
+    (include/pipelinedp_amd.h); tests/test_integration_doc.py checks
+    INTEGRATION.md's ctypes stubs against it."""
     P = ctypes.POINTER
     vp, i64, u64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int32
-    sig = {
+    return {
         "pdp_abi_version": (ctypes.c_int, []),
         "pdp_last_error": (ctypes.c_char_p, []),
         "pdp_bound_workspace_bytes": (ctypes.c_int, [P(BoundConfig), P(u64)]),
@@ -231,7 +234,10 @@ def _declare(lib):
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),
     }
-    for name, (res, args) in sig.items():
+
+
+def _declare(lib):
+    for name, (res, args) in signatures().items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
