@@ -87,6 +87,10 @@ def parse():
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
     ap.add_argument("--sieve", type=int, default=0,
                     help="threshold sieve t * 2^16 (0 auto, -1 off; pdp_bound_config.sieve)")
+    ap.add_argument("--strategy", choices=("truncated_geometric", "gaussian", "laplace"),
+                    default="truncated_geometric",
+                    help="c4 / c5: AggregateParams.partition_selection_strategy (SURVEY §8(d) C4 names "
+                         "TRUNCATED_GEOMETRIC and GAUSSIAN_THRESHOLDING)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the "
                          "n_gpus it sees (tests/test_bench_launcher.py)")
@@ -285,13 +289,18 @@ def run_api_workload(args, workload, world, rank, device):
     # steps below pass "trusted": the check does not change between steps)
     verify_ms = verify_sharding(pid, world)
     table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U * world, n_partitions=P)
+    strategy = {"truncated_geometric": pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC,
+                "gaussian": pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING,
+                "laplace": pdp.PartitionSelectionStrategy.LAPLACE_THRESHOLDING}[args.strategy]
     if workload == "c4":
         params = pdp.AggregateParams(metrics=[pdp.Metrics.VARIANCE, pdp.Metrics.PRIVACY_ID_COUNT],
+                                     partition_selection_strategy=strategy,
                                      noise_kind=pdp.NoiseKind.GAUSSIAN, max_partitions_contributed=w["l0"],
                                      max_contributions_per_partition=w["linf"], min_value=MIN_VALUE,
                                      max_value=MAX_VALUE)
     else:
         params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN],
+                                     partition_selection_strategy=strategy,
                                      noise_kind=pdp.NoiseKind.LAPLACE, max_partitions_contributed=w["l0"],
                                      max_contributions_per_partition=w["linf"], min_value=MIN_VALUE,
                                      max_value=C5["max_value"])
@@ -338,9 +347,10 @@ def run_api_workload(args, workload, world, rank, device):
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
     path_bytes = 24.0 * n
     path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
-    desc = ("C4: DPEngine.aggregate VARIANCE+PRIVACY_ID_COUNT, Gaussian, private partitions (truncated "
-            "geometric), L0=4, Linf=2, uniform keys" if workload == "c4" else
-            "C5: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions, L0=4, Linf=2, rows per "
+    strat = args.strategy.replace("_", " ") + ("" if args.strategy == "truncated_geometric" else " thresholding")
+    desc = (f"C4: DPEngine.aggregate VARIANCE+PRIVACY_ID_COUNT, Gaussian, private partitions ({strat}), "
+            f"L0=4, Linf=2, uniform keys" if workload == "c4" else
+            f"C5: DPEngine.aggregate COUNT+SUM+MEAN, Laplace, private partitions ({strat}), L0=4, Linf=2, rows per "
             "privacy id Pareto(1.5) capped at 1e6, Zipf(1.1) partition keys, lognormal values in [0, 20]")
     return {
         "value": n * world * args.steps / elapsed,

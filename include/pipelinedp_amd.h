@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 8
+#define PDP_ABI_VERSION 9
 
 /* error codes */
 #define PDP_OK 0
@@ -406,7 +406,14 @@ int pdp_dataset_histograms_finish(int32_t value_kind, int64_t n_rows, int64_t n_
  * pdp_dataset_histograms_pairs / _finish for rows of one privacy id on one
  * rank: between _rows and _finish the caller sums pk_rows and pk_count
  * (uint64[n_partitions]) and psum (double[n_partitions]) over ranks and takes
- * min / max of the two minmax words, at the offsets _exchange_offsets gives. */
+ * min / max of the two minmax words, at the offsets _exchange_offsets gives.
+ * The L0 / L1 weight sums must be global before they are rounded: between
+ * _rows and _finish the caller sums the dense weights (double[2][1000] at
+ * _weight_offsets' wsmall: values below 1000) over ranks and keeps them on one
+ * rank (zeros elsewhere), takes every live entry of the weight table
+ * ({uint64 key, double weight}[wtab_slots] at wtab, key 0 = empty) out of it
+ * (zeroing the table), sums the entries per key over ranks, and after _finish
+ * adds each key's global sum once with pdp_dataset_histograms_weight_bins. */
 int pdp_dataset_histograms_preaggregated_workspace_bytes(int64_t n_rows, int64_t n_partitions, uint64_t* bytes);
 int pdp_dataset_histograms_preaggregated(const int64_t* partition, const int64_t* count, const double* sum,
                                          const int64_t* n_partitions_of_pid, const int64_t* n_contributions_of_pid,
@@ -419,9 +426,17 @@ int pdp_dataset_histograms_preaggregated_rows(const int64_t* partition, const in
                                               uint64_t workspace_bytes, void* stream);
 int pdp_dataset_histograms_preaggregated_exchange_offsets(int64_t n_rows, int64_t n_partitions, uint64_t* pk_rows,
                                                           uint64_t* pk_count, uint64_t* psum, uint64_t* minmax);
+int pdp_dataset_histograms_preaggregated_weight_offsets(int64_t n_rows, int64_t n_partitions, uint64_t* wsmall,
+                                                        uint64_t* wtab, uint64_t* wtab_slots);
 int pdp_dataset_histograms_preaggregated_finish(const double* sum, int64_t n_rows, int64_t n_partitions,
                                                 int32_t partition_histograms, const pdp_histogram_bins* out,
                                                 void* workspace, uint64_t workspace_bytes, void* stream);
+/* Adds n weight-table entries (keys as in the table above: value * 2 +
+ * histogram + 1, histogram 0 = L0, 1 = L1; key 0 skipped) to the integer bins:
+ * int(round(weight)) elements of the value, half to even; the bin's max is the
+ * value even at count 0.  Device arrays; asynchronous on `stream`. */
+int pdp_dataset_histograms_weight_bins(const uint64_t* keys, const double* weights, int64_t n,
+                                       const pdp_histogram_bins* out, void* stream);
 
 /* Kernel profiler: when enabled, every kernel launch of this library is
  * bracketed by HIP events recorded on its launch stream.  enable(1) clears

@@ -422,6 +422,28 @@ def _is_int(x) -> bool:
 
 
 # -------------------------------------------------------------- backend --
+def shard_rows_by_privacy_id(mode, pid_t, pk_t, val_t, pid_enc):
+    """Multi-rank: verify that no privacy id spans ranks ("verify"), or
+    shuffle the rows to the privacy ids' owner ranks ("shuffle"); "trusted"
+    returns the rows unchanged (ColumnarBackend privacy_id_sharding).
+    Identities: integer ids themselves, else a fixed-key hash of the key
+    (parallel.key_identities).  Returns (pid_t, pk_t, val_t, pid_enc)."""
+    import torch
+    if mode == "trusted" or parallel.world_info()[0] == 1:
+        return pid_t, pk_t, val_t, pid_enc
+    table = None if pid_enc.decode is None else \
+        torch.as_tensor(parallel.key_identities(pid_enc.decode)).to(pid_t.device)
+    if mode == "verify":
+        parallel.check_privacy_ids_disjoint(torch.unique(pid_t) if table is None else table)
+        return pid_t, pk_t, val_t, pid_enc
+    ident = pid_t if table is None else table[pid_t]
+    ident, (pk_t, val_t) = parallel.shuffle_by_privacy_id(ident, [pk_t, val_t])
+    uniq, inv = torch.unique(ident, return_inverse=True)  # dense local codes of the received ids
+    pid_t = inv.to(torch.int64).contiguous()
+    return pid_t, pk_t.contiguous(), None if val_t is None else val_t.contiguous(), \
+        C.EncodedKeys(pid_t, max(int(uniq.numel()), 1), None)
+
+
 class ColumnarBackend(pipeline_backend.PipelineBackend):
     """Columnar, lazily executed PipelineBackend running on one MI355X GPU
     (or one GPU per rank with torch.distributed; see parallel.py).
@@ -613,22 +635,7 @@ class AggregateRun:
         return pid_t, pk_t, val_t, value_kind, pid_enc, pk_enc, public_codes
 
     def _shard_privacy_ids(self, pid_t, pk_t, val_t, pid_enc):
-        """Multi-rank: verify that no privacy id spans ranks, or shuffle the
-        rows to the privacy ids' owner ranks (ColumnarBackend
-        privacy_id_sharding).  Identities: integer ids themselves, else a
-        fixed-key hash of the key (parallel.key_identities)."""
-        import torch
-        table = None if pid_enc.decode is None else \
-            torch.as_tensor(parallel.key_identities(pid_enc.decode)).to(pid_t.device)
-        if self.backend._pid_sharding == "verify":
-            parallel.check_privacy_ids_disjoint(torch.unique(pid_t) if table is None else table)
-            return pid_t, pk_t, val_t, pid_enc
-        ident = pid_t if table is None else table[pid_t]
-        ident, (pk_t, val_t) = parallel.shuffle_by_privacy_id(ident, [pk_t, val_t])
-        uniq, inv = torch.unique(ident, return_inverse=True)  # dense local codes of the received ids
-        pid_t = inv.to(torch.int64).contiguous()
-        return pid_t, pk_t.contiguous(), None if val_t is None else val_t.contiguous(), \
-            C.EncodedKeys(pid_t, max(int(uniq.numel()), 1), None)
+        return shard_rows_by_privacy_id(self.backend._pid_sharding, pid_t, pk_t, val_t, pid_enc)
 
     def _bounding_spec(self, value_kind):
         from pipelinedp_amd.executor import BoundingSpec

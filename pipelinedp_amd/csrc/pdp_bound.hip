@@ -121,9 +121,12 @@ constexpr int kSieveMaxT16 = 1 << 15;                          // t <= 1/2
 constexpr int kBloomWords = 16384;                             // k_sieve_rescan: 64 KiB LDS Bloom filter
 constexpr int kRescanThreads = 512;                            // two workgroups per CU
 constexpr int kSieveL2Groups = 4;  // tile groups per level-2 workgroup with the sieve
-// every flush but a tile's last holds > kSieveCap - kSieveChunk records, so a
-// tile flushes at most kStagesPerTile times (its blocks fit the level-1 slots)
-static_assert(kTileRows / (kSieveCap - kSieveChunk + 1) + 1 <= kStagesPerTile, "sieve flushes per tile");
+// a tile flushes at most once per chunk, and every flush but its last holds
+// > kSieveCap - kSieveChunk records, so its blocks fit the kStagesPerTile
+// level-1 slots
+static_assert(kTileRows / kSieveChunk <= kStagesPerTile ||
+                  kTileRows / (kSieveCap - kSieveChunk + 1) + 1 <= kStagesPerTile,
+              "sieve flushes per tile");
 static_assert(kSieveCap <= 65535, "u16 run offsets");
 size_t sieve_stage_bytes(int key_format);  // LDS of the sieve's level-1 stage (after StageLds)
 inline bool sieve_hist_u16(int key_format, int64_t n_buckets) {
@@ -1420,96 +1423,132 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
     ++slot;
     __syncthreads();
   };
-  auto load = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
-#pragma unroll
-    for (int q = 0; q < Q; q += 2) {
-      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
-      if (kp.keys_vec && i + 1 < t1) {
-        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
-        const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
-        u[q] = a.x;
-        u[q + 1] = a.y;
-        k[q] = c.x;
-        k[q + 1] = c.y;
-      } else {
-        u[q] = i < t1 ? pid[i] : 0;
-        k[q] = i < t1 ? pk[i] : 0;
-        u[q + 1] = i + 1 < t1 ? pid[i + 1] : 0;
-        k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
-      }
-    }
-  };
   // U16: the tile's counts in two halves (counts_tm, counts_tm2)
   const bool split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
-  // one chunk: filter, then (its registers free) the loads of the chunk two
-  // ahead go out, then append / flush -- two chunks of loads in flight
-  auto body = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
-    const bool more = c0 + kSieveChunk < t1;  // block-uniform
-    bool cand[Q];
-    int d[Q];
-    K x[Q];
+  bool bad = false;  // a key outside [0, U) x [0, P): flagged once per thread at the end
+  // FULL (a whole tile of 16-byte aligned columns): every load is an
+  // unconditional 16-byte load and the prefetch address is clamped into the
+  // tile, so no branch surrounds a load and the compiler keeps two chunks of
+  // loads in flight (a guarded load per row made it wait for every load);
+  // otherwise guarded 8-byte loads (the last tile, unaligned columns)
+  auto run = [&](auto full_tag) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    auto load = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
-      cand[q] = false;
-      d[q] = 0;
-      x[q] = 0;
-      if (i >= t1) continue;
-      if (u[q] < 0 || u[q] >= kp.U || k[q] < 0 || k[q] >= kp.P) {  // invalid key: flagged, dropped
-        atomicOr(err, 1u);
-        continue;
+      for (int q = 0; q < Q; q += 2) {
+        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+        if constexpr (FULL) {
+          const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
+          const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
+          u[q] = a.x;
+          u[q + 1] = a.y;
+          k[q] = c.x;
+          k[q + 1] = c.y;
+        } else {
+          u[q] = i < t1 ? pid[i] : 0;
+          k[q] = i < t1 ? pk[i] : 0;
+          u[q + 1] = i + 1 < t1 ? pid[i + 1] : 0;
+          k[q + 1] = i + 1 < t1 ? pk[i + 1] : 0;
+        }
       }
-      if (allowed != nullptr && allowed[k[q]] == 0) continue;  // non-public partition
-      if (pair_hash(kp.seed, u[q], k[q]) >= t32) continue;
-      cand[q] = true;
-      const int64_t bkt = u[q] >> kp.bucket_bits;
-      if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
-      else atomicAdd(bh + bkt, 1u);
-      d[q] = (int)(u[q] >> mid_bits);
-      if constexpr (FMT == PDP_KEYS_COMPACT) {
-        x[q] = (K)compact_key(kp, u[q], k[q], false);
-      } else {  // PACKED / PACKED_WIDE
-        x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
-      }
-    }
-    if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
-    // append this wave's candidates at one reserved range of the stage
-    unsigned long long m[Q];
-    unsigned nw = 0;
+    };
+    // one chunk: filter, then (its registers free) the loads of the chunk two
+    // ahead go out, then append / flush -- two chunks of loads in flight
+    auto body = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
+      const bool more = c0 + kSieveChunk < t1;  // block-uniform
+      bool cand[Q];
+      int d[Q];
+      K x[Q];
+      uint8_t pub[Q];  // public partitions: the rows' mask bytes, gathered together (one wait)
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      m[q] = __ballot(cand[q]);
-      nw += (unsigned)__popcll(m[q]);
-    }
-    unsigned base = 0;
-    if (lane == 0 && nw) base = atomicAdd(&fill, nw);
-    base = __shfl(base, 0, 64);
+      for (int q = 0; q < Q; ++q) pub[q] = 1;
+      if (allowed != nullptr) {  // block-uniform
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      if (cand[q]) {
-        const unsigned pos = base + (unsigned)__popcll(m[q] & below);
-        s.keys[pos] = x[q];
-        s.dest[pos] = (typename SL::D)d[q];
-        if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
+        for (int q = 0; q < Q; ++q) pub[q] = allowed[(uint64_t)k[q] < (uint64_t)kp.P ? k[q] : 0];
       }
-      base += (unsigned)__popcll(m[q]);
-    }
-    __syncthreads();
-    const unsigned f = fill;
-    if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
-    else __syncthreads();  // every thread has read `fill` before the next chunk's appends
-    if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
-      flush_counts(counts_tm + t * kp.n_buckets);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+        const bool valid = FULL || i < t1;
+        const bool in_range = (uint64_t)u[q] < (uint64_t)kp.U && (uint64_t)k[q] < (uint64_t)kp.P;
+        bad |= valid && !in_range;
+        // every term evaluated (no short circuit: no branch, no per-row load wait);
+        // a non-public partition's rows are dropped
+        bool c = valid & in_range & (pub[q] != 0);
+        c = c & (pair_hash(kp.seed, u[q], k[q]) < t32);
+        cand[q] = c;
+        d[q] = (int)(u[q] >> mid_bits);
+        if constexpr (FMT == PDP_KEYS_COMPACT) {
+          x[q] = (K)compact_key(kp, u[q], k[q], false);
+        } else {  // PACKED / PACKED_WIDE
+          x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
+        }
+        if (c) {
+          const int64_t bkt = u[q] >> kp.bucket_bits;
+          if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+          else atomicAdd(bh + bkt, 1u);
+        }
+      }
+      if constexpr (FULL) {
+        const int64_t cp = c0 + 2 * kSieveChunk < t1 ? c0 + 2 * kSieveChunk : t1 - kSieveChunk;
+        load(cp, u, k);
+      } else {
+        if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
+      }
+      // append this wave's candidates at one reserved range of the stage
+      unsigned long long m[Q];
+      unsigned nw = 0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        m[q] = __ballot(cand[q]);
+        nw += (unsigned)__popcll(m[q]);
+      }
+      unsigned base = 0;
+      if (lane == 0 && nw) base = atomicAdd(&fill, nw);
+      base = __shfl(base, 0, 64);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (cand[q]) {
+          const unsigned pos = base + (unsigned)__popcll(m[q] & below);
+          s.keys[pos] = x[q];
+          s.dest[pos] = (typename SL::D)d[q];
+          if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
+        }
+        base += (unsigned)__popcll(m[q]);
+      }
       __syncthreads();
+      const unsigned f = fill;
+      if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
+      else __syncthreads();  // every thread has read `fill` before the next chunk's appends
+      if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
+        flush_counts(counts_tm + t * kp.n_buckets);
+        __syncthreads();
+      }
+    };
+    int64_t ua[Q], ka[Q], ub[Q], kb[Q];
+    if constexpr (FULL) {
+      load(t0, ua, ka);
+      load(t0 + kSieveChunk, ub, kb);
+    } else {
+      if (t0 < t1) load(t0, ua, ka);
+      if (t0 + kSieveChunk < t1) load(t0 + kSieveChunk, ub, kb);
+    }
+    if constexpr (FULL) {  // a fixed trip count: the same loads are pending on every path
+      static_assert((kTileRows / kSieveChunk) % 2 == 0, "chunk pairs per tile");
+      for (int j = 0; j < (int)(kTileRows / kSieveChunk); j += 2) {
+        body(t0 + (int64_t)j * kSieveChunk, ua, ka);
+        body(t0 + (int64_t)(j + 1) * kSieveChunk, ub, kb);
+      }
+    } else {
+      for (int64_t c0 = t0; c0 < t1; c0 += 2 * kSieveChunk) {
+        body(c0, ua, ka);
+        if (c0 + kSieveChunk < t1) body(c0 + kSieveChunk, ub, kb);  // block-uniform
+      }
     }
   };
-  int64_t ua[Q], ka[Q], ub[Q], kb[Q];
-  if (t0 < t1) load(t0, ua, ka);
-  if (t0 + kSieveChunk < t1) load(t0 + kSieveChunk, ub, kb);
-  for (int64_t c0 = t0; c0 < t1; c0 += 2 * kSieveChunk) {
-    body(c0, ua, ka);
-    if (c0 + kSieveChunk < t1) body(c0 + kSieveChunk, ub, kb);  // block-uniform
-  }
+  if (kp.keys_vec && t1 - t0 == kTileRows) run(std::true_type{});
+  else run(std::false_type{});
+  if (bad) atomicOr(err, 1u);
   // the tile's unused slots: empty runs
   for (int j = slot; j < kStagesPerTile; ++j) {
     const int64_t sl = t * kStagesPerTile + j;
@@ -2099,6 +2138,34 @@ __device__ __forceinline__ unsigned bloom_bits(uint32_t h) {
 // its own) and, on a hit, against the exact bitmap.  Rows of unresolved ids
 // are appended to fix_rec as (privacy id << 32 | row) -- one returning atomic
 // per wave and batch -- and counted per bucket.  No unresolved id: no work.
+// VEC (16-byte aligned column): the full block iterations load their rows
+// with unconditional 16-byte loads, the next iteration's in flight while this
+// one is tested (branch-free, so the loads are not serialised by waits); the
+// remaining rows go through a guarded scalar loop.
+__device__ __forceinline__ void rescan_emit(const KP& kp, int64_t u, int64_t i, const unsigned* bloom,
+                                            const unsigned* __restrict__ unres_bits, unsigned* __restrict__ sctl,
+                                            unsigned* __restrict__ fix_cnt, unsigned long long* __restrict__ fix_rec) {
+  bool hit = false;
+  if ((uint64_t)u < (uint64_t)kp.U) {  // invalid ids were flagged by level 1
+    const uint32_t h = bloom_hash((uint32_t)u);
+    const unsigned bits = bloom_bits(h);
+    if ((bloom[h & (kBloomWords - 1)] & bits) == bits) hit = (unres_bits[u >> 5] >> (u & 31)) & 1u;
+  }
+  const unsigned long long m = __ballot(hit);
+  if (m == 0) return;  // wave-uniform
+  const unsigned long long active = __ballot(true);
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)active) - 1;
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(sctl + 1, (unsigned)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (hit) {
+    fix_rec[base + __popcll(m & ((1ULL << lane) - 1))] = ((unsigned long long)u << 32) | (unsigned long long)(uint32_t)i;
+    atomicAdd(fix_cnt + (u >> kp.bucket_bits), 1u);
+  }
+}
+
+template <bool VEC>
 __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const int64_t* __restrict__ pid,
                                                                  const unsigned* __restrict__ unres_bits,
                                                                  const unsigned* __restrict__ unres_list,
@@ -2115,56 +2182,33 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
     atomicOr(bloom + (h & (kBloomWords - 1)), bloom_bits(h));
   }
   __syncthreads();
-  constexpr int KU = 8;  // 16-byte loads (two rows) in flight per lane
-  const int lane = threadIdx.x & 63;
-  const unsigned long long below = (1ULL << lane) - 1;
-  const int64_t n_pairs = (kp.n + 1) / 2;
-  const int64_t step = (int64_t)gridDim.x * blockDim.x * KU;
-  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x * KU; g0 < n_pairs; g0 += step) {  // block-uniform trips
-    int64_t u[2 * KU];
+  constexpr int KU = 8;  // 16-byte loads (two rows) per lane and iteration
+  const int64_t per_iter = (int64_t)blockDim.x * KU;  // row pairs per block iteration
+  const int64_t n_iters = VEC ? (kp.n / 2) / per_iter : 0;
+  const longlong2* __restrict__ pv = reinterpret_cast<const longlong2*>(pid);
+  int64_t it = blockIdx.x;
+  if (it < n_iters) {
+    longlong2 cur[KU], nxt[KU];
 #pragma unroll
-    for (int v = 0; v < KU; ++v) {
-      const int64_t i = 2 * (g0 + (int64_t)v * blockDim.x + threadIdx.x);
-      if (kp.keys_vec && i + 1 < kp.n) {
-        const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
-        u[2 * v] = a.x;
-        u[2 * v + 1] = a.y;
-      } else {
-        u[2 * v] = i < kp.n ? pid[i] : -1;
-        u[2 * v + 1] = i + 1 < kp.n ? pid[i + 1] : -1;
+    for (int v = 0; v < KU; ++v) cur[v] = pv[it * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
+    for (; it < n_iters; it += gridDim.x) {  // block-uniform trips
+      const int64_t nx = it + gridDim.x < n_iters ? it + gridDim.x : it;  // in range: no branch around the loads
+#pragma unroll
+      for (int v = 0; v < KU; ++v) nxt[v] = pv[nx * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
+#pragma unroll
+      for (int v = 0; v < KU; ++v) {
+        const int64_t i = 2 * (it * per_iter + (int64_t)v * blockDim.x + threadIdx.x);
+        rescan_emit(kp, cur[v].x, i, bloom, unres_bits, sctl, fix_cnt, fix_rec);
+        rescan_emit(kp, cur[v].y, i + 1, bloom, unres_bits, sctl, fix_cnt, fix_rec);
       }
-    }
-    bool hit[2 * KU];
 #pragma unroll
-    for (int e = 0; e < 2 * KU; ++e) {
-      hit[e] = false;
-      if (u[e] < 0 || u[e] >= kp.U) continue;  // invalid ids were flagged by level 1
-      const uint32_t h = bloom_hash((uint32_t)u[e]);
-      const unsigned bits = bloom_bits(h);
-      if ((bloom[h & (kBloomWords - 1)] & bits) != bits) continue;
-      hit[e] = (unres_bits[u[e] >> 5] >> (u[e] & 31)) & 1u;
-    }
-    unsigned long long m[2 * KU];
-    unsigned nw = 0;
-#pragma unroll
-    for (int e = 0; e < 2 * KU; ++e) {
-      m[e] = __ballot(hit[e]);
-      nw += (unsigned)__popcll(m[e]);
-    }
-    if (nw == 0) continue;  // wave-uniform
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(sctl + 1, nw);
-    base = __shfl(base, 0, 64);
-#pragma unroll
-    for (int e = 0; e < 2 * KU; ++e) {
-      if (hit[e]) {
-        const int64_t i = 2 * (g0 + (int64_t)(e / 2) * blockDim.x + threadIdx.x) + (e & 1);
-        fix_rec[base + __popcll(m[e] & below)] = ((unsigned long long)u[e] << 32) | (unsigned long long)(uint32_t)i;
-        atomicAdd(fix_cnt + (u[e] >> kp.bucket_bits), 1u);
-      }
-      base += (unsigned)__popcll(m[e]);
+      for (int v = 0; v < KU; ++v) cur[v] = nxt[v];
     }
   }
+  // the rows no full iteration covered (all of them without VEC)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = 2 * n_iters * per_iter + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += stride)
+    rescan_emit(kp, pid[i], i, bloom, unres_bits, sctl, fix_cnt, fix_rec);
 }
 
 // Fix-up step 2: the listed rows -> bucket order (fix_start = exclusive scan
@@ -2829,9 +2873,14 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   unsigned* fix_cnt = (unsigned*)(ws + w.fix_cnt);
   unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
   PDP_PROF_BEGIN("k_sieve_rescan", st);
-  hipLaunchKernelGGL(k_sieve_rescan, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
-                     (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
-                     fix_rec);
+  if (kp.keys_vec)
+    hipLaunchKernelGGL(k_sieve_rescan<true>, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
+                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
+                       fix_rec);
+  else
+    hipLaunchKernelGGL(k_sieve_rescan<false>, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
+                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
+                       fix_rec);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   rc = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts

@@ -604,6 +604,8 @@ __global__ void __launch_bounds__(kBlock) k_hp_rows(PT t, const int64_t* __restr
     if (lw[b] != 0.0) atomicAdd(wsmall + b, lw[b]);
 }
 
+__device__ __forceinline__ void weight_bin_add(const IntHists& H, unsigned long long key, double weight);
+
 // int(round(sum of weights)) per distinct value (:94-97), into its bin
 __global__ void __launch_bounds__(kBlock) k_hp_weights(const double* __restrict__ wsmall,
                                                        const WSlot* __restrict__ wtab, uint64_t cap, IntHists H) {
@@ -624,17 +626,33 @@ __global__ void __launch_bounds__(kBlock) k_hp_weights(const double* __restrict_
   const int64_t j = i - 2 * kWSmall;
   if (j >= (int64_t)cap) return;
   const WSlot s = wtab[j];
-  if (s.key == 0) return;
-  const unsigned long long x = s.key - 1;
+  weight_bin_add(H, s.key, s.w);
+}
+
+// a weight-table entry (key = value * 2 + histogram + 1, 0 = none) into its
+// logarithmic bin: int(round(weight)) elements of that value; the bin exists
+// (max = value) even when the weight rounds to 0
+__device__ __forceinline__ void weight_bin_add(const IntHists& H, unsigned long long key, double weight) {
+  if (key == 0) return;
+  const unsigned long long x = key - 1;
   const int h = (int)(x & 1);
   const unsigned long long v = x >> 1;
-  const unsigned long long f = (unsigned long long)rint(s.w);
+  const unsigned long long f = (unsigned long long)rint(weight);
   const int64_t g = (int64_t)h * kLogBins + log_bin_index(v);
   if (f) {
     atomicAdd(H.count + g, f);
     atomicAdd(H.sum + g, f * v);
   }
   atomicMax(H.max + g, v);
+}
+
+// pdp_dataset_histograms_weight_bins: an explicit (key, weight) list, e.g.
+// the global weight sums a rank owns after the multi-rank exchange
+__global__ void __launch_bounds__(kBlock) k_hp_weight_list(const unsigned long long* __restrict__ keys,
+                                                           const double* __restrict__ weights, int64_t n,
+                                                           IntHists H) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) weight_bin_add(H, keys[i], weights[i]);
 }
 
 // per partition with rows: COUNT_PER_PARTITION (sum of counts),
@@ -1041,6 +1059,33 @@ int pdp_dataset_histograms_preaggregated_exchange_offsets(int64_t n_rows, int64_
   *pk_count = w.pkcount;
   *psum = w.psum;
   *minmax = w.minmax;
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms_preaggregated_weight_offsets(int64_t n_rows, int64_t n_partitions, uint64_t* wsmall,
+                                                        uint64_t* wtab, uint64_t* wtab_slots) {
+  if (wsmall == nullptr || wtab == nullptr || wtab_slots == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  if (n_rows < 0 || n_partitions < 0) return pdp::set_error(PDP_E_INVALID, "sizes must be >= 0");
+  const pdp::PWs w = pdp::playout(n_rows, n_partitions);
+  *wsmall = w.wsmall;
+  *wtab = w.wtab;
+  *wtab_slots = pdp::wtab_capacity(n_rows);
+  return PDP_OK;
+}
+
+int pdp_dataset_histograms_weight_bins(const uint64_t* keys, const double* weights, int64_t n,
+                                       const pdp_histogram_bins* out, void* stream) {
+  if (out == nullptr || out->int_count == nullptr || out->int_sum == nullptr || out->int_max == nullptr)
+    return pdp::set_error(PDP_E_INVALID, "the integer pdp_histogram_bins outputs must be set");
+  if (n < 0) return pdp::set_error(PDP_E_INVALID, "n must be >= 0");
+  if (n == 0) return PDP_OK;
+  if (keys == nullptr || weights == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL list");
+  hipStream_t st = (hipStream_t)stream;
+  const pdp::IntHists H{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
+                        (unsigned long long*)out->int_max};
+  PDP_HLAUNCH("k_hp_weight_list", st, pdp::k_hp_weight_list, dim3(pdp::grid_for(n, (int64_t)1 << 30)),
+              dim3(pdp::kBlock), 0, st, (const unsigned long long*)keys, weights, n, H);
   return PDP_OK;
 }
 

@@ -106,10 +106,13 @@ def compute_dataset_histograms(col, data_extractors, backend=None) -> List[hist.
     (privacy id, partition) pair (Linf: rows, Linf-sum: value sum), and per
     partition (rows, distinct privacy ids, value sum).  Returns a one-element
     list holding a DatasetHistograms.  Under torch.distributed each rank
-    passes its shard of rows (sharded by privacy id) and every rank gets the
-    histograms of the whole dataset."""
+    passes its shard of rows and every rank gets the histograms of the whole
+    dataset.  The rows of one privacy id must sit on one rank: as in
+    DPEngine.aggregate, `backend`'s privacy_id_sharding decides whether that
+    is verified (default; ValueError otherwise), established by a shuffle of
+    the rows, or trusted."""
     from pipelinedp_amd import executor as X
-    from pipelinedp_amd.columnar_backend import _h2d, _host_or_device, _value_tensor
+    from pipelinedp_amd.columnar_backend import _h2d, _host_or_device, _value_tensor, shard_rows_by_privacy_id
     import torch
     device = _device(backend)
     pid_raw, pk_raw, val_raw, n_pid, n_pk = _columns(col, data_extractors)
@@ -121,6 +124,11 @@ def compute_dataset_histograms(col, data_extractors, backend=None) -> List[hist.
     pid_t = _h2d(pid_enc.codes, device, torch.int64)
     pk_t = _h2d(pk_enc.codes, device, torch.int64)
     val_t = _value_tensor(val_raw, device) if val_raw is not None else None
+    if parallel.world_info()[0] > 1:
+        if val_t is not None and parallel.all_ranks_any(val_t.dtype != torch.int64):
+            val_t = val_t.to(torch.float64)  # one value kind on every rank
+        mode = getattr(backend, "_pid_sharding", "verify")
+        pid_t, pk_t, val_t, pid_enc = shard_rows_by_privacy_id(mode, pid_t, pk_t, val_t, pid_enc)
     raw = X.dataset_histograms(pid_t, pk_t, val_t, n_privacy_ids=pid_enc.n, n_partitions=pk_enc.n)
     flags = ctypes.c_uint32()
     N.check(N.lib().pdp_bound_error_flags(X._ptr(raw["workspace"]), ctypes.byref(flags), X._stream()),

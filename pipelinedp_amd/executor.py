@@ -541,10 +541,22 @@ def dataset_histograms_preaggregated(pk, count, total, n_partitions_of_pid, n_co
         psum = ws[offs[2].value:offs[2].value + 8 * P].view(torch.float64)
         minmax = ws[offs[3].value:offs[3].value + 16].view(torch.int64)
         parallel.exchange_preaggregated_stats(pk_rows, pk_count, psum, minmax, group)
+        # L0 / L1 weight sums: global before rounding (one owner rank per value)
+        woff = [ctypes.c_uint64() for _ in range(3)]
+        N.check(lib.pdp_dataset_histograms_preaggregated_weight_offsets(n, P, *[ctypes.byref(o) for o in woff]),
+                "pdp_dataset_histograms_preaggregated_weight_offsets")
+        wsmall = ws[woff[0].value:woff[0].value + 8 * 2000].view(torch.float64)
+        slots = woff[2].value
+        wtab = ws[woff[1].value:woff[1].value + 16 * slots].view(torch.int64).view(slots, 2)
+        wkeys, wsums = parallel.exchange_preaggregated_weights(wsmall, wtab, group)
         N.check(lib.pdp_dataset_histograms_preaggregated_finish(_ptr(total), n, P, 1 if rank == 0 else 0,
                                                                 ctypes.byref(s), _ptr(ws), int(ws.numel()),
                                                                 _stream(stream)),
                 "pdp_dataset_histograms_preaggregated_finish")
+        wkeys, wsums = wkeys.contiguous(), wsums.contiguous()
+        N.check(lib.pdp_dataset_histograms_weight_bins(_ptr(wkeys), _ptr(wsums), int(wkeys.numel()),
+                                                       ctypes.byref(s), _stream(stream)),
+                "pdp_dataset_histograms_weight_bins")
         parallel.merge_histogram_bins(out, group)
     out["workspace"] = ws
     return out

@@ -306,6 +306,41 @@ def exchange_preaggregated_stats(pk_rows, pk_count, psum, minmax, group=None):
     minmax[1:2] = hi ^ _SIGN
 
 
+def exchange_preaggregated_weights(wsmall, wtab, group=None):
+    """Between pdp_dataset_histograms_preaggregated_rows and _finish: makes the
+    L0 / L1 weight sums global before they are rounded (a privacy
+    id whose rows sit on two ranks must not be rounded per rank).  `wsmall`
+    (double[2000], values below 1000) is summed over ranks and kept on rank 0
+    only; every live entry of the weight table `wtab` (int64[slots, 2]: key,
+    weight bits; key 0 = empty) goes to the rank that owns its key, which sums
+    the entries per key; the table itself is zeroed.  Returns (keys, weights),
+    the global sums of the keys this rank owns, for
+    pdp_dataset_histograms_weight_bins after _finish (each key on one rank,
+    so merge_histogram_bins adds every value's bin once)."""
+    import torch
+    import torch.distributed as dist
+    world, rank = world_info(group)
+    host = dist.get_backend(group) == "gloo"
+    ws = wsmall.cpu() if host else wsmall
+    dist.all_reduce(ws, op=dist.ReduceOp.SUM, group=group)
+    if rank == 0:
+        wsmall.copy_(ws)
+    else:
+        wsmall.zero_()
+    live = wtab[:, 0] != 0
+    keys = wtab[:, 0][live].clone()
+    w = wtab[:, 1][live].clone().view(torch.float64)
+    wtab.zero_()
+    dest = _owner(keys, world)
+    order = torch.argsort(dest, stable=True)
+    counts = torch.bincount(dest, minlength=world)
+    rk, rw = _exchange([keys[order], w[order]], counts, group)
+    uniq, inv = torch.unique(rk, return_inverse=True)
+    tot = torch.zeros(uniq.numel(), dtype=torch.float64, device=rw.device)
+    tot.index_add_(0, inv, rw)
+    return uniq.to(wtab.device), tot.to(wtab.device)
+
+
 def merge_histogram_bins(out, group=None):
     """Merges the bin arrays of pdp_dataset_histograms_finish over ranks:
     counts and sums added, maxima by maximum over the bins that hold

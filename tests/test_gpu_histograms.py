@@ -311,17 +311,37 @@ def test_preaggregated_empty_input():
     assert all(not getattr(got, f).bins for f in OH.HIST_FIELDS)
 
 
-def _pre_worker(rank, port, results):
+def _pre_data(split):
+    if split == "pid":
+        return _two_rank_data()
+    # privacy ids with 10^3..10^5 rows (L0 / L1 values above 1000: the weight
+    # table, not only the dense sums)
+    rng = np.random.default_rng(22)
+    n = 300_000
+    pid = np.minimum(rng.zipf(1.5, n) - 1, 9_999)
+    pk = np.minimum(rng.zipf(1.3, n) - 1, 1_999)
+    val = np.round(rng.normal(1, 3, n) * 8) / 8
+    return pid, pk, val
+
+
+def _pre_worker(rank, port, results, split):
     import os
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=2)
     try:
-        pid, pk, val = _two_rank_data()
+        pid, pk, val = _pre_data(split)
         pre = HU.preaggregate(pid, pk, val)
-        # shard the pre-aggregated rows by privacy id: rows of one pid on one rank
-        pairs_pid = np.unique(np.stack([pid, pk], 1), axis=0)[:, 0]
-        keep = pairs_pid % 2 == rank
+        if split == "pid":
+            # shard the pre-aggregated rows by privacy id: rows of one pid on one rank
+            pairs_pid = np.unique(np.stack([pid, pk], 1), axis=0)[:, 0]
+            keep = pairs_pid % 2 == rank
+        else:
+            # every other (pid, pk) row: a privacy id's rows span both ranks,
+            # which pre-aggregated input (no privacy-id column) cannot rule out;
+            # its 1 / n_partitions weights must be summed over ranks before
+            # rounding, not rounded per rank
+            keep = np.arange(len(pre[0])) % 2 == rank
         h = _run_pre(*(c[keep] for c in pre), P=2000)
         results[rank] = {f: [tuple(map(float, (b.lower, b.upper, b.count, b.sum, b.max)))
                              for b in getattr(h, f).bins] for f in OH.HIST_FIELDS}
@@ -331,17 +351,18 @@ def _pre_worker(rank, port, results):
         dist.destroy_process_group()
 
 
-def test_preaggregated_two_ranks_match_single_process():
+@pytest.mark.parametrize("split", ["pid", "row"])
+def test_preaggregated_two_ranks_match_single_process(split):
     import socket
     import torch.multiprocessing as mp
-    pid, pk, val = _two_rank_data()
+    pid, pk, val = _pre_data(split)
     single = _run_pre(*HU.preaggregate(pid, pk, val), P=2000)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     results = ctx.Manager().dict()
-    mp.spawn(_pre_worker, args=(port, results), nprocs=2, join=True)
+    mp.spawn(_pre_worker, args=(port, results, split), nprocs=2, join=True)
     res = dict(results)
     assert all(isinstance(res[r], dict) for r in (0, 1)), res
     for r in (0, 1):

@@ -168,6 +168,20 @@ def _pid_worker(rank, port, results):
         allin = [None] * WORLD
         dist.all_gather_object(allin, mine)
         assert every == sorted(r for part in allin for r in part)
+        # the helper aggregate() and compute_dataset_histograms() share
+        # (histograms of row-sharded input were silently wrong)
+        from pipelinedp_amd import columnar as C
+        from pipelinedp_amd.columnar_backend import shard_rows_by_privacy_id
+        enc = C.EncodedKeys(pid, 300, None)
+        try:
+            shard_rows_by_privacy_id("verify", pid, pk, val, enc)
+            results[rank] = "row-sharded ids not detected"
+            return
+        except ValueError as e:
+            assert "more than one rank" in str(e)
+        sp, spk, sval, senc = shard_rows_by_privacy_id("shuffle", pid, pk, val, enc)
+        assert senc.n == int(torch.unique(sp).numel()) and len(spk) == len(sval) == len(sp)
+        assert shard_rows_by_privacy_id("trusted", pid, pk, val, enc)[0] is pid
         results[rank] = "ok"
     except Exception as e:
         results[rank] = repr(e)

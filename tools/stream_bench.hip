@@ -1,0 +1,122 @@
+// stream_bench.hip -- achievable read bandwidth of streaming-load shapes on
+// gfx950, to choose the shape of the privacy-id rescan (pdp_bound.hip
+// k_sieve_rescan) and the level-1 sieve.  Reads an 8 GiB int64 column (the
+// C3 privacy-id column) and prints GB/s per variant (hipEvent timing, best of
+// 5 after a warm-up).  Build:
+//   hipcc --offload-arch=gfx950 -O3 -o tools/stream_bench tools/stream_bench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                                   \
+  do {                                                                             \
+    hipError_t e = (x);                                                            \
+    if (e != hipSuccess) {                                                         \
+      fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));                       \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+constexpr size_t kRows = (size_t)1 << 30;  // 1 Gi int64 = 8 GiB
+
+// A: grid-stride, U independent 16-byte loads per thread per iteration
+template <int U>
+__global__ void __launch_bounds__(256) k_grid(const longlong2* __restrict__ p, size_t n2, unsigned* out) {
+  long long acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x * U;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x * U + threadIdx.x; i < n2; i += stride) {
+    longlong2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i + (size_t)u * blockDim.x < n2 ? p[i + (size_t)u * blockDim.x] : longlong2{0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y;
+  }
+  if (acc == 0x1234567) out[0] = 1;
+}
+
+// B: each block one contiguous span (blocks in order), U loads per thread per step
+template <int U>
+__global__ void __launch_bounds__(256) k_span(const longlong2* __restrict__ p, size_t n2, unsigned* out) {
+  long long acc = 0;
+  const size_t per = (n2 + gridDim.x - 1) / gridDim.x;
+  const size_t b0 = blockIdx.x * per, b1 = b0 + per < n2 ? b0 + per : n2;
+  for (size_t i = b0 + threadIdx.x; i < b1; i += (size_t)blockDim.x * U) {
+    longlong2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i + (size_t)u * blockDim.x < b1 ? p[i + (size_t)u * blockDim.x] : longlong2{0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y;
+  }
+  if (acc == 0x1234567) out[0] = 1;
+}
+
+// C: B + one random LDS probe per row (the rescan's Bloom filter, 64 KiB)
+template <int U>
+__global__ void __launch_bounds__(256) k_span_lds(const longlong2* __restrict__ p, size_t n2, unsigned* out) {
+  __shared__ unsigned bloom[16384];
+  for (int i = threadIdx.x; i < 16384; i += blockDim.x) bloom[i] = i * 2654435761u;
+  __syncthreads();
+  unsigned acc = 0;
+  const size_t per = (n2 + gridDim.x - 1) / gridDim.x;
+  const size_t b0 = blockIdx.x * per, b1 = b0 + per < n2 ? b0 + per : n2;
+  for (size_t i = b0 + threadIdx.x; i < b1; i += (size_t)blockDim.x * U) {
+    longlong2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = i + (size_t)u * blockDim.x < b1 ? p[i + (size_t)u * blockDim.x] : longlong2{0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned h0 = (unsigned)v[u].x * 0x9E3779B1u, h1 = (unsigned)v[u].y * 0x9E3779B1u;
+      acc += bloom[h0 >> 18] & (1u << (h0 & 31));
+      acc += bloom[h1 >> 18] & (1u << (h1 & 31));
+    }
+  }
+  if (acc == 0x1234567) out[0] = 1;
+}
+
+template <typename F>
+double time_it(F&& launch) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  launch();
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CHECK(hipEventRecord(a));
+    launch();
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    best = ms < best ? ms : best;
+  }
+  return best;
+}
+
+int main() {
+  longlong2* p;
+  unsigned* out;
+  CHECK(hipMalloc(&p, kRows * 8));
+  CHECK(hipMalloc(&out, 64));
+  CHECK(hipMemset(p, 3, kRows * 8));
+  const size_t n2 = kRows / 2;
+  const double gb = kRows * 8 / 1e9;
+  auto report = [&](const char* name, double ms) { printf("%-28s %8.3f ms %8.1f GB/s\n", name, ms, gb / (ms * 1e-3)); };
+#define RUN(NAME, KERNEL, GRID)                                                                           \
+  report(NAME, time_it([&] { hipLaunchKernelGGL(KERNEL, dim3(GRID), dim3(256), 0, 0, p, n2, out); }))
+  RUN("grid U=4 g=2048", k_grid<4>, 2048);
+  RUN("grid U=8 g=2048", k_grid<8>, 2048);
+  RUN("grid U=4 g=8192", k_grid<4>, 8192);
+  RUN("grid U=8 g=1024", k_grid<8>, 1024);
+  RUN("span U=4 g=2048", k_span<4>, 2048);
+  RUN("span U=8 g=2048", k_span<8>, 2048);
+  RUN("span U=4 g=8192", k_span<4>, 8192);
+  RUN("span U=8 g=1024", k_span<8>, 1024);
+  RUN("span+lds U=4 g=1024", k_span_lds<4>, 1024);
+  RUN("span+lds U=8 g=1024", k_span_lds<8>, 1024);
+  RUN("span+lds U=8 g=2048", k_span_lds<8>, 2048);
+  CHECK(hipFree(p));
+  CHECK(hipFree(out));
+  return 0;
+}
