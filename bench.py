@@ -79,7 +79,7 @@ def parse():
                          "share of an N-GPU run on one GPU")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5"), default="c3")
+    ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5", "hist"), default="c3")
     ap.add_argument("--rows", type=int, default=0, help="override: rows in total (c3) / per GPU (c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
@@ -373,6 +373,106 @@ def run_api_workload(args, workload, world, rank, device):
     }
 
 
+HIST = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000)
+
+
+def run_hist_workload(args, world, rank, device):
+    """compute_dataset_histograms' device pass (SURVEY §8(f) rank 4,
+    computing_histograms.py:456-513) on C2's shape: 1e8 rows per GPU, 1e6
+    privacy ids, 1e5 partitions, fp64 values N(5, 3) clipped to [0, 10],
+    inputs resident in HBM.  One step = one pdp_dataset_histograms call (all
+    seven histograms, bins on the device; multi-rank: the exchange and merge
+    included)."""
+    import torch
+    import torch.distributed as dist
+    from pipelinedp_amd import _native as N
+    from pipelinedp_amd import executor as X
+    n = args.rows or HIST["rows"]
+    U, P = HIST["privacy_ids"], HIST["partitions"]
+    g = torch.Generator(device=device)
+    g.manual_seed(3000 + rank)
+    pid = torch.randint(0, U, (n,), generator=g, device=device, dtype=torch.int64)
+    pk = torch.randint(0, P, (n,), generator=g, device=device, dtype=torch.int64)
+    val = (torch.randn(n, generator=g, device=device, dtype=torch.float64) * 3.0 + 5.0).clamp_(MIN_VALUE, MAX_VALUE)
+    ws = X.BoundWorkspace()
+
+    def step():
+        X.dataset_histograms(pid, pk, val, n_privacy_ids=U, n_partitions=P, workspace=ws)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    N.profiler_enable(True)
+    for _ in range(args.steps):
+        step()
+    kernels = N.profiler_report()
+    N.profiler_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    del pid, pk, val, ws
+    kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
+    launches = {k: v[1] / args.steps for k, v in kernels.items()}
+    # algorithmic bytes per launch (DESIGN.md §3b): rows read / records moved once
+    alg = {"k_hb_count": 16.0 * n, "k_hb_l1": (24.0 + 16.0) * n, "k_hb_bcount": 8.0 * n,
+           "k_hb_l2": 32.0 * n, "k_hb_pairs": 16.0 * n}
+    table = {}
+    for k, ms in kernel_ms.items():
+        e = {"ms": ms, "launches_per_step": launches[k]}
+        if k in alg:
+            e["alg_bytes"] = alg[k]
+            e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
+            e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
+        table[k] = e
+    dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
+    ms_per_step = elapsed / args.steps * 1e3
+    path_bytes = 24.0 * n
+    path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
+    return {
+        "value": n * world * args.steps / elapsed,
+        "ms_per_step": ms_per_step,
+        "config": {"workload": f"dataset histograms (compute_dataset_histograms, all seven) over {n:.3g} rows "
+                               f"per GPU, {U:.3g} privacy ids, {P:.3g} partitions, fp64 values",
+                   "rows_per_gpu": n, "privacy_ids": U, "partitions": P,
+                   "parallelism": f"rows sharded by privacy_id over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": table[dom].get("achieved_gbs"),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": table[dom].get("frac"), "traffic": None,
+                     "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom]},
+        "path_roofline": {"achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes},
+        "kernels": table, "bound_plan": None, "partitions_kept": None, "api": None,
+    }
+
+
+def hist_cpu_baseline(sample_rows):
+    """The NumPy oracle of compute_dataset_histograms (oracle/histograms.py,
+    vectorised, one process) on a sample of the hist workload."""
+    from oracle import histograms as OH
+    from oracle import strong_baseline as strong
+    rng = np.random.default_rng(3)
+    n = sample_rows
+    pid = rng.integers(0, max(1, HIST["privacy_ids"] * n // HIST["rows"]), n)
+    pk = rng.integers(0, HIST["partitions"], n)
+    val = np.clip(rng.normal(5.0, 3.0, n), MIN_VALUE, MAX_VALUE)
+    t0 = time.perf_counter()
+    OH.dataset_histograms(pid, pk, val)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": 1, "kind": "port", "cpu_model": strong.cpu_model(),
+            "sample": f"{n} rows shaped like the hist workload; oracle/histograms.py (vectorised NumPy "
+                      f"restatement of computing_histograms.py) on one core, {dt:.1f} s"}
+
+
 def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
     """Algorithmic bytes of each kernel of one step: every
     input it must read once plus every output it must write once.  `stats`
@@ -600,6 +700,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2"):
         cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "hist":
+        cpu = (hist_cpu_baseline(4 * args.cpu_sample_rows), None)
     import torch
     import torch.distributed as dist
     # PDP_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
@@ -619,6 +721,8 @@ def main():
     if args.workload in ("c4", "c5"):
         r = run_api_workload(args, args.workload, world, rank, device)
         r.setdefault("api", None)
+    elif args.workload == "hist":
+        r = run_hist_workload(args, world, rank, device)
     else:
         r = run_workload(args, args.workload, world, rank, device, PMC_SUMMARY[args.workload])
     result = {
@@ -639,6 +743,7 @@ def main():
                  "c4": "synthetic (uniform pid/pk, U(0,10) values), generated on device",
                  "c5": "synthetic (Pareto(1.5) rows per pid, Zipf(1.1) pk, lognormal(1,1) values clipped to "
                        "[0,20]), generated on device",
+                 "hist": "synthetic (uniform pid/pk, N(5,3) clipped values), generated on device",
                  }[args.workload],
         "config": r["config"],
         "roofline": r["roofline"],

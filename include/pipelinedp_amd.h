@@ -340,7 +340,14 @@ int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uin
  * when min == max (one bin [min, min]), 0 when empty.  A bin with count 0 is
  * absent from the reference's histogram.  All outputs are device arrays the
  * library zeroes and fills on `stream`; out-of-range keys set the error word
- * that pdp_bound_error_flags reads from this workspace.  n_rows < 2^31. */
+ * that pdp_bound_error_flags reads from this workspace.  n_rows < 2^31.
+ * Up to ~1e8 rows the (privacy id, partition) pairs are found by hashing rows
+ * into pair buckets, one LDS table per bucket; the call then reads one word
+ * back (it synchronizes `stream` once) to confirm no bucket overflowed, and
+ * redoes the pairs on an HBM pair table if one did (never for hashed real
+ * data).  Larger shards use the HBM pair table directly.  value_kind |
+ * PDP_HIST_FORCE_PAIR_TABLE (tests) forces the pair table. */
+#define PDP_HIST_FORCE_PAIR_TABLE 0x100
 #define PDP_HIST_LOG_BINS 16384
 #define PDP_HIST_SUM_BUCKETS 10000
 #define PDP_HIST_N_INT 5

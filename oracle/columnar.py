@@ -75,7 +75,8 @@ def pair_hash(seed, pid, pk):
     hi = (pid >> _U64(32)).astype(np.uint32)
     pk32 = (pk & _U64(0xFFFFFFFF)).astype(np.uint32)
     with np.errstate(over="ignore"):
-        h = fmix32((lo * np.uint32(0x9E3779B1)) ^ (hi * np.uint32(0x7FEB352D)) ^ s0)
+        rot = (hi << np.uint32(16)) | (hi >> np.uint32(16))
+        h = (lo ^ rot ^ s0) * np.uint32(0x9E3779B1)
         return fmix32(h ^ (pk32 * np.uint32(0xC2B2AE3D) + s1))
 
 

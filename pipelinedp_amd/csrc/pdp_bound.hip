@@ -112,15 +112,31 @@ inline bool l1_hist_u16(int key_format, int64_t n_buckets) {
 // second bucket-kernel launch whose pair records follow the main ones.
 // Kept pairs and rows are exactly those of the unsieved path.
 constexpr int kSieveChunkItems = 4;                            // rows per thread and chunk
+#ifndef PDP_AB_L1BUFS
+constexpr int kSieveBufs = 2;  // full tiles: chunks of loads in flight (register buffers)
+#else
+constexpr int kSieveBufs = PDP_AB_L1BUFS;
+#endif
 constexpr int kSieveChunk = kL1Threads * kSieveChunkItems;     // rows filtered per chunk
 constexpr int kSieveCap = 12288;                               // candidate slots of the LDS stage
 constexpr int kSieveItems = kSieveCap / kL1Threads;            // per thread at a flush
 // a tile's flush blocks lie back to back from tile * kSieveTileStride
 constexpr int64_t kSieveTileStride = kTileRows;
 constexpr int kSieveMaxT16 = 1 << 15;                          // t <= 1/2
-constexpr int kBloomWords = 16384;                             // k_sieve_rescan: 64 KiB LDS Bloom filter
-constexpr int kRescanThreads = 512;                            // two workgroups per CU
-constexpr int kSieveL2Groups = 4;  // tile groups per level-2 workgroup with the sieve
+// k_sieve_rescan: a 16 KiB LDS Bloom filter (a 64 KiB one limits the CU to
+// two workgroups, and the rescan then streams at 3.7 instead of 6.1 TB/s:
+// tools/stream_bench.hip, profiles/r03/stream_bench.txt); above
+// kBloomMaxIds unresolved ids it is skipped and every row tests the bitmap
+constexpr int kBloomWords = 4096;  // == 1 << kBloomBits
+constexpr unsigned kBloomMaxIds = 8192;
+constexpr int kRescanThreads = 512;
+constexpr int kRescanBlocks = 1024;
+// tile groups per level-2 workgroup with the sieve, at most: the plan takes
+// as many as keep a workgroup's expected records (tiles x candidates per tile
+// / super-buckets) within one LDS window (kL2Target), since a second window
+// holding a few hundred records costs as much latency as a full one
+constexpr int kSieveL2Groups = 4;
+constexpr double kL2Target = 7000.0;
 // a tile flushes at most once per chunk, and every flush but its last holds
 // > kSieveCap - kSieveChunk records, so its blocks fit the kStagesPerTile
 // level-1 slots
@@ -157,6 +173,7 @@ struct Plan {
   int sieve;            // threshold sieve: t = sieve / 2^16 (0 = off); k_sieve_l1 instead of k_scatter_l1_local
   int64_t n_slots1;     // level-1 blocks (stages, or sieve flush slots: n_tiles * kStagesPerTile)
   int64_t buckets_out;  // buckets of pair records: n_buckets, 2 * n_buckets with the sieve (fix-up after)
+  int l2_mult;          // tile groups per level-2 workgroup (1 without the sieve)
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -270,7 +287,8 @@ Plan make_plan(const pdp_bound_config* c) {
   const bool sieve_ok = p.algorithm == PDP_ALGO_BUCKETED && p.l1_local && p.merge == PDP_MERGE_RANGES &&
                         p.bucket_bits >= 6 && p.key_format != PDP_KEYS_WIDE &&
                         (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) <= kL1LocalLds &&
-                        p.n_tiles * kSieveTileStride < ((int64_t)1 << 32);
+                        p.n_tiles * kSieveTileStride < ((int64_t)1 << 32) &&
+                        c->n_privacy_ids < ((int64_t)1 << 32) - 1;  // fix-up lists hold 32-bit ids
   int t16 = 0;
   if (sieve_ok && c->sieve > 0) {
     t16 = c->sieve < kSieveMaxT16 ? c->sieve : kSieveMaxT16;
@@ -286,6 +304,14 @@ Plan make_plan(const pdp_bound_config* c) {
   p.sieve = t16 > 0 ? t16 : 0;
   p.n_slots1 = p.sieve ? p.n_tiles * kStagesPerTile : p.n_stages;
   p.buckets_out = p.sieve ? 2 * p.n_buckets : p.n_buckets;
+  p.l2_mult = 1;
+  if (p.sieve) {
+    // expected records of one (group of kL2GroupTiles tiles, super-bucket)
+    const double per_group = (double)kL2GroupTiles * (double)kTileRows * ((double)p.sieve / 65536.0) /
+                             (double)(p.n_supers > 0 ? p.n_supers : 1);
+    int m = (int)(kL2Target / (per_group > 1.0 ? per_group : 1.0));
+    p.l2_mult = m < 1 ? 1 : (m > kSieveL2Groups ? kSieveL2Groups : m);
+  }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
     p.lds_bytes += ((int64_t)8 << p.bucket_bits);  // {pid hash, sketch-maximum high half} per pid
@@ -315,7 +341,7 @@ struct Ws {
   // bucketed path
   uint64_t counts_tm, counts, chunk_sums, super_base, super_tm, super_off, keys1, rows1, keys2, rows2;
   uint64_t csum, gcur;  // level-2 cursor scans: per tile chunk, per tile group (x n_buckets)
-  uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, record index)
+  uint64_t cand_key, cand_idx;  // bucket kernel: B1's candidate list (record-local key, row)
   uint64_t soff;                // tile-local level 1: per stage, super-bucket run starts (u16)
   uint64_t counts_tm2;          // tile-local level 1, u16 counts: second half-tile bucket counts
   // threshold sieve: flush-block starts (u32 per slot), unresolved privacy
@@ -486,7 +512,7 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.n_fine_ranges = p.n_fine;
   k.keys_vec = 0;
   k.n_slots1 = p.n_slots1;
-  k.l2_group_mult = p.sieve ? kSieveL2Groups : 1;
+  k.l2_group_mult = p.l2_mult;
   k.sieve_t32 = (uint32_t)p.sieve << 16;
   k.sieve_mark = p.sieve != 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
@@ -1183,6 +1209,7 @@ __global__ void __launch_bounds__(kBlock) k_super_scan(KP kp, const unsigned* __
 // privacy-id column is read once (k_part_hist + k_super_scan are not run).
 static_assert(kTileRows % kL1Rows == 0, "a tile is a whole number of level-1 stages");
 static_assert(kL2Runs * kSieveL2Groups <= kL2Threads, "one level-1 slot per thread in the run scan");
+static_assert(kSieveTileStride == kTileRows, "level 2 recovers a run's tile from its position");
 
 // the LDS stage block [0, total) -> dst, 16 bytes per lane
 template <typename K>
@@ -1337,6 +1364,9 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
 // the tile's unused slots get empty runs.  Rows with invalid keys set the
 // error word; dead rows (non-public partitions) are simply dropped.  The
 // tile's candidate counts per bucket feed the level-2 cursors as before.
+#ifdef PDP_PHASE_CLOCK
+__device__ unsigned g_phase_l1, g_phase_l2, g_phase_bk;  // profiling builds: prints so far per kernel
+#endif
 template <int FMT, bool U16>
 __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
                                                          const int64_t* __restrict__ pk,
@@ -1383,11 +1413,27 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   unsigned written = 0;  // block-uniform: this tile's records already written
   int slot = 0;
   // the stage's `total` records -> counting sort by super-bucket -> block
+#ifdef PDP_PHASE_CLOCK
+  unsigned long long fl_ticks = 0, t_start = wall_clock64();
+#endif
   auto flush = [&](unsigned total) {
+#ifdef PDP_PHASE_CLOCK
+    const unsigned long long f0 = wall_clock64();
+#endif
     // runs per super-bucket: LDS histogram, one-wave scan
     for (int B = threadIdx.x; B < nd; B += blockDim.x) s.hist[B] = 0;
     __syncthreads();
-    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) atomicAdd(s.hist + s.dest[e], 1u);
+    // runs per super-bucket, and the tile's candidates per bucket (counted
+    // here, on the compacted stage, rather than per row)
+    const uint64_t mid_mask = ((uint64_t)1 << mid_bits) - 1;
+    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) {
+      const unsigned dd = s.dest[e];
+      atomicAdd(s.hist + dd, 1u);
+      const int64_t bkt = ((int64_t)dd << kp.super_bits) |
+                          (int64_t)((((uint64_t)s.keys[e] >> kp.pk_bits) & mid_mask) >> kp.bucket_bits);
+      if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+      else atomicAdd(bh + bkt, 1u);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {
       unsigned carry = 0;
@@ -1422,6 +1468,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
     written += total;
     ++slot;
     __syncthreads();
+#ifdef PDP_PHASE_CLOCK
+    fl_ticks += wall_clock64() - f0;
+#endif
   };
   // U16: the tile's counts in two halves (counts_tm, counts_tm2)
   const bool split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
@@ -1438,8 +1487,15 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
       for (int q = 0; q < Q; q += 2) {
         const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
         if constexpr (FULL) {
+#ifdef PDP_AB_NT
+          typedef long long v2i64 __attribute__((ext_vector_type(2)));
+          const v2i64 av = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(pid + i));
+          const v2i64 cv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(pk + i));
+          const longlong2 a{av.x, av.y}, c{cv.x, cv.y};
+#else
           const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
           const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
+#endif
           u[q] = a.x;
           u[q + 1] = a.y;
           k[q] = c.x;
@@ -1483,14 +1539,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         } else {  // PACKED / PACKED_WIDE
           x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
         }
-        if (c) {
-          const int64_t bkt = u[q] >> kp.bucket_bits;
-          if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
-          else atomicAdd(bh + bkt, 1u);
-        }
       }
       if constexpr (FULL) {
-        const int64_t cp = c0 + 2 * kSieveChunk < t1 ? c0 + 2 * kSieveChunk : t1 - kSieveChunk;
+        const int64_t cp = c0 + kSieveBufs * kSieveChunk < t1 ? c0 + kSieveBufs * kSieveChunk : t1 - kSieveChunk;
         load(cp, u, k);
       } else {
         if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
@@ -1525,21 +1576,19 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         __syncthreads();
       }
     };
-    int64_t ua[Q], ka[Q], ub[Q], kb[Q];
-    if constexpr (FULL) {
-      load(t0, ua, ka);
-      load(t0 + kSieveChunk, ub, kb);
-    } else {
+    if constexpr (FULL) {  // a fixed trip count: the same loads are pending on every path
+      static_assert((kTileRows / kSieveChunk) % kSieveBufs == 0, "chunk groups per tile");
+      int64_t ub[kSieveBufs][Q], kb[kSieveBufs][Q];
+#pragma unroll
+      for (int b = 0; b < kSieveBufs; ++b) load(t0 + (int64_t)b * kSieveChunk, ub[b], kb[b]);
+      for (int j = 0; j < (int)(kTileRows / kSieveChunk); j += kSieveBufs) {
+#pragma unroll
+        for (int b = 0; b < kSieveBufs; ++b) body(t0 + (int64_t)(j + b) * kSieveChunk, ub[b], kb[b]);
+      }
+    } else {  // the last tile, unaligned columns: two chunks in flight
+      int64_t ua[Q], ka[Q], ub[Q], kb[Q];
       if (t0 < t1) load(t0, ua, ka);
       if (t0 + kSieveChunk < t1) load(t0 + kSieveChunk, ub, kb);
-    }
-    if constexpr (FULL) {  // a fixed trip count: the same loads are pending on every path
-      static_assert((kTileRows / kSieveChunk) % 2 == 0, "chunk pairs per tile");
-      for (int j = 0; j < (int)(kTileRows / kSieveChunk); j += 2) {
-        body(t0 + (int64_t)j * kSieveChunk, ua, ka);
-        body(t0 + (int64_t)(j + 1) * kSieveChunk, ub, kb);
-      }
-    } else {
       for (int64_t c0 = t0; c0 < t1; c0 += 2 * kSieveChunk) {
         body(c0, ua, ka);
         if (c0 + kSieveChunk < t1) body(c0 + kSieveChunk, ub, kb);  // block-uniform
@@ -1549,6 +1598,11 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   if (kp.keys_vec && t1 - t0 == kTileRows) run(std::true_type{});
   else run(std::false_type{});
   if (bad) atomicOr(err, 1u);
+#ifdef PDP_PHASE_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x % 1999 == 5 && atomicAdd(&g_phase_l1, 1u) < 40u)
+    printf("l1 tile %d slots %d records %u total %llu flush %llu (10 ns)\n", (int)t, slot, written,
+           wall_clock64() - t_start, fl_ticks);
+#endif
   // the tile's unused slots: empty runs
   for (int j = slot; j < kStagesPerTile; ++j) {
     const int64_t sl = t * kStagesPerTile + j;
@@ -1611,16 +1665,22 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   using SL = StageLds<KO, MAXD, true, NI, kL2Threads>;
   using D = typename SL::D;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
+#ifdef PDP_PHASE_CLOCK
+  unsigned long long c0 = wall_clock64(), c_tab = 0, c_ld = 0, c_sort = 0, c_wr = 0, cw = 0;
+  int n_win = 0;
+#endif
   // the workgroup's non-empty runs, in slot order
+  // (a run's tile is rsrc / kTileRows: every level-1 block of tile t starts at
+  // or after t * kTileRows, inside its tile's region -- and keeping the LDS of
+  // a PACKED workgroup at <= 80 KiB lets two of them share a CU)
   __shared__ unsigned rbeg[kL2Threads + 1];  // start of each run in the concatenation
   __shared__ unsigned rsrc[kL2Threads];      // its first record in keys1
-  __shared__ unsigned rtile[kL2Threads];     // PACKED: first row of its tile
   __shared__ unsigned wsum[kL2Threads / 64 + 1], wsum2[kL2Threads / 64 + 1];
   // XCD-aware order: a group's workgroups (all super-buckets) run one after
   // another on one XCD (blocks are placed round-robin, linear id % 8), so the
   // cache lines that two neighbouring runs of a stage block share are read
   // from that XCD's L2
-  // a workgroup takes kp.l2_group_mult tile groups (4 with the sieve, whose
+  // a workgroup takes kp.l2_group_mult tile groups (up to 4 with the sieve, whose
   // blocks hold a fraction of the rows; <= kL2Threads slots, one per thread)
   const int nd = (int)kp.n_supers;
   const int M = kp.l2_group_mult;
@@ -1647,7 +1707,6 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   if (len > 0) {
     rbeg[idx] = ex;
     rsrc[idx] = src;
-    rtile[idx] = (unsigned)(((S0 + threadIdx.x) / kStagesPerTile) * kTileRows);
   }
   if (threadIdx.x == 0) rbeg[nnz] = total;
   const int nr = (int)nnz;
@@ -1659,6 +1718,9 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   }
   __syncthreads();
   if (total == 0) return;  // block-uniform
+#ifdef PDP_PHASE_CLOCK
+  c_tab = wall_clock64() - c0;
+#endif
   const int bb = kp.bucket_bits;
   const uint32_t local_mask = (1u << bb) - 1;
   const int sub_shift = kp.pk_bits + kp.bucket_bits;
@@ -1696,7 +1758,7 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
           const unsigned i = rsrc[j] + (v - rbeg[j]);
           raw[q] = keys1[i];
           if (ROWS1) rr[q] = rows1[i];
-          else rr[q] = rtile[j];
+          else rr[q] = rsrc[j] & ~(unsigned)(kTileRows - 1);  // first row of the run's tile
         }
       }
 #pragma unroll
@@ -1719,12 +1781,31 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
       }
     }
     __syncthreads();  // the destination tags are rewritten by the counting sort
+#ifdef PDP_PHASE_CLOCK
+    const unsigned long long ca = wall_clock64();
+#endif
     unsigned rank[NI];
     stage_count(s, nsub, d, rank);
+#ifdef PDP_PHASE_CLOCK
+    const unsigned long long cb = wall_clock64();
+#endif
     stage_write(s, nsub, d, rank, x, r, keys2, rows2);
     for (int t = threadIdx.x; t < nsub; t += blockDim.x) s.gcur[t] += s.hist[t];
     __syncthreads();
+#ifdef PDP_PHASE_CLOCK
+    const unsigned long long cc = wall_clock64();
+    c_ld += ca - (cw ? cw : c0 + c_tab);
+    c_sort += cb - ca;
+    c_wr += cc - cb;
+    cw = cc;
+    ++n_win;
+#endif
   }
+#ifdef PDP_PHASE_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x % 4001 == 77 && atomicAdd(&g_phase_l2, 1u) < 40u)
+    printf("l2 wg %d runs %d records %u windows %d table %llu load %llu sort %llu write %llu total %llu (10 ns)\n",
+           (int)blockIdx.x, nr, total, n_win, c_tab, c_ld, c_sort, c_wr, wall_clock64() - c0);
+#endif
 }
 
 // Per-wave LDS queue of candidate rows (capacity 2 waves' worth): rows that
@@ -1882,6 +1963,22 @@ struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
   double* f2;                    // normalized sum of squares
 };
 
+// PDP_PHASE_CLOCK (profiling builds only, tools/build_variants.sh): thread 0
+// of a few buckets prints the wall-clock time (10 ns ticks) of each phase of
+// k_bucket_bound; results are unchanged (the r02 ablation builds that skipped
+// phases left the merge reading unwritten records)
+#ifdef PDP_PHASE_CLOCK
+#define PDP_PHASE(k)                             \
+  do {                                           \
+    __syncthreads();                             \
+    if (threadIdx.x == 0) ph[k] = wall_clock64(); \
+  } while (0)
+#else
+#define PDP_PHASE(k) \
+  do {               \
+  } while (0)
+#endif
+
 template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES, bool COMPACT>
 __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const RecKey<COMPACT>* __restrict__ keys,
                                                                  const unsigned* __restrict__ rowidx,
@@ -1894,6 +1991,20 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
                                                                  unsigned* __restrict__ unres_list,
                                                                  unsigned* __restrict__ sctl, unsigned* __restrict__ err) {
   extern __shared__ unsigned long long smem[];
+#ifdef PDP_PHASE_CLOCK
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+  if (threadIdx.x == 0) ph[0] = wall_clock64();
+#endif
+  // an empty bucket of the sieve's fix-up launch (most of them: only
+  // unresolved privacy ids have rows there) writes its empty runs and stops;
+  // the main launch's empty buckets still mark their privacy ids unresolved
+  if (!kp.sieve_mark && offsets[blockIdx.x] == offsets[blockIdx.x + 1]) {  // block-uniform
+    if (RANGES) {
+      unsigned* const run0 = rec.runs + (int64_t)blockIdx.x * (kp.n_ranges + 1);
+      for (int t = threadIdx.x; t <= kp.n_ranges; t += blockDim.x) run0[t] = 0;
+    }
+    return;
+  }
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
   const int64_t n_slots = S * l0;
@@ -1941,17 +2052,20 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   // sketch at its first row and never left it (the maximum only decreases),
   // so every one of its rows is a candidate here: the candidates still in
   // their sketch after the insert are appended to a per-bucket list
-  // (record-local key + record index) and B2 reads only that list.
+  // (record-local key + row) and B2 reads only that list.
   __shared__ unsigned ccount;
   if (threadIdx.x == 0) ccount = 0;
   __syncthreads();
+  PDP_PHASE(1);
   const uint64_t lbits = ((uint64_t)1 << (kp.pk_bits + kp.bucket_bits)) - 1;  // local pid | partition
-  stream_bucket<COMPACT ? 4 : kUnroll, kRowIndex>(
+  // (each record's row index rides along, loaded with its key: B2 then needs
+  // no dependent gather of it)
+  stream_bucket<COMPACT ? 4 : kUnroll, kRowLoad>(
       keys, rowidx, begin, end, wq,
       // the candidate test rides on the pid-hash read (b1_candidate)
       [&](RecKey<COMPACT> v) -> uint64_t { return b1_candidate(kp, hpid, v); },
       [&](uint64_t x) { return x != kEmpty; },
-      [&](uint64_t x, uint32_t i)  {
+      [&](uint64_t x, uint32_t i)  {  // i: the record's row
         const int64_t pl = (int64_t)((x >> kp.pk_bits) & bmask);
         unsigned long long* s = sk + pl;
         if (x < s[(l0 - 1) * S]) sketch_insert_strided(s, l0, S, x);
@@ -1992,11 +2106,8 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
       }
     }
   }
-#ifdef PDP_ABL_B1_ONLY
-  return;
-#endif
-  // B2: rows of kept pairs, from B1's candidate list (the row index gathered
-  // for the rows of kept pairs only)
+  PDP_PHASE(2);
+  // B2: rows of kept pairs, from B1's candidate list (key + row)
   const int flags = kp.clip.flags;
   stream_bucket<COMPACT ? 1 : kUnroll / 2, kRowLoad>(
       cand_key, cand_idx, begin, begin + ccount, wq, conv,
@@ -2009,7 +2120,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
       const int64_t pl = (x >> kp.pk_bits) & bmask;
       const int j = sketch_find_strided(sk + pl, l0, S, x);
       if (j < 0) return;
-      const uint32_t r = rowidx[ci];
+      const uint32_t r = ci;  // the candidate's row (B1 carried it)
       if (r >= (uint64_t)kp.n) {  // malformed record: flagged, never dereferenced
         atomicOr(err, 1u);
         return;
@@ -2041,9 +2152,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
       }
   });
   __syncthreads();
-#ifdef PDP_ABL_NO_B3
-  return;
-#endif
+  PDP_PHASE(3);
   if (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) {
     // B2.5: the kept rows' values replace their row keys in the row sketches,
     // all of a thread's gathers in flight together (B3 then reads LDS only;
@@ -2070,6 +2179,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     }
     __syncthreads();
   }
+  PDP_PHASE(4);
   const void* const b3_value = (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) ? nullptr : value;
   unsigned* run = nullptr;
   if (RANGES) {
@@ -2122,46 +2232,47 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
       add_pair_to_partition(acc, p, ps, flags);
     }
   }
+#ifdef PDP_PHASE_CLOCK
+  PDP_PHASE(5);
+  if (threadIdx.x == 0 && blockIdx.x % 997 == 11 && atomicAdd(&g_phase_bk, 1u) < 40u)
+    printf("phase bucket %d records %u cand %u init %llu b1 %llu b2 %llu b25 %llu b3 %llu (10 ns)\n", (int)b,
+           (unsigned)(end - begin), ccount, ph[1] - ph[0], ph[2] - ph[1], ph[3] - ph[2], ph[4] - ph[3],
+           ph[5] - ph[4]);
+#endif
 }
 
 // ------------------------------------------------ threshold-sieve fix-up --
-// Bloom hash of a privacy id: word index from bits [0, 14), three bit
-// positions from bits [15, 30) (one LDS word per test)
-__device__ __forceinline__ uint32_t bloom_hash(uint32_t id) { return fmix32(id * 0x9E3779B1u + 0x7F4A7C15u); }
-__device__ __forceinline__ unsigned bloom_bits(uint32_t h) {
-  return (1u << ((h >> 15) & 31)) | (1u << ((h >> 20) & 31)) | (1u << ((h >> 25) & 31));
-}
+// Bloom filter of the unresolved privacy ids (k_sieve_rescan): one
+// multiplicative hash per id, its top 12 bits the LDS word, two bit
+// positions from its low 10 bits (one full-rate-cheap test per row: the
+// rescan streams 8 B per row and must stay memory-bound)
+constexpr int kBloomBits = 12;
+static_assert(kBloomWords == 1 << kBloomBits, "Bloom filter size");
+__device__ __forceinline__ uint32_t bloom_hash(uint32_t id) { return id * 0x9E3779B1u; }
+__device__ __forceinline__ unsigned bloom_word(uint32_t h) { return h >> (32 - kBloomBits); }
+__device__ __forceinline__ unsigned bloom_bits(uint32_t h) { return (1u << (h & 31)) | (1u << ((h >> 5) & 31)); }
 
-// Fix-up step 1: every row of an unresolved privacy id.  One streaming read
-// of the privacy-id column (8 B per row); a row is tested against an LDS Bloom
-// filter of the unresolved list (one word, three bits; each workgroup builds
-// its own) and, on a hit, against the exact bitmap.  Rows of unresolved ids
-// are appended to fix_rec as (privacy id << 32 | row) -- one returning atomic
-// per wave and batch -- and counted per bucket.  No unresolved id: no work.
-// VEC (16-byte aligned column): the full block iterations load their rows
-// with unconditional 16-byte loads, the next iteration's in flight while this
-// one is tested (branch-free, so the loads are not serialised by waits); the
-// remaining rows go through a guarded scalar loop.
-__device__ __forceinline__ void rescan_emit(const KP& kp, int64_t u, int64_t i, const unsigned* bloom,
-                                            const unsigned* __restrict__ unres_bits, unsigned* __restrict__ sctl,
-                                            unsigned* __restrict__ fix_cnt, unsigned long long* __restrict__ fix_rec) {
-  bool hit = false;
-  if ((uint64_t)u < (uint64_t)kp.U) {  // invalid ids were flagged by level 1
+// Fix-up step 1: the rows that may belong to an unresolved privacy id.  One
+// streaming read of the privacy-id column (8 B per row); a row is tested
+// against an LDS Bloom filter of the unresolved list (one word, two bits;
+// each workgroup builds its own), and the positives -- with the filter's
+// false positives, ~1e-3 of the rows -- are appended to fix_rec as
+// (privacy id << 32 | row).  The test touches LDS only, and positives wait in
+// a per-wave LDS queue that goes out 64 entries at a time, so the stream's
+// loads (the next iteration's in flight while this one is tested) are never
+// drained by a dependent global access.  k_fix_filter then keeps the exact
+// ones.  Without the filter (more than kBloomMaxIds unresolved ids) every
+// in-range row is tested against the bitmap here.  No unresolved id: no work.
+constexpr int kRescanQueue = 128;  // per-wave queue: < 64 waiting + one batch of <= 64
+template <bool BLOOM>
+__device__ __forceinline__ bool rescan_maybe(const KP& kp, int64_t u, const unsigned* bloom,
+                                             const unsigned* __restrict__ unres_bits) {
+  if constexpr (BLOOM) {  // LDS only, no short circuit: the reads of a batch go out together
     const uint32_t h = bloom_hash((uint32_t)u);
     const unsigned bits = bloom_bits(h);
-    if ((bloom[h & (kBloomWords - 1)] & bits) == bits) hit = (unres_bits[u >> 5] >> (u & 31)) & 1u;
-  }
-  const unsigned long long m = __ballot(hit);
-  if (m == 0) return;  // wave-uniform
-  const unsigned long long active = __ballot(true);
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)active) - 1;
-  unsigned base = 0;
-  if (lane == leader) base = atomicAdd(sctl + 1, (unsigned)__popcll(m));
-  base = __shfl(base, leader, 64);
-  if (hit) {
-    fix_rec[base + __popcll(m & ((1ULL << lane) - 1))] = ((unsigned long long)u << 32) | (unsigned long long)(uint32_t)i;
-    atomicAdd(fix_cnt + (u >> kp.bucket_bits), 1u);
+    return ((uint64_t)u < (uint64_t)kp.U) & ((bloom[bloom_word(h)] & bits) == bits);
+  } else {
+    return (uint64_t)u < (uint64_t)kp.U && ((unres_bits[u >> 5] >> (u & 31)) & 1u);  // invalid ids: flagged by level 1
   }
 }
 
@@ -2170,45 +2281,111 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
                                                                  const unsigned* __restrict__ unres_bits,
                                                                  const unsigned* __restrict__ unres_list,
                                                                  unsigned* __restrict__ sctl,
-                                                                 unsigned* __restrict__ fix_cnt,
                                                                  unsigned long long* __restrict__ fix_rec) {
   __shared__ unsigned bloom[kBloomWords];
+  __shared__ unsigned long long queue[kRescanThreads / 64][kRescanQueue];
   const unsigned n_unres = sctl[0];
   if (n_unres == 0) return;  // grid-uniform
+  const bool use_bloom = n_unres <= kBloomMaxIds;  // grid-uniform
   for (int i = threadIdx.x; i < kBloomWords; i += blockDim.x) bloom[i] = 0;
   __syncthreads();
-  for (unsigned i = threadIdx.x; i < n_unres; i += blockDim.x) {
+  for (unsigned i = threadIdx.x; use_bloom && i < n_unres; i += blockDim.x) {
     const uint32_t h = bloom_hash(unres_list[i]);
-    atomicOr(bloom + (h & (kBloomWords - 1)), bloom_bits(h));
+    atomicOr(bloom + bloom_word(h), bloom_bits(h));
   }
   __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  unsigned long long* const wq = queue[threadIdx.x >> 6];
+  int qn = 0;  // wave-uniform queue length
+  // the wave's positives (`pos` on the active lanes) into its queue; 64 out
+  auto enqueue = [&](bool pos, int64_t u, int64_t i) {
+    const unsigned long long m = __ballot(pos);
+    if (m == 0) return;  // wave-uniform
+    if (pos) wq[qn + __popcll(m & below)] = ((unsigned long long)u << 32) | (unsigned long long)(uint32_t)i;
+    qn += __popcll(m);
+    if (qn >= 64) {
+      wave_lds_fence();
+      const unsigned long long e = wq[lane];
+      unsigned base = 0;
+      if (lane == 0) base = atomicAdd(sctl + 1, 64u);
+      base = __shfl(base, 0, 64);
+      fix_rec[base + lane] = e;
+      const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
+      wave_lds_fence();
+      if (lane + 64 < qn) wq[lane] = rest;
+      qn -= 64;
+      wave_lds_fence();
+    }
+  };
   constexpr int KU = 8;  // 16-byte loads (two rows) per lane and iteration
   const int64_t per_iter = (int64_t)blockDim.x * KU;  // row pairs per block iteration
   const int64_t n_iters = VEC ? (kp.n / 2) / per_iter : 0;
   const longlong2* __restrict__ pv = reinterpret_cast<const longlong2*>(pid);
-  int64_t it = blockIdx.x;
-  if (it < n_iters) {
-    longlong2 cur[KU], nxt[KU];
+  auto run = [&](auto bloom_tag) {
+    constexpr bool BLOOM = decltype(bloom_tag)::value;
+    int64_t it = blockIdx.x;
+    if (it < n_iters) {
+      longlong2 cur[KU], nxt[KU];
 #pragma unroll
-    for (int v = 0; v < KU; ++v) cur[v] = pv[it * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
-    for (; it < n_iters; it += gridDim.x) {  // block-uniform trips
-      const int64_t nx = it + gridDim.x < n_iters ? it + gridDim.x : it;  // in range: no branch around the loads
+      for (int v = 0; v < KU; ++v) cur[v] = pv[it * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
+      for (; it < n_iters; it += gridDim.x) {  // block-uniform trips
+        const int64_t nx = it + gridDim.x < n_iters ? it + gridDim.x : it;  // in range: no branch around the loads
 #pragma unroll
-      for (int v = 0; v < KU; ++v) nxt[v] = pv[nx * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
+        for (int v = 0; v < KU; ++v) nxt[v] = pv[nx * per_iter + (int64_t)v * blockDim.x + threadIdx.x];
+        unsigned maybe = 0;
 #pragma unroll
-      for (int v = 0; v < KU; ++v) {
-        const int64_t i = 2 * (it * per_iter + (int64_t)v * blockDim.x + threadIdx.x);
-        rescan_emit(kp, cur[v].x, i, bloom, unres_bits, sctl, fix_cnt, fix_rec);
-        rescan_emit(kp, cur[v].y, i + 1, bloom, unres_bits, sctl, fix_cnt, fix_rec);
+        for (int v = 0; v < KU; ++v) {
+          maybe |= (unsigned)rescan_maybe<BLOOM>(kp, cur[v].x, bloom, unres_bits) << (2 * v);
+          maybe |= (unsigned)rescan_maybe<BLOOM>(kp, cur[v].y, bloom, unres_bits) << (2 * v + 1);
+        }
+        if (__ballot(maybe != 0) != 0) {  // wave-uniform, ~1 in 2 wave iterations at C3
+#pragma unroll
+          for (int v = 0; v < KU; ++v) {
+            const int64_t i = 2 * (it * per_iter + (int64_t)v * blockDim.x + threadIdx.x);
+            enqueue((maybe >> (2 * v)) & 1u, cur[v].x, i);
+            enqueue((maybe >> (2 * v + 1)) & 1u, cur[v].y, i + 1);
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < KU; ++v) cur[v] = nxt[v];
       }
-#pragma unroll
-      for (int v = 0; v < KU; ++v) cur[v] = nxt[v];
     }
+    // the rows no full iteration covered (all of them without VEC): every lane
+    // of a wave runs the same trip count, so the queue stays wave-uniform
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = 2 * n_iters * per_iter + (int64_t)blockIdx.x * blockDim.x;
+    for (int64_t w0 = i0 + (int64_t)(threadIdx.x & ~63); w0 < kp.n; w0 += stride) {  // w0: the wave's first row
+      const int64_t i = w0 + lane;
+      const int64_t u = i < kp.n ? pid[i] : -1;
+      enqueue(i < kp.n && rescan_maybe<BLOOM>(kp, u, bloom, unres_bits), u, i);
+    }
+  };
+  if (use_bloom) run(std::true_type{});
+  else run(std::false_type{});
+  // the rest of the queue
+  wave_lds_fence();
+  if (qn > 0) {
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(sctl + 1, (unsigned)qn);
+    base = __shfl(base, 0, 64);
+    if (lane < qn) fix_rec[base + lane] = wq[lane];
   }
-  // the rows no full iteration covered (all of them without VEC)
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = 2 * n_iters * per_iter + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < kp.n; i += stride)
-    rescan_emit(kp, pid[i], i, bloom, unres_bits, sctl, fix_cnt, fix_rec);
+}
+
+// Fix-up step 1b: the exact test of every listed row (the bitmap of the
+// unresolved ids); a false positive's entry becomes ~0 (skipped by
+// k_fix_scatter), a true one is counted for its bucket.
+__global__ void __launch_bounds__(kBlock) k_fix_filter(KP kp, const unsigned* __restrict__ unres_bits,
+                                                       const unsigned* __restrict__ sctl,
+                                                       unsigned long long* __restrict__ fix_rec,
+                                                       unsigned* __restrict__ fix_cnt) {
+  const int64_t total = sctl[1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t u = fix_rec[i] >> 32;
+    if ((unres_bits[u >> 5] >> (u & 31)) & 1u) atomicAdd(fix_cnt + (u >> kp.bucket_bits), 1u);
+    else fix_rec[i] = ~0ULL;
+  }
 }
 
 // Fix-up step 2: the listed rows -> bucket order (fix_start = exclusive scan
@@ -2227,6 +2404,7 @@ __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __
   const uint64_t lmask = ((uint64_t)1 << kp.bucket_bits) - 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t e = fix_rec[i];
+    if (e == ~0ULL) continue;  // a Bloom false positive (k_fix_filter)
     const uint64_t u = e >> 32;
     const uint32_t r = (uint32_t)e;
     const int64_t k = pk[r];
@@ -2874,13 +3052,16 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
   PDP_PROF_BEGIN("k_sieve_rescan", st);
   if (kp.keys_vec)
-    hipLaunchKernelGGL(k_sieve_rescan<true>, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
-                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
-                       fix_rec);
+    hipLaunchKernelGGL(k_sieve_rescan<true>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid,
+                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_rec);
   else
-    hipLaunchKernelGGL(k_sieve_rescan<false>, dim3(512), dim3(kRescanThreads), 0, st, kp, pid,
-                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_cnt,
-                       fix_rec);
+    hipLaunchKernelGGL(k_sieve_rescan<false>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid,
+                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_rec);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  PDP_PROF_BEGIN("k_fix_filter", st);
+  hipLaunchKernelGGL(k_fix_filter, dim3(grid_for(kp.n, 1024)), dim3(kBlock), 0, st, kp,
+                     (const unsigned*)(ws + w.unres_bits), (const unsigned*)sctl, fix_rec, fix_cnt);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   rc = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts

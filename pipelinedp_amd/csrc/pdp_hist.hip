@@ -78,8 +78,41 @@ uint64_t slots_capacity(int64_t n_rows, int64_t P) {
 }
 
 struct HWs {
-  uint64_t err, slots, rbase, rchunks, pidstat, pkstat, psum, minmax, fmax, total;
+  uint64_t err, slots, rbase, rchunks, pidstat, pkstat, psum, minmax, fmax;
+  // bucketed pairs (hb_*): per (tile, super-bucket) row counts -> offsets,
+  // super-bucket bases, rows per pair bucket -> starts (+ scan scratch), write
+  // cursors, the pair sums, {mode, pairs, overflow}; the level-1 / level-2
+  // records reuse the pair-table region
+  uint64_t hb_cts, hb_sbase, hb_bcnt, hb_bchunks, hb_bcur, hb_pairsum, hb_ctl;
+  uint64_t total;
 };
+
+// ---- bucketed pairs (the raw-row pairs phase) -------
+// Rows are partitioned by a hash of their (privacy id, partition) pair into
+// NB pair buckets (two LDS counting-sort levels: <= 256 super-buckets of <=
+// 256 buckets), and one workgroup per bucket finds the bucket's distinct
+// pairs in an LDS hash table: no pair table in HBM, no global CAS.  A bucket
+// holds ~kHbRowsPerBucket rows, an upper bound of its pairs, so its table
+// (kHbSlots) stays at most ~60 % full; a table that would pass kHbFill falls
+// back to the pair-table path for the whole call (never for hashed real data).
+constexpr int kHbTileRows = 65536;
+constexpr int kHbThreads = 1024;         // count / level-1 workgroups
+constexpr int kHbStage = 8192;           // level-1 rows per LDS stage (8 per thread)
+constexpr int kHbFan = 256;              // buckets per super-bucket
+constexpr int kHbL2Threads = 512;
+constexpr int kHbWin = 4096;             // level-2 records per window (8 per thread)
+constexpr int kHbK = 8;                  // level-2 workgroups per super-bucket
+constexpr int kHbSlots = 3072;           // LDS pair table per bucket
+constexpr int kHbFill = 2760;            // 90 % of kHbSlots: more distinct pairs -> fallback
+constexpr int64_t kHbRowsPerBucket = 1536;
+constexpr int64_t kHbMaxBuckets = (int64_t)kHbFan * 256;
+constexpr int kHbPairThreads = 512;
+
+inline int64_t hb_buckets(int64_t n) {
+  const int64_t nb = (n + kHbRowsPerBucket - 1) / kHbRowsPerBucket;
+  return nb < 1 ? 1 : nb;
+}
+inline bool hb_eligible(int64_t n) { return n > 0 && hb_buckets(n) <= kHbMaxBuckets; }
 
 // err first: pdp_bound_error_flags reads the error word at offset 0
 HWs hlayout(int64_t n, int64_t U, int64_t P) {
@@ -98,6 +131,18 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
   w.psum = off; off = align256(off + (uint64_t)P * 8);
   w.minmax = off; off = align256(off + 4 * 8);        // ordered u64: pair min, max; partition min, max
   w.fmax = off; off = align256(off + 2 * kSumBuckets * 8);  // ordered u64 bin maxima
+  if (hb_eligible(n)) {
+    const int64_t nb = hb_buckets(n);
+    const int64_t ns = (nb + kHbFan - 1) / kHbFan;
+    const int64_t nt = (n + kHbTileRows - 1) / kHbTileRows;
+    w.hb_cts = off; off = align256(off + (uint64_t)(nt * ns) * 4);
+    w.hb_sbase = off; off = align256(off + (uint64_t)(ns + 1) * 4);
+    w.hb_bcnt = off; off = align256(off + (uint64_t)(nb + 1) * 4);
+    w.hb_bchunks = off; off = align256(off + (uint64_t)scan_chunk_sums_len(nb + 1) * 4);
+    w.hb_bcur = off; off = align256(off + (uint64_t)nb * 4);
+    w.hb_pairsum = off; off = align256(off + (uint64_t)n * 8);
+  }
+  w.hb_ctl = off; off = align256(off + 16);  // {mode (1 = bucketed), pairs, overflow}
   w.total = off;
   return w;
 }
@@ -107,6 +152,7 @@ struct HT {
   int pk_bits, has_value, do_parts;  // do_parts: per-partition histograms (multi-rank: one rank)
   uint64_t cap, pk_mask;             // cap: allocated slots (regions use a prefix of them)
   int64_t R;                         // regions
+  int64_t nb, n_supers, n_tiles;     // bucketed pairs: pair buckets, super-buckets, tiles
 };
 
 // order-preserving u64 image of an fp64 (for atomicMin/atomicMax)
@@ -418,6 +464,8 @@ constexpr int kFloatBlock = 1024;
 // pair sums: counts and sums in LDS (one workgroup per CU, 16 waves), flushed
 // once; partition sums (P elements): global atomics
 __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
+                                                         const double* __restrict__ pairsum,
+                                                         const unsigned* __restrict__ hb_ctl,
                                                          const unsigned long long* __restrict__ pkstat,
                                                          const double* __restrict__ psum,
                                                          const double* __restrict__ lowers,
@@ -432,7 +480,16 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
   const int64_t C = (int64_t)t.cap;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
-  if (nl0 > 0) {
+  if (nl0 > 0 && hb_ctl[0] == 1) {  // the bucketed path's list of pair sums
+    const int64_t np = hb_ctl[1];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += stride) {
+      const double v = pairsum[i];
+      const int b = float_bin(lowers, nl0, v);
+      atomicAdd(lcnt + b, 1u);
+      atomicAdd(lsum + b, v);
+      max_filtered(F.omax + b, ord(v));
+    }
+  } else if (nl0 > 0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += stride) {
       const Slot sl = slots[i];
       if (sl.key == 0) continue;
@@ -482,6 +539,356 @@ __global__ void __launch_bounds__(kBlock) k_h_final(IntHists H, FloatHists F, do
 // min images all ones, max images zero
 __global__ void k_h_init(unsigned long long* minmax) {
   if (threadIdx.x < 4) minmax[threadIdx.x] = (threadIdx.x & 1) ? 0ULL : ~0ULL;
+}
+
+// ------------------------------------------------------- bucketed pairs ----
+// pair bucket of a (privacy id << pk_bits | partition) key: the high half of
+// SplitMix64(key), scaled to [0, nb)
+__device__ __forceinline__ unsigned hb_bucket(unsigned long long x, int64_t nb) {
+  return (unsigned)(((mix64(x ^ 0x2545F4914F6CDD1DULL) >> 32) * (uint64_t)nb) >> 32);
+}
+
+// exclusive scan of one u32 per thread over the workgroup (wsum: nw + 1 words)
+__device__ __forceinline__ unsigned hb_block_scan(unsigned x, unsigned* wsum, unsigned* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  unsigned inc = x;
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned y = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    const unsigned v = lane < nw ? wsum[lane] : 0;
+    unsigned vi = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned y = __shfl_up(vi, off, 64);
+      if (lane >= off) vi += y;
+    }
+    if (lane < nw) wsum[lane] = vi - v;
+    if (lane == nw - 1) wsum[nw] = vi;
+  }
+  __syncthreads();
+  const unsigned r = wsum[w] + inc - x;
+  *total = wsum[nw];
+  __syncthreads();
+  return r;
+}
+
+// step 1: valid rows per (tile, super-bucket); invalid keys set the error word
+__global__ void __launch_bounds__(kHbThreads) k_hb_count(HT t, const int64_t* __restrict__ pid,
+                                                         const int64_t* __restrict__ pk, unsigned* __restrict__ cts,
+                                                         unsigned* err) {
+  __shared__ unsigned h[kHbFan];
+  for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const int64_t t0 = (int64_t)blockIdx.x * kHbTileRows;
+  const int64_t t1 = t0 + kHbTileRows < t.n ? t0 + kHbTileRows : t.n;
+  bool bad = false;
+  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    const int64_t u = pid[i], k = pk[i];
+    if ((uint64_t)u >= (uint64_t)t.U || (uint64_t)k >= (uint64_t)t.P) {
+      bad = true;
+      continue;
+    }
+    atomicAdd(h + hb_bucket(((uint64_t)u << t.pk_bits) | (uint64_t)k, t.nb) / kHbFan, 1u);
+  }
+  if (bad) atomicOr(err, 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x) cts[(int64_t)blockIdx.x * t.n_supers + b] = h[b];
+}
+
+// step 2: per super-bucket, the tiles' counts -> offsets (in place, exclusive,
+// tile order) and the super-bucket's total
+__global__ void __launch_bounds__(kHbThreads) k_hb_scan_tiles(HT t, unsigned* __restrict__ cts,
+                                                              unsigned* __restrict__ stotal) {
+  __shared__ unsigned wsum[kHbThreads / 64 + 1];
+  const int s = blockIdx.x;
+  unsigned carry = 0;
+  for (int64_t c = 0; c < t.n_tiles; c += blockDim.x) {  // block-uniform
+    const int64_t tt = c + threadIdx.x;
+    const unsigned v = tt < t.n_tiles ? cts[tt * t.n_supers + s] : 0u;
+    unsigned tot;
+    const unsigned ex = hb_block_scan(v, wsum, &tot);
+    if (tt < t.n_tiles) cts[tt * t.n_supers + s] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) stotal[s] = carry;
+}
+
+// super-bucket totals -> bases (in place; sbase[n_supers] = valid rows)
+__global__ void __launch_bounds__(kHbFan) k_hb_scan_supers(HT t, unsigned* __restrict__ sbase) {
+  __shared__ unsigned wsum[kHbFan / 64 + 1];
+  const unsigned v = (int)threadIdx.x < t.n_supers ? sbase[threadIdx.x] : 0u;
+  unsigned tot;
+  const unsigned ex = hb_block_scan(v, wsum, &tot);
+  if ((int)threadIdx.x < t.n_supers) sbase[threadIdx.x] = ex;
+  if (threadIdx.x == 0) sbase[t.n_supers] = tot;
+}
+
+// step 3: each tile's valid rows -> its super-buckets' regions (tile order
+// within a region), as (key, value) records; LDS counting sort per stage
+template <int VK>
+__global__ void __launch_bounds__(kHbThreads) k_hb_l1(HT t, const int64_t* __restrict__ pid,
+                                                      const int64_t* __restrict__ pk, const void* __restrict__ value,
+                                                      const unsigned* __restrict__ cts,
+                                                      const unsigned* __restrict__ sbase,
+                                                      unsigned long long* __restrict__ okey, double* __restrict__ oval) {
+  extern __shared__ unsigned long long hb_lds[];
+  unsigned long long* skey = hb_lds;                       // [kHbStage]
+  double* sval = (double*)(skey + kHbStage);               // [kHbStage] (VK != NONE)
+  unsigned* hist = (unsigned*)(sval + (VK != PDP_VALUE_NONE ? kHbStage : 0));  // [kHbFan]
+  unsigned* start = hist + kHbFan;                         // [kHbFan]
+  unsigned* cur = start + kHbFan;                          // [kHbFan]: the tile's output cursor per super
+  uint8_t* dest = (uint8_t*)(cur + kHbFan);                // [kHbStage]
+  constexpr int N = kHbStage / kHbThreads;
+  const int64_t t0 = (int64_t)blockIdx.x * kHbTileRows;
+  const int64_t t1 = t0 + kHbTileRows < t.n ? t0 + kHbTileRows : t.n;
+  for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x)
+    cur[b] = sbase[b] + cts[(int64_t)blockIdx.x * t.n_supers + b];
+  for (int64_t c0 = t0; c0 < t1; c0 += kHbStage) {
+    for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    unsigned long long x[N];
+    double v[N];
+    int d[N];
+    unsigned rank[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int64_t i = c0 + (int64_t)q * blockDim.x + threadIdx.x;
+      d[q] = -1;
+      x[q] = 0;
+      v[q] = 0.0;
+      if (i >= t1) continue;
+      const int64_t u = pid[i], k = pk[i];
+      if ((uint64_t)u >= (uint64_t)t.U || (uint64_t)k >= (uint64_t)t.P) continue;  // flagged by k_hb_count
+      x[q] = ((uint64_t)u << t.pk_bits) | (uint64_t)k;
+      if (VK == PDP_VALUE_F64) v[q] = ((const double*)value)[i];
+      if (VK == PDP_VALUE_I64) v[q] = (double)((const long long*)value)[i];
+      d[q] = (int)(hb_bucket(x[q], t.nb) / kHbFan);
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) rank[q] = d[q] >= 0 ? atomicAdd(hist + d[q], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of hist by one wave
+      const int lane = threadIdx.x;
+      unsigned carry = 0;
+      for (int base = 0; base < t.n_supers; base += 64) {
+        const unsigned hv = base + lane < t.n_supers ? hist[base + lane] : 0u;
+        unsigned incl = hv;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned up = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += up;
+        }
+        if (base + lane < t.n_supers) start[base + lane] = carry + incl - hv;
+        carry += __shfl(incl, 63, 64);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      if (d[q] < 0) continue;
+      const unsigned slot = start[d[q]] + rank[q];
+      skey[slot] = x[q];
+      if (VK != PDP_VALUE_NONE) sval[slot] = v[q];
+      dest[slot] = (uint8_t)d[q];
+    }
+    __syncthreads();
+    const unsigned total = t.n_supers > 0 ? start[t.n_supers - 1] + hist[t.n_supers - 1] : 0u;
+    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) {
+      const unsigned dd = dest[e];
+      const unsigned g = cur[dd] + (e - start[dd]);
+      okey[g] = skey[e];
+      if (VK != PDP_VALUE_NONE) oval[g] = sval[e];
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x) cur[b] += hist[b];
+  }
+}
+
+size_t hb_l1_lds(int vk) {
+  return (size_t)kHbStage * (8 + (vk != PDP_VALUE_NONE ? 8 : 0) + 1) + 3 * kHbFan * 4;
+}
+
+// step 4: rows per pair bucket -- workgroup (s, k) counts windows k, k + K, ...
+// of super-bucket s's region in LDS, one atomic per (workgroup, bucket)
+__global__ void __launch_bounds__(kHbL2Threads) k_hb_bcount(HT t, const unsigned* __restrict__ sbase,
+                                                            const unsigned long long* __restrict__ key,
+                                                            unsigned* __restrict__ bcnt) {
+  __shared__ unsigned h[kHbFan];
+  const int s = blockIdx.x / kHbK, k = blockIdx.x % kHbK;
+  for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const int64_t a = sbase[s], e = sbase[s + 1];
+  for (int64_t w0 = a + (int64_t)k * kHbWin; w0 < e; w0 += (int64_t)kHbK * kHbWin) {
+    const int64_t w1 = w0 + kHbWin < e ? w0 + kHbWin : e;
+    for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) atomicAdd(h + hb_bucket(key[i], t.nb) % kHbFan, 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) {
+    const int64_t g = (int64_t)s * kHbFan + b;
+    if (h[b] && g < t.nb) atomicAdd(bcnt + g, h[b]);
+  }
+}
+
+// step 5: super-bucket windows -> pair buckets: LDS counting sort by bucket,
+// one cursor atomic per (window, bucket) run
+template <bool HAS_VALUE>
+__global__ void __launch_bounds__(kHbL2Threads) k_hb_l2(HT t, const unsigned* __restrict__ sbase,
+                                                        const unsigned long long* __restrict__ ikey,
+                                                        const double* __restrict__ ival,
+                                                        const unsigned* __restrict__ bstart,
+                                                        unsigned* __restrict__ bcur,
+                                                        unsigned long long* __restrict__ okey,
+                                                        double* __restrict__ oval) {
+  __shared__ unsigned long long skey[kHbWin];
+  __shared__ double sval[HAS_VALUE ? kHbWin : 1];
+  __shared__ uint8_t dest[kHbWin];
+  __shared__ unsigned hist[kHbFan], start[kHbFan], base[kHbFan];
+  constexpr int N = kHbWin / kHbL2Threads;
+  const int s = blockIdx.x / kHbK, k = blockIdx.x % kHbK;
+  const int64_t a = sbase[s], e = sbase[s + 1];
+  for (int64_t w0 = a + (int64_t)k * kHbWin; w0 < e; w0 += (int64_t)kHbK * kHbWin) {  // block-uniform
+    const int64_t w1 = w0 + kHbWin < e ? w0 + kHbWin : e;
+    for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) hist[b] = 0;
+    __syncthreads();
+    unsigned long long x[N];
+    double v[N];
+    int d[N];
+    unsigned rank[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int64_t i = w0 + (int64_t)q * blockDim.x + threadIdx.x;
+      d[q] = -1;
+      x[q] = 0;
+      v[q] = 0.0;
+      if (i < w1) {
+        x[q] = ikey[i];
+        if (HAS_VALUE) v[q] = ival[i];
+        d[q] = (int)(hb_bucket(x[q], t.nb) % kHbFan);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) rank[q] = d[q] >= 0 ? atomicAdd(hist + d[q], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      unsigned carry = 0;
+      for (int b0 = 0; b0 < kHbFan; b0 += 64) {
+        const unsigned hv = hist[b0 + lane];
+        unsigned incl = hv;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned up = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += up;
+        }
+        start[b0 + lane] = carry + incl - hv;
+        carry += __shfl(incl, 63, 64);
+      }
+    }
+    // one cursor reservation per non-empty run of this window
+    for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) {
+      const int64_t g = (int64_t)s * kHbFan + b;
+      base[b] = (hist[b] && g < t.nb) ? bstart[g] + atomicAdd(bcur + g, hist[b]) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      if (d[q] < 0) continue;
+      const unsigned slot = start[d[q]] + rank[q];
+      skey[slot] = x[q];
+      if (HAS_VALUE) sval[slot] = v[q];
+      dest[slot] = (uint8_t)d[q];
+    }
+    __syncthreads();
+    const unsigned total = (unsigned)(w1 - w0);
+    for (unsigned i = threadIdx.x; i < total; i += blockDim.x) {
+      const unsigned dd = dest[i];
+      const unsigned g = base[dd] + (i - start[dd]);
+      okey[g] = skey[i];
+      if (HAS_VALUE) oval[g] = sval[i];
+    }
+    __syncthreads();
+  }
+}
+
+// step 6: one workgroup per pair bucket: its distinct pairs in an LDS hash
+// table (key, rows, value sum), then per pair exactly what k_h_pairs does
+// per table slot: per pid and per partition (distinct << 32 | rows) and value
+// sums, the Linf histogram, the pair sums' min / max, and the pair sum into
+// the compact list k_h_float bins.  More than kHbFill distinct pairs in one
+// bucket: the overflow word is set and the call falls back.
+template <bool HAS_VALUE>
+__global__ void __launch_bounds__(kHbPairThreads) k_hb_pairs(HT t, const unsigned* __restrict__ bstart,
+                                                             const unsigned long long* __restrict__ key,
+                                                             const double* __restrict__ val,
+                                                             unsigned long long* pidstat, unsigned long long* pkstat,
+                                                             double* psum, IntHists H, unsigned long long* minmax,
+                                                             double* __restrict__ pairsum, unsigned* ctl) {
+  __shared__ unsigned long long tkey[kHbSlots];
+  __shared__ unsigned tcnt[kHbSlots];
+  __shared__ double tsum[HAS_VALUE ? kHbSlots : 1];
+  __shared__ unsigned lds[kSmallBins];
+  __shared__ unsigned fill, s_base;
+  for (int i = threadIdx.x; i < kHbSlots; i += blockDim.x) {
+    tkey[i] = ~0ULL;
+    tcnt[i] = 0;
+    if (HAS_VALUE) tsum[i] = 0.0;
+  }
+  for (int b = threadIdx.x; b < kSmallBins; b += blockDim.x) lds[b] = 0;
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  const int64_t a = bstart[blockIdx.x], e = bstart[blockIdx.x + 1];
+  bool over = false;
+  for (int64_t i = a + threadIdx.x; i < e; i += blockDim.x) {
+    const unsigned long long x = key[i];
+    unsigned sl = (unsigned)(((mix64(x) & 0xFFFFFFFFULL) * (uint64_t)kHbSlots) >> 32);
+    for (;;) {
+      const unsigned long long cur = tkey[sl];
+      if (cur == x) break;
+      if (cur == ~0ULL) {
+        if (atomicAdd(&fill, 1u) >= (unsigned)kHbFill) {  // table too full: fall back
+          over = true;
+          break;
+        }
+        const unsigned long long old = atomicCAS(tkey + sl, ~0ULL, x);
+        if (old == ~0ULL) break;
+        atomicSub(&fill, 1u);  // lost the slot to another key
+        if (old == x) break;
+      }
+      sl = sl + 1 == (unsigned)kHbSlots ? 0u : sl + 1;
+    }
+    if (over) break;
+    atomicAdd(tcnt + sl, 1u);
+    if (HAS_VALUE) atomicAdd(tsum + sl, val[i]);
+  }
+  if (over) atomicOr(ctl + 2, 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s_base = atomicAdd(ctl + 1, fill);  // this bucket's pair sums
+    fill = 0;
+  }
+  __syncthreads();
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+  for (int j = threadIdx.x; j < kHbSlots; j += blockDim.x) {
+    const unsigned long long x = tkey[j];
+    const unsigned rows = tcnt[j];
+    if (x == ~0ULL || rows == 0) continue;
+    const double sum = HAS_VALUE ? tsum[j] : 0.0;
+    const unsigned long long inc = (1ULL << 32) | rows;
+    atomicAdd(pidstat + (x >> t.pk_bits), inc);
+    const uint64_t p = x & t.pk_mask;
+    atomicAdd(pkstat + p, inc);
+    if (HAS_VALUE) atomicAdd(psum + p, sum);
+    int_hist_add(H, lds, H_LINF, 0, rows);
+    const unsigned long long o = ord(sum);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+    const unsigned long long at = (unsigned long long)s_base + atomicAdd(&fill, 1u);
+    if (at < (unsigned long long)t.n) pairsum[at] = sum;  // (an overflowed call is discarded)
+  }
+  block_minmax(mn, mx, minmax);  // contains __syncthreads
+  __syncthreads();
+  flush_small(H, lds, 0, H_LINF);
 }
 
 // ------------------------------------------------------ pre-aggregated input --
@@ -770,6 +1177,7 @@ int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_
     return set_error(PDP_E_INVALID, "every pdp_histogram_bins output must be set");
   if (n_rows < 0 || n_privacy_ids < 0 || n_partitions < 0) return set_error(PDP_E_INVALID, "sizes must be >= 0");
   if (n_rows >= (int64_t)1 << 31) return set_error(PDP_E_UNSUPPORTED, "n_rows must be < 2^31 per shard");
+  value_kind &= ~PDP_HIST_FORCE_PAIR_TABLE;
   if (value_kind != PDP_VALUE_NONE && value_kind != PDP_VALUE_F64 && value_kind != PDP_VALUE_I64)
     return set_error(PDP_E_INVALID, "bad value_kind");
   if (bits_for(n_privacy_ids) + bits_for(n_partitions) > 63)
@@ -789,9 +1197,83 @@ int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_
   t.has_value = value_kind != PDP_VALUE_NONE;
   t.do_parts = 1;
   t.pk_mask = (1ULL << t.pk_bits) - 1;
+  t.nb = hb_buckets(n_rows);
+  t.n_supers = (t.nb + kHbFan - 1) / kHbFan;
+  t.n_tiles = (n_rows + kHbTileRows - 1) / kHbTileRows;
   c->H = IntHists{(unsigned long long*)out->int_count, (unsigned long long*)out->int_sum,
                   (unsigned long long*)out->int_max};
   c->F = FloatHists{(unsigned long long*)out->float_count, out->float_sum, (unsigned long long*)(c->ws + c->w.fmax)};
+  return PDP_OK;
+}
+
+// the bucketed pairs phase (k_hb_*): pair-hash partition in two levels, then
+// one LDS pair table per bucket; sets hb_ctl = {1, pairs, overflow}
+int hist_pairs_bucketed(const HCall& c, const int64_t* privacy_id, const int64_t* partition, const void* value,
+                        int32_t value_kind) {
+  const HWs& w = c.w;
+  const HT& t = c.t;
+  char* ws = c.ws;
+  hipStream_t st = c.st;
+  unsigned* err = (unsigned*)(ws + w.err);
+  unsigned* cts = (unsigned*)(ws + w.hb_cts);
+  unsigned* sbase = (unsigned*)(ws + w.hb_sbase);
+  unsigned* bcnt = (unsigned*)(ws + w.hb_bcnt);
+  unsigned* bcur = (unsigned*)(ws + w.hb_bcur);
+  unsigned* ctl = (unsigned*)(ws + w.hb_ctl);
+  // level-1 and level-2 records in the pair-table region (>= 48 bytes per row)
+  unsigned long long* key1 = (unsigned long long*)(ws + w.slots);
+  double* val1 = (double*)(key1 + t.n);
+  unsigned long long* key2 = (unsigned long long*)(val1 + t.n);
+  double* val2 = (double*)(key2 + t.n);
+  const bool hv = value_kind != PDP_VALUE_NONE;
+  PDP_HLAUNCH("k_hb_count", st, k_hb_count, dim3((unsigned)t.n_tiles), dim3(kHbThreads), 0, st, t, privacy_id,
+              partition, cts, err);
+  PDP_HLAUNCH("k_hb_scan_tiles", st, k_hb_scan_tiles, dim3((unsigned)t.n_supers), dim3(kHbThreads), 0, st, t, cts,
+              sbase);
+  PDP_HLAUNCH("k_hb_scan_supers", st, k_hb_scan_supers, dim3(1), dim3(kHbFan), 0, st, t, sbase);
+  const size_t lds1 = hb_l1_lds(value_kind);
+  const void* l1 = value_kind == PDP_VALUE_F64 ? (const void*)k_hb_l1<PDP_VALUE_F64>
+                   : value_kind == PDP_VALUE_I64 ? (const void*)k_hb_l1<PDP_VALUE_I64>
+                                                 : (const void*)k_hb_l1<PDP_VALUE_NONE>;
+  PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+  {
+    const HT tt = t;
+    const unsigned* cts_c = cts;
+    const unsigned* sbase_c = sbase;
+    void* args[] = {(void*)&tt, (void*)&privacy_id, (void*)&partition, (void*)&value, (void*)&cts_c,
+                    (void*)&sbase_c, (void*)&key1, (void*)&val1};
+    PDP_PROF_BEGIN("k_hb_l1", st);
+    PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)t.n_tiles), dim3(kHbThreads), args, lds1, st));
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+  }
+  PDP_HIP_CHECK(hipMemsetAsync(bcnt, 0, (uint64_t)(t.nb + 1) * 4, st));
+  PDP_HIP_CHECK(hipMemsetAsync(bcur, 0, (uint64_t)t.nb * 4, st));
+  const unsigned g2 = (unsigned)(t.n_supers * kHbK);
+  PDP_HLAUNCH("k_hb_bcount", st, k_hb_bcount, dim3(g2), dim3(kHbL2Threads), 0, st, t, (const unsigned*)sbase,
+              (const unsigned long long*)key1, bcnt);
+  const int rc = scan_u32(bcnt, t.nb, (unsigned*)(ws + w.hb_bchunks), st);  // -> bucket starts
+  if (rc != PDP_OK) return rc;
+  if (hv)
+    PDP_HLAUNCH("k_hb_l2", st, k_hb_l2<true>, dim3(g2), dim3(kHbL2Threads), 0, st, t, (const unsigned*)sbase,
+                (const unsigned long long*)key1, (const double*)val1, (const unsigned*)bcnt, bcur, key2, val2);
+  else
+    PDP_HLAUNCH("k_hb_l2", st, k_hb_l2<false>, dim3(g2), dim3(kHbL2Threads), 0, st, t, (const unsigned*)sbase,
+                (const unsigned long long*)key1, (const double*)val1, (const unsigned*)bcnt, bcur, key2, val2);
+  PDP_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)ctl, 1u, 1, st));  // mode: bucketed
+  unsigned long long* pidstat = (unsigned long long*)(ws + w.pidstat);
+  unsigned long long* pkstat = (unsigned long long*)(ws + w.pkstat);
+  double* psum = (double*)(ws + w.psum);
+  unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
+  double* pairsum = (double*)(ws + w.hb_pairsum);
+  if (hv)
+    PDP_HLAUNCH("k_hb_pairs", st, k_hb_pairs<true>, dim3((unsigned)t.nb), dim3(kHbPairThreads), 0, st, t,
+                (const unsigned*)bcnt, (const unsigned long long*)key2, (const double*)val2, pidstat, pkstat, psum,
+                c.H, minmax, pairsum, ctl);
+  else
+    PDP_HLAUNCH("k_hb_pairs", st, k_hb_pairs<false>, dim3((unsigned)t.nb), dim3(kHbPairThreads), 0, st, t,
+                (const unsigned*)bcnt, (const unsigned long long*)key2, (const double*)val2, pidstat, pkstat, psum,
+                c.H, minmax, pairsum, ctl);
   return PDP_OK;
 }
 
@@ -803,8 +1285,14 @@ int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partiti
   const HT& t = c.t;
   char* ws = c.ws;
   hipStream_t st = c.st;
+  const bool force_table = (value_kind & PDP_HIST_FORCE_PAIR_TABLE) != 0;
+  value_kind &= ~PDP_HIST_FORCE_PAIR_TABLE;
+  const bool bucketed = !force_table && hb_eligible(t.n);
   PDP_HIP_CHECK(hipMemsetAsync(ws + w.err, 0, 16, st));
-  PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.minmax - w.slots, st));  // slots .. psum
+  // the pair table (slots .. region scan) only for its own path; the per-pid
+  // and per-partition statistics for both
+  if (!bucketed) PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.pidstat - w.slots, st));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.pidstat, 0, w.minmax - w.pidstat, st));  // pidstat .. psum
   PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
   PDP_HIP_CHECK(hipMemsetAsync(ws + w.fmax, 0, 2 * kSumBuckets * 8, st));
   PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
@@ -813,9 +1301,26 @@ int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partiti
   PDP_HIP_CHECK(hipMemsetAsync(out->float_count, 0, 2 * kSumBuckets * 8, st));
   PDP_HIP_CHECK(hipMemsetAsync(out->float_sum, 0, 2 * kSumBuckets * 8, st));
   PDP_HIP_CHECK(hipMemsetAsync(out->float_lowers, 0, 2 * kNLowers * 8, st));
+  PDP_HIP_CHECK(hipMemsetAsync(ws + w.hb_ctl, 0, 16, st));
   if (t.n == 0) return PDP_OK;
   if (privacy_id == nullptr || partition == nullptr || (value_kind != PDP_VALUE_NONE && value == nullptr))
     return set_error(PDP_E_INVALID, "NULL column");
+  if (bucketed) {
+    const int rc = hist_pairs_bucketed(c, privacy_id, partition, value, value_kind);
+    if (rc != PDP_OK) return rc;
+    unsigned over = 0;
+    PDP_HIP_CHECK(hipMemcpyAsync(&over, ws + w.hb_ctl + 8, 4, hipMemcpyDeviceToHost, st));
+    PDP_HIP_CHECK(hipStreamSynchronize(st));
+    if (!over) return PDP_OK;
+    // a bucket's table overflowed (adversarial keys): the pair-table path
+    // from scratch
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.hb_ctl, 0, 16, st));
+    PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
+    PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
+    PDP_HIP_CHECK(hipMemsetAsync(out->int_sum, 0, 5 * kLogBins * 8, st));
+    PDP_HIP_CHECK(hipMemsetAsync(out->int_max, 0, 5 * kLogBins * 8, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.minmax - w.slots, st));  // slots .. psum
+  }
   Slot* slots = (Slot*)(ws + w.slots);
   unsigned* err = (unsigned*)(ws + w.err);
   unsigned* rbase = (unsigned*)(ws + w.rbase);
@@ -874,7 +1379,8 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   int64_t gf = (mf + kFloatBlock - 1) / kFloatBlock;
   gf = gf < cus ? gf : cus;
   PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, (const Slot*)(ws + w.slots),
-              pkstat, psum, out->float_lowers, out->float_n_lowers, c.F);
+              (const double*)(w.hb_pairsum ? ws + w.hb_pairsum : nullptr), (const unsigned*)(ws + w.hb_ctl), pkstat,
+              psum, out->float_lowers, out->float_n_lowers, c.F);
   PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
               c.F, out->float_max, 0x1F);
   return PDP_OK;

@@ -61,11 +61,16 @@ __host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
   return h ^ (h >> 16);
 }
 
-// 32 random bits of the pair (pid, pk) under `seed`: a per-pid hash, then the
-// partition folded in as an odd-multiplier progression (32-bit multiplies only;
-// ties between one pid's pairs, p ~ 2^-32, break by partition).
+// 32 random bits of the pair (pid, pk) under `seed`: a per-pid word (the id
+// keyed by the seed's low half, one odd multiply: a bijection of the id's low
+// 32 bits), then the partition folded in as an odd-multiplier progression and
+// the MurmurHash3 finaliser, which mixes both.  Within one pid distinct
+// partitions (< 2^32) give distinct finaliser inputs, so they never tie.
+// Four 32-bit multiplies per row (quarter rate on gfx950): the level-1 sieve
+// hashes every row.
 __host__ __device__ __forceinline__ uint32_t pid_hash(uint64_t seed, int64_t pid) {
-  return fmix32((uint32_t)pid * 0x9E3779B1U ^ (uint32_t)((uint64_t)pid >> 32) * 0x7FEB352DU ^ (uint32_t)seed);
+  const uint32_t hi = (uint32_t)((uint64_t)pid >> 32);
+  return ((uint32_t)pid ^ ((hi << 16) | (hi >> 16)) ^ (uint32_t)seed) * 0x9E3779B1U;
 }
 
 __host__ __device__ __forceinline__ uint32_t pair_hash_from(uint32_t hpid, uint64_t seed, int64_t pk) {

@@ -28,15 +28,62 @@ def _check_all(got, want, what, exact=False):
         HU.assert_bins_equal(getattr(got, field).bins, want[field], f"{what}/{field}", exact=exact)
 
 
-def _run_codes(pid, pk, val, U=None, P=None):
+def _run_codes(pid, pk, val, U=None, P=None, force_pair_table=False):
     import torch
     d = _dev()
     U = int(pid.max()) + 1 if U is None else U
     P = int(pk.max()) + 1 if P is None else P
     vt = None if val is None else torch.as_tensor(val, device=d)
     raw = X.dataset_histograms(torch.as_tensor(pid, device=d), torch.as_tensor(pk, device=d), vt,
-                               n_privacy_ids=U, n_partitions=P)
+                               n_privacy_ids=U, n_partitions=P, force_pair_table=force_pair_table)
     return CH.histograms_from_device(raw)
+
+
+@pytest.mark.parametrize("case", ["uniform", "zipf_pids", "heavy_pairs", "int_values", "no_values"])
+def test_pair_buckets_and_pair_table_agree_with_oracle(case):
+    """The two pairs phases of pdp_hist.hip -- rows hashed into pair buckets
+    with one LDS table each (default up to ~1e8 rows) and the HBM pair table
+    (PDP_HIST_FORCE_PAIR_TABLE) -- give the oracle's bins; 3e6 rows, so the
+    buckets span two partition levels (1,954 buckets in 8 super-buckets)."""
+    rng = np.random.default_rng({"uniform": 11, "zipf_pids": 12, "heavy_pairs": 13, "int_values": 14,
+                                 "no_values": 15}[case])
+    n = 3_000_000
+    pid = rng.integers(0, 200_000, n)
+    pk = rng.integers(0, 40_000, n)
+    if case == "zipf_pids":    # privacy ids with 10^4..10^6 rows
+        pid = np.minimum(rng.zipf(1.4, n) - 1, 99_999)
+    if case == "heavy_pairs":  # a few pairs with 10^5 rows each (one bucket holds them all)
+        pid[:400_000] = rng.integers(0, 4, 400_000)
+        pk[:400_000] = rng.integers(0, 2, 400_000)
+    val = np.round(rng.normal(1, 3, n) * 8) / 8
+    if case == "int_values":
+        val = rng.integers(-20, 60, n)
+    if case == "no_values":
+        val = None
+    want = OH.dataset_histograms(pid, pk, np.zeros(n) if val is None else val)
+    for force in (False, True):
+        got = _run_codes(pid, pk, val, force_pair_table=force)
+        _check_all(got, want, f"{case}/force={force}", exact=True)
+
+
+def test_pair_bucket_overflow_falls_back():
+    """3,000 distinct pairs that all hash into pair bucket 0 of 2 (crafted with
+    the kernel's bucket hash): more than one LDS table holds (kHbFill = 2,760),
+    so the call redoes the pairs on the HBM pair table -- same bins."""
+    from oracle.columnar import mix64
+    U, P = 5_000, 64
+    cand_pid = np.repeat(np.arange(U, dtype=np.int64), P)
+    cand_pk = np.tile(np.arange(P, dtype=np.int64), U)
+    pk_bits = max(1, int(np.ceil(np.log2(P))))
+    x = (cand_pid.astype(np.uint64) << np.uint64(pk_bits)) | cand_pk.astype(np.uint64)
+    h = (mix64(x ^ np.uint64(0x2545F4914F6CDD1D)) >> np.uint64(32)).astype(np.uint64)
+    b = (h * np.uint64(2)) >> np.uint64(32)
+    pick = np.flatnonzero(b == 0)[:3000]
+    assert len(pick) == 3000
+    pid, pk = cand_pid[pick], cand_pk[pick]
+    val = np.round(np.random.default_rng(7).normal(0, 2, len(pid)) * 4) / 4
+    got = _run_codes(pid, pk, val, U=U, P=P)
+    _check_all(got, OH.dataset_histograms(pid, pk, val), "overflow", exact=True)
 
 
 @pytest.mark.parametrize("fx", HU.fixtures(), ids=lambda f: f["name"])

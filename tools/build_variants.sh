@@ -1,12 +1,12 @@
 #!/bin/bash
-# Builds A/B variants of the library (compile-time knobs) into build/variants/
+# Builds A/B variants of the library (compile-time knobs) into abv/
 # for tools/gpu_variants.sh; the product library is built by __graft_entry__.build().
 set -e
 cd "$(dirname "$0")/.."
-mkdir -p build/variants
+mkdir -p abv
 build() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -munsafe-fp-atomics -I include "${@:2}" \
-    -o build/variants/$1.so pipelinedp_amd/csrc/*.hip
+    -o abv/$1.so pipelinedp_amd/csrc/*.hip
 }
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
@@ -14,4 +14,4 @@ for spec in "$@"; do
   build $name $flags &
 done
 wait
-ls -la build/variants
+ls -la abv

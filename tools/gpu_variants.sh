@@ -1,11 +1,11 @@
 #!/bin/bash
-# Runs the bench once per library variant in build/variants (TAG = $1)
+# Runs the bench once per library variant in abv (TAG = $1)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-variants}
 mkdir -p $OUT
-for so in build/variants/*.so; do
+for so in abv/*.so; do
   v=$(basename $so .so)
   PIPELINEDP_AMD_LIB=$PWD/$so timeout -k 10 240 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/$v.log 2>&1 || { echo "variant $v failed"; tail -5 $OUT/$v.log; exit 1; }
   python3 - $OUT/$v.log $v <<'PY'

@@ -51,11 +51,11 @@ __global__ void __launch_bounds__(256) k_span(const longlong2* __restrict__ p, s
   if (acc == 0x1234567) out[0] = 1;
 }
 
-// C: B + one random LDS probe per row (the rescan's Bloom filter, 64 KiB)
-template <int U>
-__global__ void __launch_bounds__(256) k_span_lds(const longlong2* __restrict__ p, size_t n2, unsigned* out) {
-  __shared__ unsigned bloom[16384];
-  for (int i = threadIdx.x; i < 16384; i += blockDim.x) bloom[i] = i * 2654435761u;
+// C: B + one random LDS probe per row (the rescan's Bloom filter, W words)
+template <int U, int W = 16384>
+__global__ void __launch_bounds__(512) k_span_lds(const longlong2* __restrict__ p, size_t n2, unsigned* out) {
+  __shared__ unsigned bloom[W];
+  for (int i = threadIdx.x; i < W; i += blockDim.x) bloom[i] = i * 2654435761u;
   __syncthreads();
   unsigned acc = 0;
   const size_t per = (n2 + gridDim.x - 1) / gridDim.x;
@@ -67,8 +67,8 @@ __global__ void __launch_bounds__(256) k_span_lds(const longlong2* __restrict__ 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const unsigned h0 = (unsigned)v[u].x * 0x9E3779B1u, h1 = (unsigned)v[u].y * 0x9E3779B1u;
-      acc += bloom[h0 >> 18] & (1u << (h0 & 31));
-      acc += bloom[h1 >> 18] & (1u << (h1 & 31));
+      acc += bloom[(h0 >> 14) & (W - 1)] & (1u << (h0 & 31));
+      acc += bloom[(h1 >> 14) & (W - 1)] & (1u << (h1 & 31));
     }
   }
   if (acc == 0x1234567) out[0] = 1;
@@ -113,9 +113,16 @@ int main() {
   RUN("span U=8 g=2048", k_span<8>, 2048);
   RUN("span U=4 g=8192", k_span<4>, 8192);
   RUN("span U=8 g=1024", k_span<8>, 1024);
-  RUN("span+lds U=4 g=1024", k_span_lds<4>, 1024);
-  RUN("span+lds U=8 g=1024", k_span_lds<8>, 1024);
-  RUN("span+lds U=8 g=2048", k_span_lds<8>, 2048);
+  RUN("span+lds64K U=8 g=1024", k_span_lds<8>, 1024);
+  RUN("span+lds64K U=8 g=2048", k_span_lds<8>, 2048);
+#define RUN2(NAME, KERNEL, GRID, TH)                                                                      \
+  report(NAME, time_it([&] { hipLaunchKernelGGL(KERNEL, dim3(GRID), dim3(TH), 0, 0, p, n2, out); }))
+  RUN2("span+lds16K U=8 g=2048 t256", (k_span_lds<8, 4096>), 2048, 256);
+  RUN2("span+lds16K U=8 g=2048 t512", (k_span_lds<8, 4096>), 2048, 512);
+  RUN2("span+lds8K U=8 g=2048 t256", (k_span_lds<8, 2048>), 2048, 256);
+  RUN2("span+lds8K U=8 g=2048 t512", (k_span_lds<8, 2048>), 2048, 512);
+  RUN2("span+lds4K U=8 g=4096 t256", (k_span_lds<8, 1024>), 4096, 256);
+  RUN2("span+lds8K U=4 g=4096 t256", (k_span_lds<4, 2048>), 4096, 256);
   CHECK(hipFree(p));
   CHECK(hipFree(out));
   return 0;
