@@ -75,8 +75,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--privacy-ids", type=int, default=0,
-                    help="C3 privacy ids in total (default: the config's 1e7); with --rows, one rank's "
-                         "share of an N-GPU run on one GPU")
+                    help="C3: privacy ids in total (default: the config's 1e7; with --rows, one rank's "
+                         "share of an N-GPU run on one GPU); C4 / C5: privacy ids per rank")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5", "hist"), default="c3")
@@ -280,7 +280,7 @@ def run_api_workload(args, workload, world, rank, device):
     from pipelinedp_amd import columnar_backend as CB
     from pipelinedp_amd import executor as X
     w = C4 if workload == "c4" else C5
-    n, U, P = args.rows or w["rows"], w["privacy_ids"], w["partitions"]
+    n, U, P = args.rows or w["rows"], args.privacy_ids or w["privacy_ids"], w["partitions"]
     gen = gen_c4 if workload == "c4" else gen_c5
     pid, pk, value = gen(n, U, P, rank, device, 4000 if workload == "c4" else 5000)
     pid += rank * U  # privacy ids of different ranks are different people

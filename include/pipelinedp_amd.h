@@ -342,12 +342,16 @@ int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uin
  * library zeroes and fills on `stream`; out-of-range keys set the error word
  * that pdp_bound_error_flags reads from this workspace.  n_rows < 2^31.
  * Up to ~1e8 rows the (privacy id, partition) pairs are found by hashing rows
- * into pair buckets, one LDS table per bucket; the call then reads one word
- * back (it synchronizes `stream` once) to confirm no bucket overflowed, and
- * redoes the pairs on an HBM pair table if one did (never for hashed real
- * data).  Larger shards use the HBM pair table directly.  value_kind |
- * PDP_HIST_FORCE_PAIR_TABLE (tests) forces the pair table. */
+ * into buckets, one LDS table per bucket: first by privacy id (every pid's
+ * statistics complete in one workgroup), and if a bucket's distinct pairs do
+ * not fit (privacy ids with thousands of partitions) by (pid, pk) pair; the
+ * call reads one word back after each attempt (it synchronizes `stream`) and
+ * redoes the pairs on an HBM pair table if both overflowed (never for hashed
+ * real data).  Larger shards use the HBM pair table directly.  value_kind |
+ * PDP_HIST_FORCE_PAIR_TABLE (tests) forces the pair table, value_kind |
+ * PDP_HIST_FORCE_PAIR_HASH (tests) skips the privacy-id buckets. */
 #define PDP_HIST_FORCE_PAIR_TABLE 0x100
+#define PDP_HIST_FORCE_PAIR_HASH 0x200
 #define PDP_HIST_LOG_BINS 16384
 #define PDP_HIST_SUM_BUCKETS 10000
 #define PDP_HIST_N_INT 5

@@ -180,6 +180,7 @@ class MetricOp(ctypes.Structure):
 
 HIST_LOG_BINS = 16384
 HIST_FORCE_PAIR_TABLE = 0x100  # tests only: value_kind bit (pipelinedp_amd.h)
+HIST_FORCE_PAIR_HASH = 0x200   # tests only: skip the privacy-id buckets
 HIST_SUM_BUCKETS = 10000
 HIST_N_INT = 5
 HIST_N_FLOAT = 2

@@ -112,11 +112,7 @@ inline bool l1_hist_u16(int key_format, int64_t n_buckets) {
 // second bucket-kernel launch whose pair records follow the main ones.
 // Kept pairs and rows are exactly those of the unsieved path.
 constexpr int kSieveChunkItems = 4;                            // rows per thread and chunk
-#ifndef PDP_AB_L1BUFS
 constexpr int kSieveBufs = 2;  // full tiles: chunks of loads in flight (register buffers)
-#else
-constexpr int kSieveBufs = PDP_AB_L1BUFS;
-#endif
 constexpr int kSieveChunk = kL1Threads * kSieveChunkItems;     // rows filtered per chunk
 constexpr int kSieveCap = 12288;                               // candidate slots of the LDS stage
 constexpr int kSieveItems = kSieveCap / kL1Threads;            // per thread at a flush
@@ -1425,10 +1421,17 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
     __syncthreads();
     // runs per super-bucket, and the tile's candidates per bucket (counted
     // here, on the compacted stage, rather than per row)
+    // (each entry's rank in its run is taken here, so the scatter below
+    // needs no second round of contended LDS atomics)
     const uint64_t mid_mask = ((uint64_t)1 << mid_bits) - 1;
-    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) {
+    unsigned rk[kSieveItems];
+#pragma unroll
+    for (int j = 0; j < kSieveItems; ++j) {
+      const unsigned e = threadIdx.x + (unsigned)j * blockDim.x;
+      rk[j] = 0;
+      if (e >= total) continue;
       const unsigned dd = s.dest[e];
-      atomicAdd(s.hist + dd, 1u);
+      rk[j] = atomicAdd(s.hist + dd, 1u);
       const int64_t bkt = ((int64_t)dd << kp.super_bits) |
                           (int64_t)((((uint64_t)s.keys[e] >> kp.pk_bits) & mid_mask) >> kp.bucket_bits);
       if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
@@ -1444,17 +1447,18 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
           const unsigned up = __shfl_up(incl, off, 64);
           if (lane >= off) incl += up;
         }
-        if (base + lane < nd) s.start[base + lane] = s.gcur[base + lane] = carry + incl - v;
+        if (base + lane < nd) s.start[base + lane] = carry + incl - v;
         carry += __shfl(incl, 63, 64);
       }
     }
     __syncthreads();
     // every record straight to its run: the block (<= kSieveCap records) is
-    // written whole by this workgroup, so its partial lines merge in L2; no
-    // register holds a record across a barrier (the prefetched chunks stay
-    // in flight)
-    for (unsigned e = threadIdx.x; e < total; e += blockDim.x) {
-      const unsigned pos = written + atomicAdd(s.gcur + s.dest[e], 1u);
+    // written whole by this workgroup, so its partial lines merge in L2
+#pragma unroll
+    for (int j = 0; j < kSieveItems; ++j) {
+      const unsigned e = threadIdx.x + (unsigned)j * blockDim.x;
+      if (e >= total) continue;
+      const unsigned pos = written + s.start[s.dest[e]] + rk[j];
       blk[pos] = s.keys[e];
       if (ROWS) rblk[pos] = s.rows[e];
     }
@@ -1487,15 +1491,8 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
       for (int q = 0; q < Q; q += 2) {
         const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
         if constexpr (FULL) {
-#ifdef PDP_AB_NT
-          typedef long long v2i64 __attribute__((ext_vector_type(2)));
-          const v2i64 av = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(pid + i));
-          const v2i64 cv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(pk + i));
-          const longlong2 a{av.x, av.y}, c{cv.x, cv.y};
-#else
           const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
           const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
-#endif
           u[q] = a.x;
           u[q + 1] = a.y;
           k[q] = c.x;
@@ -1701,6 +1698,13 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
     src = (sbase != nullptr ? (unsigned)((sl / kStagesPerTile) * kSieveTileStride) + sbase[sl]
                             : (unsigned)(sl * kL1Rows)) + o[0];
   }
+  // the buckets' write cursors: loaded with the run table (independent of it)
+  const int nsub = 1 << kp.super_bits;
+  const int64_t s_first = (int64_t)B << kp.super_bits;
+  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+    const int64_t b = s_first + t;
+    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
+  }
   unsigned total, nnz;
   const unsigned ex = block_excl_scan(len, wsum, &total);
   const unsigned idx = block_excl_scan(len > 0 ? 1u : 0u, wsum2, &nnz);
@@ -1710,12 +1714,6 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   }
   if (threadIdx.x == 0) rbeg[nnz] = total;
   const int nr = (int)nnz;
-  const int nsub = 1 << kp.super_bits;
-  const int64_t s_first = (int64_t)B << kp.super_bits;
-  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
-    const int64_t b = s_first + t;
-    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
-  }
   __syncthreads();
   if (total == 0) return;  // block-uniform
 #ifdef PDP_PHASE_CLOCK

@@ -84,6 +84,9 @@ struct HWs {
   // cursors, the pair sums, {mode, pairs, overflow}; the level-1 / level-2
   // records reuse the pair-table region
   uint64_t hb_cts, hb_sbase, hb_bcnt, hb_bchunks, hb_bcur, hb_pairsum, hb_ctl;
+  // privacy-id buckets with partition ranges: each bucket's run start per
+  // range (k_hb_pid_pairs -> k_hb_prange)
+  uint64_t hb_pruns;
   uint64_t total;
 };
 
@@ -107,6 +110,29 @@ constexpr int kHbFill = 2760;            // 90 % of kHbSlots: more distinct pair
 constexpr int64_t kHbRowsPerBucket = 1536;
 constexpr int64_t kHbMaxBuckets = (int64_t)kHbFan * 256;
 constexpr int kHbPairThreads = 512;
+// Privacy-id buckets (the default, round 3): the same two levels keyed by a
+// hash of the privacy id alone, so one workgroup (k_hb_pid_pairs) sees every
+// row of its privacy ids and finishes their L0 / L1 counts in LDS; its pairs
+// leave as (partition, rows, sum) records grouped by 2,048-partition range,
+// which k_hb_prange sums per partition in LDS: no per-pair global atomics.
+// Each thread keeps its <= 4 table slots in registers after the pair phase,
+// so the 20-byte slots' LDS is reused by the pid table and the range
+// counters: 80,640 B + a few words, two 1,024-thread workgroups per CU.
+constexpr int kHbPidThreads = 1024;
+constexpr int kHbPidSlots = 4032;
+constexpr int kHbPidFill = 3628;         // 90 % of kHbPidSlots
+constexpr int kHbPidPer = (kHbPidSlots + kHbPidThreads - 1) / kHbPidThreads;
+constexpr int kHbRangeBits = 11;
+constexpr int kHbRangeW = 1 << kHbRangeBits;
+constexpr int kHbRangeMax = 128;         // more ranges (P > 262,144): per-pair partition atomics
+constexpr int kHbRangeThreads = 1024;
+static_assert(kHbPidSlots * 12 + kSmallBins * 4 + 3 * (kHbRangeMax + 1) * 4 <= kHbPidSlots * 20,
+              "the pid table, Linf bins and range counters reuse the pair table's LDS");
+
+inline int64_t hb_ranges(int64_t P) {
+  const int64_t R = (P + kHbRangeW - 1) >> kHbRangeBits;
+  return R >= 1 && R <= kHbRangeMax ? R : 0;
+}
 
 inline int64_t hb_buckets(int64_t n) {
   const int64_t nb = (n + kHbRowsPerBucket - 1) / kHbRowsPerBucket;
@@ -141,6 +167,8 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
     w.hb_bchunks = off; off = align256(off + (uint64_t)scan_chunk_sums_len(nb + 1) * 4);
     w.hb_bcur = off; off = align256(off + (uint64_t)nb * 4);
     w.hb_pairsum = off; off = align256(off + (uint64_t)n * 8);
+    const int64_t R = hb_ranges(P);
+    if (R > 0) { w.hb_pruns = off; off = align256(off + (uint64_t)nb * (R + 1) * 4); }
   }
   w.hb_ctl = off; off = align256(off + 16);  // {mode (1 = bucketed), pairs, overflow}
   w.total = off;
@@ -153,6 +181,8 @@ struct HT {
   uint64_t cap, pk_mask;             // cap: allocated slots (regions use a prefix of them)
   int64_t R;                         // regions
   int64_t nb, n_supers, n_tiles;     // bucketed pairs: pair buckets, super-buckets, tiles
+  int hb_pid;                        // buckets keyed by privacy id (else by the pair)
+  int64_t hb_R;                      // privacy-id buckets: partition ranges (0: per-pair atomics)
 };
 
 // order-preserving u64 image of an fp64 (for atomicMin/atomicMax)
@@ -547,6 +577,10 @@ __global__ void k_h_init(unsigned long long* minmax) {
 __device__ __forceinline__ unsigned hb_bucket(unsigned long long x, int64_t nb) {
   return (unsigned)(((mix64(x ^ 0x2545F4914F6CDD1DULL) >> 32) * (uint64_t)nb) >> 32);
 }
+// the bucket of a row's pair key under the call's keying (privacy id or pair)
+__device__ __forceinline__ unsigned hb_bucket_t(const HT& t, unsigned long long x) {
+  return hb_bucket(t.hb_pid ? x >> t.pk_bits : x, t.nb);
+}
 
 // exclusive scan of one u32 per thread over the workgroup (wsum: nw + 1 words)
 __device__ __forceinline__ unsigned hb_block_scan(unsigned x, unsigned* wsum, unsigned* total) {
@@ -591,7 +625,7 @@ __global__ void __launch_bounds__(kHbThreads) k_hb_count(HT t, const int64_t* __
       bad = true;
       continue;
     }
-    atomicAdd(h + hb_bucket(((uint64_t)u << t.pk_bits) | (uint64_t)k, t.nb) / kHbFan, 1u);
+    atomicAdd(h + hb_bucket_t(t, ((uint64_t)u << t.pk_bits) | (uint64_t)k) / kHbFan, 1u);
   }
   if (bad) atomicOr(err, 1u);
   __syncthreads();
@@ -665,7 +699,7 @@ __global__ void __launch_bounds__(kHbThreads) k_hb_l1(HT t, const int64_t* __res
       x[q] = ((uint64_t)u << t.pk_bits) | (uint64_t)k;
       if (VK == PDP_VALUE_F64) v[q] = ((const double*)value)[i];
       if (VK == PDP_VALUE_I64) v[q] = (double)((const long long*)value)[i];
-      d[q] = (int)(hb_bucket(x[q], t.nb) / kHbFan);
+      d[q] = (int)(hb_bucket_t(t, x[q]) / kHbFan);
     }
 #pragma unroll
     for (int q = 0; q < N; ++q) rank[q] = d[q] >= 0 ? atomicAdd(hist + d[q], 1u) : 0u;
@@ -722,7 +756,7 @@ __global__ void __launch_bounds__(kHbL2Threads) k_hb_bcount(HT t, const unsigned
   const int64_t a = sbase[s], e = sbase[s + 1];
   for (int64_t w0 = a + (int64_t)k * kHbWin; w0 < e; w0 += (int64_t)kHbK * kHbWin) {
     const int64_t w1 = w0 + kHbWin < e ? w0 + kHbWin : e;
-    for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) atomicAdd(h + hb_bucket(key[i], t.nb) % kHbFan, 1u);
+    for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) atomicAdd(h + hb_bucket_t(t, key[i]) % kHbFan, 1u);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) {
@@ -765,7 +799,7 @@ __global__ void __launch_bounds__(kHbL2Threads) k_hb_l2(HT t, const unsigned* __
       if (i < w1) {
         x[q] = ikey[i];
         if (HAS_VALUE) v[q] = ival[i];
-        d[q] = (int)(hb_bucket(x[q], t.nb) % kHbFan);
+        d[q] = (int)(hb_bucket_t(t, x[q]) % kHbFan);
       }
     }
 #pragma unroll
@@ -889,6 +923,246 @@ __global__ void __launch_bounds__(kHbPairThreads) k_hb_pairs(HT t, const unsigne
   block_minmax(mn, mx, minmax);  // contains __syncthreads
   __syncthreads();
   flush_small(H, lds, 0, H_LINF);
+}
+
+// a pair's contribution to its partition, grouped by partition range
+struct alignas(16) PRec {
+  unsigned pk, rows;
+  double sum;
+};
+
+// step 6, privacy-id buckets: one workgroup per bucket holds every row of its
+// privacy ids.  Phase 1 finds the distinct pairs in an LDS table (key, rows,
+// sum); each thread then keeps its <= kHbPidPer slots in registers and the
+// LDS becomes a pid table (distinct partitions << 32 | rows per pid), the
+// Linf bins and the range counters.  Per pair: its pid's counters, the Linf
+// bin, the pair-sum range and list, and either a PRec in the bucket's region
+// (RANGES: row positions [bstart[b], bstart[b] + pairs), grouped by range,
+// run starts in pruns[b][0..R]) or the partition atomics.  Per pid: one plain
+// store of its L0 / L1 counts (no other workgroup holds that pid).  A table
+// past kHbPidFill sets the overflow word; the call then redoes the pairs
+// with pair-keyed buckets.
+template <bool HAS_VALUE, bool RANGES>
+__global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
+    HT t, const unsigned* __restrict__ bstart, const unsigned long long* __restrict__ key,
+    const double* __restrict__ val, unsigned long long* __restrict__ pidstat, unsigned long long* pkstat,
+    double* psum, IntHists H, unsigned long long* minmax, double* __restrict__ pairsum, PRec* __restrict__ prec,
+    unsigned* __restrict__ pruns, unsigned* ctl) {
+  extern __shared__ unsigned long long hp_lds[];
+  unsigned long long* tkey = hp_lds;                         // phase 1: [kHbPidSlots] pair keys
+  double* tsum = (double*)(tkey + kHbPidSlots);              //          [kHbPidSlots] value sums
+  unsigned* tcnt = (unsigned*)(tsum + kHbPidSlots);          //          [kHbPidSlots] rows
+  unsigned long long* pst = hp_lds;                          // phase 2: [kHbPidSlots] pid counters
+  unsigned* pkey = (unsigned*)(pst + kHbPidSlots);           //          [kHbPidSlots] pids
+  unsigned* lbins = pkey + kHbPidSlots;                      //          [kSmallBins] Linf bins
+  unsigned* rcnt = lbins + kSmallBins;                       //          [kHbRangeMax + 1]
+  unsigned* rstart = rcnt + kHbRangeMax + 1;                 //          [kHbRangeMax + 1]
+  __shared__ unsigned fill, s_base, s_over;
+  for (int i = threadIdx.x; i < kHbPidSlots; i += blockDim.x) {
+    tkey[i] = ~0ULL;
+    tsum[i] = 0.0;
+    tcnt[i] = 0;
+  }
+  if (threadIdx.x == 0) {
+    fill = 0;
+    s_over = 0;
+  }
+  __syncthreads();
+  const int64_t a = bstart[blockIdx.x], e = bstart[blockIdx.x + 1];
+  for (int64_t i = a + threadIdx.x; i < e; i += blockDim.x) {
+    const unsigned long long x = key[i];
+    unsigned sl = (unsigned)(((mix64(x) & 0xFFFFFFFFULL) * (uint64_t)kHbPidSlots) >> 32);
+    bool over = false;
+    for (;;) {
+      const unsigned long long cur = tkey[sl];
+      if (cur == x) break;
+      if (cur == ~0ULL) {
+        if (atomicAdd(&fill, 1u) >= (unsigned)kHbPidFill) {
+          over = true;
+          break;
+        }
+        const unsigned long long old = atomicCAS(tkey + sl, ~0ULL, x);
+        if (old == ~0ULL) break;
+        atomicSub(&fill, 1u);
+        if (old == x) break;
+      }
+      sl = sl + 1 == (unsigned)kHbPidSlots ? 0u : sl + 1;
+    }
+    if (over) {
+      s_over = 1;
+      break;
+    }
+    atomicAdd(tcnt + sl, 1u);
+    if (HAS_VALUE) atomicAdd(tsum + sl, val[i]);
+  }
+  __syncthreads();
+  if (s_over) {  // workgroup-uniform: the call's results are discarded
+    if (threadIdx.x == 0) atomicOr(ctl + 2, 1u);
+    return;
+  }
+  unsigned long long kx[kHbPidPer];
+  unsigned kc[kHbPidPer], rk[kHbPidPer], pp[kHbPidPer];
+  double ks[kHbPidPer];
+#pragma unroll
+  for (int q = 0; q < kHbPidPer; ++q) {
+    const int j = threadIdx.x + q * kHbPidThreads;
+    kx[q] = ~0ULL;
+    kc[q] = 0;
+    ks[q] = 0.0;
+    if (j < kHbPidSlots) {
+      kx[q] = tkey[j];
+      kc[q] = tcnt[j];
+      if (HAS_VALUE) ks[q] = tsum[j];
+    }
+  }
+  __syncthreads();  // the table's bytes become the pid table
+  for (int i = threadIdx.x; i < kHbPidSlots; i += blockDim.x) {
+    pst[i] = 0;
+    pkey[i] = ~0u;
+  }
+  for (int i = threadIdx.x; i < kSmallBins; i += blockDim.x) lbins[i] = 0;
+  if (RANGES)
+    for (int i = threadIdx.x; i <= kHbRangeMax; i += blockDim.x) rcnt[i] = 0;
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  unsigned long long mn = ~0ULL, mx = 0ULL;
+#pragma unroll
+  for (int q = 0; q < kHbPidPer; ++q) {
+    rk[q] = 0;
+    pp[q] = 0;
+    if (kx[q] == ~0ULL) continue;
+    const unsigned long long x = kx[q];
+    const unsigned pid = (unsigned)(x >> t.pk_bits);  // < U <= 2^32 - 1, never the empty key
+    unsigned sl = (unsigned)(((uint64_t)(pid * 0x9E3779B1u) * (uint64_t)kHbPidSlots) >> 32);
+    for (;;) {  // pids <= pairs <= kHbPidFill: a free slot exists
+      const unsigned cur = pkey[sl];
+      if (cur == pid) break;
+      if (cur == ~0u) {
+        const unsigned old = atomicCAS(pkey + sl, ~0u, pid);
+        if (old == ~0u || old == pid) break;
+      }
+      sl = sl + 1 == (unsigned)kHbPidSlots ? 0u : sl + 1;
+    }
+    atomicAdd(pst + sl, (1ULL << 32) | kc[q]);
+    int_hist_add(H, lbins, H_LINF, 0, kc[q]);
+    const unsigned long long o = ord(ks[q]);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+    pp[q] = atomicAdd(&fill, 1u);
+    const uint64_t p = x & t.pk_mask;
+    if (RANGES) {
+      rk[q] = atomicAdd(rcnt + (p >> kHbRangeBits), 1u);
+    } else {
+      atomicAdd(pkstat + p, (1ULL << 32) | kc[q]);
+      if (HAS_VALUE) atomicAdd(psum + p, ks[q]);
+    }
+  }
+  __syncthreads();
+  const int R = (int)t.hb_R;
+  if (threadIdx.x < 64) {
+    if (RANGES) {  // exclusive scan of the range counts by one wave
+      const int lane = threadIdx.x;
+      unsigned carry = 0;
+      for (int b0 = 0; b0 < R; b0 += 64) {
+        const unsigned hv = b0 + lane < R ? rcnt[b0 + lane] : 0u;
+        unsigned incl = hv;
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned up = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += up;
+        }
+        if (b0 + lane < R) rstart[b0 + lane] = carry + incl - hv;
+        carry += __shfl(incl, 63, 64);
+      }
+      if (lane == 0) rstart[R] = carry;
+    }
+    if (threadIdx.x == 0) s_base = atomicAdd(ctl + 1, fill);  // this bucket's pair sums
+  }
+  __syncthreads();
+  if (RANGES)
+    for (int r = threadIdx.x; r <= R; r += blockDim.x) pruns[(int64_t)blockIdx.x * (R + 1) + r] = rstart[r];
+#pragma unroll
+  for (int q = 0; q < kHbPidPer; ++q) {
+    if (kx[q] == ~0ULL) continue;
+    const uint64_t p = kx[q] & t.pk_mask;
+    if (RANGES) {
+      PRec rec;
+      rec.pk = (unsigned)p;
+      rec.rows = kc[q];
+      rec.sum = ks[q];
+      prec[a + rstart[p >> kHbRangeBits] + rk[q]] = rec;
+    }
+    const unsigned long long at = (unsigned long long)s_base + pp[q];
+    if (at < (unsigned long long)t.n) pairsum[at] = ks[q];
+  }
+  for (int i = threadIdx.x; i < kHbPidSlots; i += blockDim.x) {
+    const unsigned pid = pkey[i];
+    if (pid != ~0u) pidstat[pid] = pst[i];
+  }
+  flush_small(H, lbins, 0, H_LINF);
+  block_minmax(mn, mx, minmax);  // contains __syncthreads
+}
+
+size_t hb_pid_lds() { return (size_t)kHbPidSlots * 20; }
+
+// step 7 (privacy-id buckets with ranges): workgroup (r, g) sums the records
+// of partition range r over buckets [g * per, (g + 1) * per) in LDS -- per
+// partition distinct pids, rows and value sum -- and flushes each partition
+// with one packed atomic (+ one for the sum).  A chunk of 1,024 buckets'
+// runs is flattened by a workgroup scan, so every lane reads a record of the
+// same runs (contiguous within a run).
+template <bool HAS_VALUE>
+__global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsigned* __restrict__ bstart,
+                                                               const unsigned* __restrict__ pruns,
+                                                               const PRec* __restrict__ prec,
+                                                               unsigned long long* pkstat, double* psum, int64_t per) {
+  __shared__ unsigned an[kHbRangeW], ar[kHbRangeW];
+  __shared__ double as[HAS_VALUE ? kHbRangeW : 1];
+  __shared__ unsigned bex[kHbRangeThreads], bbase[kHbRangeThreads];
+  __shared__ unsigned wsum[kHbRangeThreads / 64 + 1];
+  const int64_t r = blockIdx.x, R = t.hb_R;
+  for (int p = threadIdx.x; p < kHbRangeW; p += blockDim.x) {
+    an[p] = 0;
+    ar[p] = 0;
+    if (HAS_VALUE) as[p] = 0.0;
+  }
+  const int64_t b0 = (int64_t)blockIdx.y * per;
+  const int64_t b1 = b0 + per < t.nb ? b0 + per : t.nb;
+  for (int64_t c0 = b0; c0 < b1; c0 += kHbRangeThreads) {  // workgroup-uniform
+    const int64_t b = c0 + threadIdx.x;
+    unsigned len = 0, base = 0;
+    if (b < b1) {
+      const unsigned s = pruns[b * (R + 1) + r], s1 = pruns[b * (R + 1) + r + 1];
+      base = bstart[b] + s;
+      len = s1 - s;
+    }
+    unsigned tot;
+    const unsigned ex = hb_block_scan(len, wsum, &tot);  // its barriers also order the LDS clears
+    bex[threadIdx.x] = ex;
+    bbase[threadIdx.x] = base;
+    __syncthreads();
+    for (unsigned f = threadIdx.x; f < tot; f += blockDim.x) {
+      int lo = 0, hi = kHbRangeThreads;  // the last run starting at or before f
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (bex[mid] <= f) lo = mid;
+        else hi = mid;
+      }
+      const PRec rec = prec[bbase[lo] + (f - bex[lo])];
+      const unsigned p = rec.pk & (kHbRangeW - 1);
+      atomicAdd(an + p, 1u);
+      atomicAdd(ar + p, rec.rows);
+      if (HAS_VALUE) atomicAdd(as + p, rec.sum);
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < kHbRangeW; p += blockDim.x) {
+    const unsigned n = an[p];
+    if (!n) continue;
+    const int64_t g = r * kHbRangeW + p;
+    atomicAdd(pkstat + g, ((unsigned long long)n << 32) | ar[p]);
+    if (HAS_VALUE) atomicAdd(psum + g, as[p]);
+  }
 }
 
 // ------------------------------------------------------ pre-aggregated input --
@@ -1177,7 +1451,7 @@ int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_
     return set_error(PDP_E_INVALID, "every pdp_histogram_bins output must be set");
   if (n_rows < 0 || n_privacy_ids < 0 || n_partitions < 0) return set_error(PDP_E_INVALID, "sizes must be >= 0");
   if (n_rows >= (int64_t)1 << 31) return set_error(PDP_E_UNSUPPORTED, "n_rows must be < 2^31 per shard");
-  value_kind &= ~PDP_HIST_FORCE_PAIR_TABLE;
+  value_kind &= ~(PDP_HIST_FORCE_PAIR_TABLE | PDP_HIST_FORCE_PAIR_HASH);
   if (value_kind != PDP_VALUE_NONE && value_kind != PDP_VALUE_F64 && value_kind != PDP_VALUE_I64)
     return set_error(PDP_E_INVALID, "bad value_kind");
   if (bits_for(n_privacy_ids) + bits_for(n_partitions) > 63)
@@ -1209,9 +1483,11 @@ int hist_check(int32_t value_kind, int64_t n_rows, int64_t n_privacy_ids, int64_
 // the bucketed pairs phase (k_hb_*): pair-hash partition in two levels, then
 // one LDS pair table per bucket; sets hb_ctl = {1, pairs, overflow}
 int hist_pairs_bucketed(const HCall& c, const int64_t* privacy_id, const int64_t* partition, const void* value,
-                        int32_t value_kind) {
+                        int32_t value_kind, bool pid_buckets) {
   const HWs& w = c.w;
-  const HT& t = c.t;
+  HT t = c.t;
+  t.hb_pid = pid_buckets ? 1 : 0;
+  t.hb_R = pid_buckets && w.hb_pruns ? hb_ranges(t.P) : 0;
   char* ws = c.ws;
   hipStream_t st = c.st;
   unsigned* err = (unsigned*)(ws + w.err);
@@ -1266,6 +1542,43 @@ int hist_pairs_bucketed(const HCall& c, const int64_t* privacy_id, const int64_t
   double* psum = (double*)(ws + w.psum);
   unsigned long long* minmax = (unsigned long long*)(ws + w.minmax);
   double* pairsum = (double*)(ws + w.hb_pairsum);
+  if (pid_buckets) {
+    PRec* prec = (PRec*)key1;  // level-1 records are dead after level 2 (16 bytes per row)
+    unsigned* pruns = t.hb_R ? (unsigned*)(ws + w.hb_pruns) : nullptr;
+    const size_t lds = hb_pid_lds();
+    const void* f = hv ? (t.hb_R ? (const void*)k_hb_pid_pairs<true, true> : (const void*)k_hb_pid_pairs<true, false>)
+                       : (t.hb_R ? (const void*)k_hb_pid_pairs<false, true> : (const void*)k_hb_pid_pairs<false, false>);
+    PDP_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    {
+      const HT tt = t;
+      const unsigned* bst = bcnt;
+      const unsigned long long* k2 = key2;
+      const double* v2 = val2;
+      IntHists HH = c.H;
+      void* args[] = {(void*)&tt,     (void*)&bst,    (void*)&k2,      (void*)&v2,    (void*)&pidstat,
+                      (void*)&pkstat, (void*)&psum,   (void*)&HH,      (void*)&minmax, (void*)&pairsum,
+                      (void*)&prec,   (void*)&pruns,  (void*)&ctl};
+      PDP_PROF_BEGIN("k_hb_pid_pairs", st);
+      PDP_HIP_CHECK(hipLaunchKernel(f, dim3((unsigned)t.nb), dim3(kHbPidThreads), args, lds, st));
+      PDP_PROF_END(st);
+      PDP_HIP_CHECK(hipGetLastError());
+    }
+    if (t.hb_R) {
+      // ~1,024 workgroups: R ranges x G slices of the buckets
+      int64_t G = 1024 / t.hb_R;
+      G = G < 1 ? 1 : G;
+      const int64_t per = (t.nb + G - 1) / G;
+      G = (t.nb + per - 1) / per;
+      const PRec* pr = prec;
+      if (hv)
+        PDP_HLAUNCH("k_hb_prange", st, k_hb_prange<true>, dim3((unsigned)t.hb_R, (unsigned)G), dim3(kHbRangeThreads),
+                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, per);
+      else
+        PDP_HLAUNCH("k_hb_prange", st, k_hb_prange<false>, dim3((unsigned)t.hb_R, (unsigned)G), dim3(kHbRangeThreads),
+                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, per);
+    }
+    return PDP_OK;
+  }
   if (hv)
     PDP_HLAUNCH("k_hb_pairs", st, k_hb_pairs<true>, dim3((unsigned)t.nb), dim3(kHbPairThreads), 0, st, t,
                 (const unsigned*)bcnt, (const unsigned long long*)key2, (const double*)val2, pidstat, pkstat, psum,
@@ -1286,7 +1599,8 @@ int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partiti
   char* ws = c.ws;
   hipStream_t st = c.st;
   const bool force_table = (value_kind & PDP_HIST_FORCE_PAIR_TABLE) != 0;
-  value_kind &= ~PDP_HIST_FORCE_PAIR_TABLE;
+  const bool force_hash = (value_kind & PDP_HIST_FORCE_PAIR_HASH) != 0;
+  value_kind &= ~(PDP_HIST_FORCE_PAIR_TABLE | PDP_HIST_FORCE_PAIR_HASH);
   const bool bucketed = !force_table && hb_eligible(t.n);
   PDP_HIP_CHECK(hipMemsetAsync(ws + w.err, 0, 16, st));
   // the pair table (slots .. region scan) only for its own path; the per-pid
@@ -1306,20 +1620,26 @@ int hist_pairs(const HCall& c, const int64_t* privacy_id, const int64_t* partiti
   if (privacy_id == nullptr || partition == nullptr || (value_kind != PDP_VALUE_NONE && value == nullptr))
     return set_error(PDP_E_INVALID, "NULL column");
   if (bucketed) {
-    const int rc = hist_pairs_bucketed(c, privacy_id, partition, value, value_kind);
-    if (rc != PDP_OK) return rc;
-    unsigned over = 0;
-    PDP_HIP_CHECK(hipMemcpyAsync(&over, ws + w.hb_ctl + 8, 4, hipMemcpyDeviceToHost, st));
-    PDP_HIP_CHECK(hipStreamSynchronize(st));
-    if (!over) return PDP_OK;
-    // a bucket's table overflowed (adversarial keys): the pair-table path
-    // from scratch
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.hb_ctl, 0, 16, st));
-    PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
-    PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
-    PDP_HIP_CHECK(hipMemsetAsync(out->int_sum, 0, 5 * kLogBins * 8, st));
-    PDP_HIP_CHECK(hipMemsetAsync(out->int_max, 0, 5 * kLogBins * 8, st));
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.minmax - w.slots, st));  // slots .. psum
+    // privacy-id buckets first (pids < 2^32 - 1), then pair buckets, then
+    // the pair table: a bucket whose distinct pairs overflow its LDS table
+    // (a privacy id with thousands of partitions; crafted keys) sends the
+    // whole call to the next one, from scratch
+    const bool pid_ok = !force_hash && t.U <= (int64_t)0xFFFFFFFFLL;
+    for (int attempt = pid_ok ? 0 : 1; attempt < 2; ++attempt) {
+      const int rc = hist_pairs_bucketed(c, privacy_id, partition, value, value_kind, attempt == 0);
+      if (rc != PDP_OK) return rc;
+      unsigned over = 0;
+      PDP_HIP_CHECK(hipMemcpyAsync(&over, ws + w.hb_ctl + 8, 4, hipMemcpyDeviceToHost, st));
+      PDP_HIP_CHECK(hipStreamSynchronize(st));
+      if (!over) return PDP_OK;
+      PDP_HIP_CHECK(hipMemsetAsync(ws + w.hb_ctl, 0, 16, st));
+      PDP_HLAUNCH("k_h_init", st, k_h_init, dim3(1), dim3(64), 0, st, (unsigned long long*)(ws + w.minmax));
+      PDP_HIP_CHECK(hipMemsetAsync(out->int_count, 0, 5 * kLogBins * 8, st));
+      PDP_HIP_CHECK(hipMemsetAsync(out->int_sum, 0, 5 * kLogBins * 8, st));
+      PDP_HIP_CHECK(hipMemsetAsync(out->int_max, 0, 5 * kLogBins * 8, st));
+      PDP_HIP_CHECK(hipMemsetAsync(ws + w.pidstat, 0, w.minmax - w.pidstat, st));  // pidstat .. psum
+    }
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.slots, 0, w.pidstat - w.slots, st));  // the pair table
   }
   Slot* slots = (Slot*)(ws + w.slots);
   unsigned* err = (unsigned*)(ws + w.err);

@@ -418,7 +418,8 @@ def add_noise(values, *, noise: NoiseParams, seed: int, index_offset: int = 0, o
 
 def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int, stream=None,
                        workspace: Optional[BoundWorkspace] = None, group=None,
-                       force_pair_table: bool = False) -> Dict[str, "torch.Tensor"]:
+                       force_pair_table: bool = False,
+                       force_pair_hash: bool = False) -> Dict[str, "torch.Tensor"]:
     """compute_dataset_histograms (computing_histograms.py:456-513) on device
     columns of dense codes (`pdp_dataset_histograms`): returns the raw device
     bin arrays (int_count/int_sum/int_max [5, LOG_BINS], float_count/
@@ -438,8 +439,10 @@ def dataset_histograms(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     if value is not None:
         _check_col(value, "value", (torch.int64, torch.float64), n, device)
         vk = N.VALUE_I64 if value.dtype == torch.int64 else N.VALUE_F64
-    if force_pair_table:  # tests: the HBM pair-table path instead of the pair buckets
+    if force_pair_table:  # tests: the HBM pair-table path instead of the buckets
         vk |= N.HIST_FORCE_PAIR_TABLE
+    if force_pair_hash:   # tests: pair-keyed buckets instead of privacy-id buckets
+        vk |= N.HIST_FORCE_PAIR_HASH
     nbytes = ctypes.c_uint64()
     N.check(lib.pdp_dataset_histograms_workspace_bytes(n, int(n_privacy_ids), int(n_partitions),
                                                       ctypes.byref(nbytes)),

@@ -28,25 +28,31 @@ def _check_all(got, want, what, exact=False):
         HU.assert_bins_equal(getattr(got, field).bins, want[field], f"{what}/{field}", exact=exact)
 
 
-def _run_codes(pid, pk, val, U=None, P=None, force_pair_table=False):
+def _run_codes(pid, pk, val, U=None, P=None, mode="auto"):
     import torch
     d = _dev()
     U = int(pid.max()) + 1 if U is None else U
     P = int(pk.max()) + 1 if P is None else P
     vt = None if val is None else torch.as_tensor(val, device=d)
     raw = X.dataset_histograms(torch.as_tensor(pid, device=d), torch.as_tensor(pk, device=d), vt,
-                               n_privacy_ids=U, n_partitions=P, force_pair_table=force_pair_table)
+                               n_privacy_ids=U, n_partitions=P, force_pair_table=mode == "pair_table",
+                               force_pair_hash=mode == "pair_hash")
     return CH.histograms_from_device(raw)
 
 
-@pytest.mark.parametrize("case", ["uniform", "zipf_pids", "heavy_pairs", "int_values", "no_values"])
-def test_pair_buckets_and_pair_table_agree_with_oracle(case):
-    """The two pairs phases of pdp_hist.hip -- rows hashed into pair buckets
-    with one LDS table each (default up to ~1e8 rows) and the HBM pair table
-    (PDP_HIST_FORCE_PAIR_TABLE) -- give the oracle's bins; 3e6 rows, so the
-    buckets span two partition levels (1,954 buckets in 8 super-buckets)."""
+@pytest.mark.parametrize("case", ["uniform", "zipf_pids", "heavy_pairs", "int_values", "no_values",
+                                  "wide_partitions", "zipf_partitions"])
+def test_pair_phases_agree_with_oracle(case):
+    """The three pairs phases of pdp_hist.hip -- rows hashed into privacy-id
+    buckets (default; pid counters in LDS, partition records summed per
+    2,048-partition range by k_hb_prange, or partition atomics above 262,144
+    partitions: "wide_partitions"), into pair buckets (PDP_HIST_FORCE_PAIR_HASH)
+    and the HBM pair table (PDP_HIST_FORCE_PAIR_TABLE) -- give the oracle's
+    bins; 3e6 rows, so the buckets span two levels (1,954 buckets in 8
+    super-buckets).  "zipf_pids" has privacy ids with 10^4..10^6 rows, whose
+    privacy-id buckets overflow: the default call falls back to pair buckets."""
     rng = np.random.default_rng({"uniform": 11, "zipf_pids": 12, "heavy_pairs": 13, "int_values": 14,
-                                 "no_values": 15}[case])
+                                 "no_values": 15, "wide_partitions": 16, "zipf_partitions": 17}[case])
     n = 3_000_000
     pid = rng.integers(0, 200_000, n)
     pk = rng.integers(0, 40_000, n)
@@ -55,21 +61,40 @@ def test_pair_buckets_and_pair_table_agree_with_oracle(case):
     if case == "heavy_pairs":  # a few pairs with 10^5 rows each (one bucket holds them all)
         pid[:400_000] = rng.integers(0, 4, 400_000)
         pk[:400_000] = rng.integers(0, 2, 400_000)
+    if case == "wide_partitions":
+        pk = rng.integers(0, 300_000, n)
+    if case == "zipf_partitions":  # hot partitions: LDS atomics on one range word
+        pk = np.minimum(rng.zipf(1.1, n) - 1, 99_999)
     val = np.round(rng.normal(1, 3, n) * 8) / 8
     if case == "int_values":
         val = rng.integers(-20, 60, n)
     if case == "no_values":
         val = None
     want = OH.dataset_histograms(pid, pk, np.zeros(n) if val is None else val)
-    for force in (False, True):
-        got = _run_codes(pid, pk, val, force_pair_table=force)
-        _check_all(got, want, f"{case}/force={force}", exact=True)
+    for mode in ("auto", "pair_hash", "pair_table"):
+        got = _run_codes(pid, pk, val, mode=mode)
+        _check_all(got, want, f"{case}/{mode}", exact=True)
+
+
+def test_pid_bucket_overflow_falls_back_to_pair_buckets():
+    """One privacy id with 6,000 distinct partitions (and 3,000 light ones):
+    its bucket's LDS table (kHbPidFill = 3,628 pairs) overflows, so the call
+    redoes the pairs with pair-keyed buckets -- same bins."""
+    rng = np.random.default_rng(21)
+    heavy_pk = rng.permutation(8_192)[:6_000]
+    pid = np.concatenate([np.zeros(6_000, np.int64), rng.integers(1, 1_000, 3_000)])
+    pk = np.concatenate([heavy_pk, rng.integers(0, 8_192, 3_000)])
+    val = np.round(rng.normal(0, 2, len(pid)) * 4) / 4
+    got = _run_codes(pid, pk, val, U=1_000, P=8_192)
+    _check_all(got, OH.dataset_histograms(pid, pk, val), "pid-overflow", exact=True)
 
 
 def test_pair_bucket_overflow_falls_back():
     """3,000 distinct pairs that all hash into pair bucket 0 of 2 (crafted with
-    the kernel's bucket hash): more than one LDS table holds (kHbFill = 2,760),
-    so the call redoes the pairs on the HBM pair table -- same bins."""
+    the kernel's bucket hash): with the pair-keyed buckets
+    (PDP_HIST_FORCE_PAIR_HASH) more than one LDS table holds (kHbFill =
+    2,760), so the call redoes the pairs on the HBM pair table -- same bins;
+    the default privacy-id buckets hold them."""
     from oracle.columnar import mix64
     U, P = 5_000, 64
     cand_pid = np.repeat(np.arange(U, dtype=np.int64), P)
@@ -82,8 +107,10 @@ def test_pair_bucket_overflow_falls_back():
     assert len(pick) == 3000
     pid, pk = cand_pid[pick], cand_pk[pick]
     val = np.round(np.random.default_rng(7).normal(0, 2, len(pid)) * 4) / 4
-    got = _run_codes(pid, pk, val, U=U, P=P)
-    _check_all(got, OH.dataset_histograms(pid, pk, val), "overflow", exact=True)
+    want = OH.dataset_histograms(pid, pk, val)
+    for mode in ("pair_hash", "auto"):
+        got = _run_codes(pid, pk, val, U=U, P=P, mode=mode)
+        _check_all(got, want, f"overflow/{mode}", exact=True)
 
 
 @pytest.mark.parametrize("fx", HU.fixtures(), ids=lambda f: f["name"])

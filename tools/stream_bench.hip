@@ -74,6 +74,46 @@ __global__ void __launch_bounds__(512) k_span_lds(const longlong2* __restrict__ 
   if (acc == 0x1234567) out[0] = 1;
 }
 
+// D: the level-1 shape -- one 1,024-thread block per 65,536-row tile reading
+// TWO int64 columns (pid, pk) with 16-byte loads, Q rows per thread per chunk
+template <int Q>
+__global__ void __launch_bounds__(1024) k_tiles2(const long long* __restrict__ a, const long long* __restrict__ b,
+                                                 size_t n, unsigned* out) {
+  long long acc = 0;
+  const size_t t0 = (size_t)blockIdx.x * 65536, t1 = t0 + 65536 < n ? t0 + 65536 : n;
+  for (size_t c0 = t0; c0 < t1; c0 += (size_t)1024 * Q) {
+#pragma unroll
+    for (int q = 0; q < Q; q += 2) {
+      const size_t i = c0 + 2 * (threadIdx.x + (size_t)(q / 2) * 1024);
+      if (i + 1 < t1) {
+        const longlong2 x = *reinterpret_cast<const longlong2*>(a + i);
+        const longlong2 y = *reinterpret_cast<const longlong2*>(b + i);
+        acc ^= x.x ^ x.y ^ y.x ^ y.y;
+      }
+    }
+  }
+  if (acc == 0x1234567) out[0] = 1;
+}
+
+// E: two columns, grid-stride 256-thread blocks (the best one-column shape)
+__global__ void __launch_bounds__(256) k_grid2(const longlong2* __restrict__ a, const longlong2* __restrict__ b,
+                                               size_t n2, unsigned* out) {
+  long long acc = 0;
+  const size_t stride = (size_t)gridDim.x * blockDim.x * 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x * 4 + threadIdx.x; i < n2; i += stride) {
+    longlong2 v[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t j = i + (size_t)u * blockDim.x;
+      v[2 * u] = j < n2 ? a[j] : longlong2{0, 0};
+      v[2 * u + 1] = j < n2 ? b[j] : longlong2{0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y;
+  }
+  if (acc == 0x1234567) out[0] = 1;
+}
+
 template <typename F>
 double time_it(F&& launch) {
   hipEvent_t a, b;
@@ -123,6 +163,17 @@ int main() {
   RUN2("span+lds8K U=8 g=2048 t512", (k_span_lds<8, 2048>), 2048, 512);
   RUN2("span+lds4K U=8 g=4096 t256", (k_span_lds<8, 1024>), 4096, 256);
   RUN2("span+lds8K U=4 g=4096 t256", (k_span_lds<4, 2048>), 4096, 256);
+  {  // two 4 GiB columns (the level-1 pid / pk pair): 8 GiB read per call
+    const size_t n = kRows / 2;
+    const long long* a = (const long long*)p;
+    const long long* b = a + n;
+    const unsigned tiles = (unsigned)((n + 65535) / 65536);
+    auto rep2 = [&](const char* name, double ms) { printf("%-28s %8.3f ms %8.1f GB/s\n", name, ms, gb / (ms * 1e-3)); };
+    rep2("tiles2 Q=4 (level-1 shape)", time_it([&] { hipLaunchKernelGGL((k_tiles2<4>), dim3(tiles), dim3(1024), 0, 0, a, b, n, out); }));
+    rep2("tiles2 Q=8", time_it([&] { hipLaunchKernelGGL((k_tiles2<8>), dim3(tiles), dim3(1024), 0, 0, a, b, n, out); }));
+    rep2("grid2 U=4 g=2048", time_it([&] { hipLaunchKernelGGL(k_grid2, dim3(2048), dim3(256), 0, 0, (const longlong2*)a,
+                                                               (const longlong2*)b, n / 2, out); }));
+  }
   CHECK(hipFree(p));
   CHECK(hipFree(out));
   return 0;
