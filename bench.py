@@ -494,7 +494,9 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
     # gathered; one record per kept pair out
     out["k_bucket_bound"] = key2 * cand + 12.0 * kept_rows + pair_rec * kept_pairs
     if plan.sieve:
-        out["k_sieve_rescan"] = 8.0 * n + 8.0 * fix         # privacy ids in, (id, row) per fix-up row out
+        # privacy ids in, (id, row) per fix-up row out; with no unresolved
+        # privacy id the rescan exits before reading anything
+        out["k_sieve_rescan"] = (8.0 * n + 8.0 * fix) if stats.get("unresolved_ids", 1) else 0.0
         out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * fix      # list in, partition gathered, record out
         out["k_bucket_fix"] = key2 * fix
     out["k_range_reduce"] = 2.0 * pair_rec * kept_pairs

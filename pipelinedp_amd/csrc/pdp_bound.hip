@@ -1698,13 +1698,6 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
     src = (sbase != nullptr ? (unsigned)((sl / kStagesPerTile) * kSieveTileStride) + sbase[sl]
                             : (unsigned)(sl * kL1Rows)) + o[0];
   }
-  // the buckets' write cursors: loaded with the run table (independent of it)
-  const int nsub = 1 << kp.super_bits;
-  const int64_t s_first = (int64_t)B << kp.super_bits;
-  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
-    const int64_t b = s_first + t;
-    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
-  }
   unsigned total, nnz;
   const unsigned ex = block_excl_scan(len, wsum, &total);
   const unsigned idx = block_excl_scan(len > 0 ? 1u : 0u, wsum2, &nnz);
@@ -1714,6 +1707,12 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   }
   if (threadIdx.x == 0) rbeg[nnz] = total;
   const int nr = (int)nnz;
+  const int nsub = 1 << kp.super_bits;
+  const int64_t s_first = (int64_t)B << kp.super_bits;
+  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+    const int64_t b = s_first + t;
+    s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
+  }
   __syncthreads();
   if (total == 0) return;  // block-uniform
 #ifdef PDP_PHASE_CLOCK

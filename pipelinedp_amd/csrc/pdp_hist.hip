@@ -55,6 +55,13 @@ struct alignas(32) Slot {
   unsigned cnt, pad;
 };
 
+// a pair's contribution to its partition (privacy-id buckets), grouped by
+// partition range
+struct alignas(16) PRec {
+  unsigned pk, rows;
+  double sum;
+};
+
 uint64_t table_capacity(int64_t n_rows) {
   uint64_t c = (uint64_t)n_rows + (uint64_t)n_rows / 2;
   c = (c + 255) & ~(uint64_t)255;
@@ -170,7 +177,9 @@ HWs hlayout(int64_t n, int64_t U, int64_t P) {
     const int64_t R = hb_ranges(P);
     if (R > 0) { w.hb_pruns = off; off = align256(off + (uint64_t)nb * (R + 1) * 4); }
   }
-  w.hb_ctl = off; off = align256(off + 16);  // {mode (1 = bucketed), pairs, overflow}
+  // {mode (1: pair buckets' pair-sum list, 2: privacy-id buckets' records),
+  //  pairs (mode 1), overflow, ranges (mode 2)}
+  w.hb_ctl = off; off = align256(off + 16);
   w.total = off;
   return w;
 }
@@ -223,6 +232,20 @@ __device__ __forceinline__ void int_hist_add(const IntHists& H, unsigned* lds_co
     const int64_t g = (int64_t)h * kLogBins + b;
     atomicAdd(H.count + g, 1ULL);
     atomicAdd(H.sum + g, v);
+    atomicMax(H.max + g, v);
+  }
+}
+
+// n elements of value v (one wave's elements that share a value)
+__device__ __forceinline__ void int_hist_add_n(const IntHists& H, unsigned* lds_counts, int h, int slot,
+                                               unsigned long long v, unsigned n) {
+  const int b = log_bin_index(v);
+  if (b < kSmallBins) {
+    atomicAdd(lds_counts + slot * kSmallBins + b, n);
+  } else {
+    const int64_t g = (int64_t)h * kLogBins + b;
+    atomicAdd(H.count + g, (unsigned long long)n);
+    atomicAdd(H.sum + g, v * n);
     atomicMax(H.max + g, v);
   }
 }
@@ -489,51 +512,125 @@ __device__ __forceinline__ void max_filtered(unsigned long long* omax, unsigned 
   if (o > __hip_atomic_load(omax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(omax, o);
 }
 
+// the lowers of k_h_lowers recomputed in registers (same roundings, so the
+// same doubles): a value's bin costs no memory reads
+struct LinBins {
+  double mn, mx, step, delta, inv;
+  int nb;
+};
+__device__ __forceinline__ LinBins lin_bins(const double* __restrict__ L, int nl) {
+  LinBins z{0.0, 0.0, 0.0, 0.0, 0.0, nl - 1};
+  if (nl < 2) return z;
+  z.mn = L[0];
+  z.mx = L[nl - 1];
+  z.delta = __dsub_rn(z.mx, z.mn);
+  z.step = __ddiv_rn(z.delta, (double)kSumBuckets);
+  z.inv = z.delta > 0.0 ? (double)z.nb / z.delta : 0.0;
+  return z;
+}
+__device__ __forceinline__ double lin_lower(const LinBins& z, int i) {
+  if (i == z.nb) return z.mx;
+  const double y = z.step == 0.0 ? __dmul_rn(__ddiv_rn((double)i, (double)kSumBuckets), z.delta)
+                                 : __dmul_rn((double)i, z.step);
+  return __dadd_rn(y, z.mn);
+}
+// bisect_right(lowers, v) - 1 as float_bin, from the recomputed lowers
+__device__ __forceinline__ int lin_bin(const LinBins& z, double v) {
+  const int nb = z.nb;
+  if (nb <= 1) return 0;
+  int b = (int)((v - z.mn) * z.inv);  // a guess; the loops make it exact
+  b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+  while (b + 1 < nb && lin_lower(z, b + 1) <= v) ++b;
+  while (b > 0 && lin_lower(z, b) > v) --b;
+  return b;
+}
+
 constexpr int kFloatBlock = 1024;
 
 // pair sums: counts and sums in LDS (one workgroup per CU, 16 waves), flushed
-// once; partition sums (P elements): global atomics
+// once; bin maxima: an LDS word per bin holds the high half of the largest
+// ordered image this workgroup sent to the global atomicMax, so only values
+// that can raise it go out (a value equal to it in the high half first reads
+// the global maximum: an atomic per copy of a clipped value on one address
+// took k_h_float from 1.8 to 53 ms); partition sums (P elements): global atomics
 __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
                                                          const double* __restrict__ pairsum,
                                                          const unsigned* __restrict__ hb_ctl,
+                                                         const unsigned* __restrict__ hb_bstart,
+                                                         const unsigned* __restrict__ hb_pruns,
+                                                         const PRec* __restrict__ hb_prec,
                                                          const unsigned long long* __restrict__ pkstat,
                                                          const double* __restrict__ psum,
                                                          const double* __restrict__ lowers,
                                                          const int* __restrict__ n_lowers, FloatHists F) {
   __shared__ unsigned lcnt[kSumBuckets];
   __shared__ double lsum[kSumBuckets];
+  __shared__ unsigned lmx[kSumBuckets];
   for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
     lcnt[b] = 0;
     lsum[b] = 0.0;
+    lmx[b] = 0;
   }
   __syncthreads();
   const int64_t C = (int64_t)t.cap;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
-  if (nl0 > 0 && hb_ctl[0] == 1) {  // the bucketed path's list of pair sums
+  const LinBins z0 = lin_bins(lowers, nl0);
+  auto add = [&](double v) {
+    const int b = lin_bin(z0, v);
+    atomicAdd(lcnt + b, 1u);
+    atomicAdd(lsum + b, v);
+    const unsigned long long o = ord(v);
+    const unsigned hi = (unsigned)(o >> 32);
+    const unsigned cur = lmx[b];
+    if (hi > cur) {  // raises the bin's maximum
+      atomicMax(lmx + b, hi);
+      atomicMax(F.omax + b, o);
+    } else if (hi == cur) {  // ties (clipped values: thousands per bin) read the global maximum first
+      max_filtered(F.omax + b, o);
+    }
+  };
+  constexpr int U = 4;  // values in flight per thread
+  if (nl0 > 0 && hb_ctl[0] == 1) {  // the pair buckets' list of pair sums
     const int64_t np = hb_ctl[1];
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < np; i += stride) {
-      const double v = pairsum[i];
-      const int b = float_bin(lowers, nl0, v);
-      atomicAdd(lcnt + b, 1u);
-      atomicAdd(lsum + b, v);
-      max_filtered(F.omax + b, ord(v));
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < np; i0 += U * stride) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < np ? pairsum[i0 + u * stride] : 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i0 + u * stride < np) add(v[u]);
+    }
+  } else if (nl0 > 0 && hb_ctl[0] == 2) {  // the privacy-id buckets' pair records: a wave per bucket
+    const int64_t R = hb_ctl[3];
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = stride >> 6;
+    for (int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; b < t.nb; b += nw) {
+      const unsigned a = hb_bstart[b], rows = hb_bstart[b + 1] - a;
+      unsigned c = hb_pruns[b * (R + 1) + R];
+      c = c <= rows ? c : 0u;
+      for (unsigned j0 = lane; j0 < c; j0 += U * 64) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = j0 + u * 64 < c ? hb_prec[a + j0 + u * 64].sum : 0.0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (j0 + u * 64 < c) add(v[u]);
+      }
     }
   } else if (nl0 > 0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += stride) {
       const Slot sl = slots[i];
       if (sl.key == 0) continue;
-      const int b = float_bin(lowers, nl0, sl.sum);
-      atomicAdd(lcnt + b, 1u);
-      atomicAdd(lsum + b, sl.sum);
-      max_filtered(F.omax + b, ord(sl.sum));
+      add(sl.sum);
     }
   }
   if (nl1 > 0) {
+    const LinBins z1 = lin_bins(lowers + kNLowers, nl1);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
       if (pkstat[i] == 0) continue;
       const double v = psum[i];
-      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + float_bin(lowers + kNLowers, nl1, v);
+      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + lin_bin(z1, v);
       atomicAdd(F.count + g, 1ULL);
       atomicAdd(F.sum + g, v);
       max_filtered(F.omax + g, ord(v));
@@ -925,23 +1022,20 @@ __global__ void __launch_bounds__(kHbPairThreads) k_hb_pairs(HT t, const unsigne
   flush_small(H, lds, 0, H_LINF);
 }
 
-// a pair's contribution to its partition, grouped by partition range
-struct alignas(16) PRec {
-  unsigned pk, rows;
-  double sum;
-};
-
 // step 6, privacy-id buckets: one workgroup per bucket holds every row of its
 // privacy ids.  Phase 1 finds the distinct pairs in an LDS table (key, rows,
 // sum); each thread then keeps its <= kHbPidPer slots in registers and the
-// LDS becomes a pid table (distinct partitions << 32 | rows per pid), the
-// Linf bins and the range counters.  Per pair: its pid's counters, the Linf
-// bin, the pair-sum range and list, and either a PRec in the bucket's region
-// (RANGES: row positions [bstart[b], bstart[b] + pairs), grouped by range,
-// run starts in pruns[b][0..R]) or the partition atomics.  Per pid: one plain
-// store of its L0 / L1 counts (no other workgroup holds that pid).  A table
-// past kHbPidFill sets the overflow word; the call then redoes the pairs
-// with pair-keyed buckets.
+// LDS becomes a pid table (distinct partitions << 32 | rows per pid) and the
+// range counters.  Per pair: its pid's counters and either (RANGES) a PRec
+// in the bucket's region -- row positions [bstart[b], bstart[b] + pairs),
+// grouped by partition range, run starts in pruns[b][0..R]; k_hb_prange
+// then does the partition sums, the Linf bins and the pair-sum range, and
+// k_h_float reads the pair sums there -- or the partition atomics, Linf bins,
+// pair-sum range and list here.  No global word is touched by every
+// workgroup (a returning atomic on one address per bucket serialises).  Per
+// pid: one plain store of its L0 / L1 counts (no other workgroup holds that
+// pid).  A table past kHbPidFill sets the overflow word; the call then
+// redoes the pairs with pair-keyed buckets.
 template <bool HAS_VALUE, bool RANGES>
 __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
     HT t, const unsigned* __restrict__ bstart, const unsigned long long* __restrict__ key,
@@ -997,6 +1091,9 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
   }
   __syncthreads();
   if (s_over) {  // workgroup-uniform: the call's results are discarded
+    // k_hb_prange still reads this bucket's runs: leave them empty
+    if (RANGES)
+      for (int r = threadIdx.x; r <= (int)t.hb_R; r += blockDim.x) pruns[(int64_t)blockIdx.x * (t.hb_R + 1) + r] = 0;
     if (threadIdx.x == 0) atomicOr(ctl + 2, 1u);
     return;
   }
@@ -1020,7 +1117,8 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
     pst[i] = 0;
     pkey[i] = ~0u;
   }
-  for (int i = threadIdx.x; i < kSmallBins; i += blockDim.x) lbins[i] = 0;
+  if (!RANGES)
+    for (int i = threadIdx.x; i < kSmallBins; i += blockDim.x) lbins[i] = 0;
   if (RANGES)
     for (int i = threadIdx.x; i <= kHbRangeMax; i += blockDim.x) rcnt[i] = 0;
   if (threadIdx.x == 0) fill = 0;
@@ -1044,15 +1142,15 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
       sl = sl + 1 == (unsigned)kHbPidSlots ? 0u : sl + 1;
     }
     atomicAdd(pst + sl, (1ULL << 32) | kc[q]);
-    int_hist_add(H, lbins, H_LINF, 0, kc[q]);
-    const unsigned long long o = ord(ks[q]);
-    mn = o < mn ? o : mn;
-    mx = o > mx ? o : mx;
-    pp[q] = atomicAdd(&fill, 1u);
     const uint64_t p = x & t.pk_mask;
     if (RANGES) {
       rk[q] = atomicAdd(rcnt + (p >> kHbRangeBits), 1u);
     } else {
+      int_hist_add(H, lbins, H_LINF, 0, kc[q]);
+      const unsigned long long o = ord(ks[q]);
+      mn = o < mn ? o : mn;
+      mx = o > mx ? o : mx;
+      pp[q] = atomicAdd(&fill, 1u);
       atomicAdd(pkstat + p, (1ULL << 32) | kc[q]);
       if (HAS_VALUE) atomicAdd(psum + p, ks[q]);
     }
@@ -1075,7 +1173,7 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
       }
       if (lane == 0) rstart[R] = carry;
     }
-    if (threadIdx.x == 0) s_base = atomicAdd(ctl + 1, fill);  // this bucket's pair sums
+    if (!RANGES && threadIdx.x == 0) s_base = atomicAdd(ctl + 1, fill);  // this bucket's pair sums
   }
   __syncthreads();
   if (RANGES)
@@ -1090,16 +1188,19 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
       rec.rows = kc[q];
       rec.sum = ks[q];
       prec[a + rstart[p >> kHbRangeBits] + rk[q]] = rec;
+    } else {
+      const unsigned long long at = (unsigned long long)s_base + pp[q];
+      if (at < (unsigned long long)t.n) pairsum[at] = ks[q];
     }
-    const unsigned long long at = (unsigned long long)s_base + pp[q];
-    if (at < (unsigned long long)t.n) pairsum[at] = ks[q];
   }
   for (int i = threadIdx.x; i < kHbPidSlots; i += blockDim.x) {
     const unsigned pid = pkey[i];
     if (pid != ~0u) pidstat[pid] = pst[i];
   }
-  flush_small(H, lbins, 0, H_LINF);
-  block_minmax(mn, mx, minmax);  // contains __syncthreads
+  if (!RANGES) {
+    flush_small(H, lbins, 0, H_LINF);
+    block_minmax(mn, mx, minmax);  // contains __syncthreads (workgroup-uniform branch)
+  }
 }
 
 size_t hb_pid_lds() { return (size_t)kHbPidSlots * 20; }
@@ -1107,15 +1208,18 @@ size_t hb_pid_lds() { return (size_t)kHbPidSlots * 20; }
 // step 7 (privacy-id buckets with ranges): workgroup (r, g) sums the records
 // of partition range r over buckets [g * per, (g + 1) * per) in LDS -- per
 // partition distinct pids, rows and value sum -- and flushes each partition
-// with one packed atomic (+ one for the sum).  A chunk of 1,024 buckets'
-// runs is flattened by a workgroup scan, so every lane reads a record of the
-// same runs (contiguous within a run).
+// with one packed atomic (+ one for the sum); each record is one pair, so its
+// rows go to the Linf bins (LDS) and its sum to the pair-sum range.  A chunk
+// of 1,024 buckets' runs is flattened by a workgroup scan, so every lane
+// reads a record of the same runs (contiguous within a run).
 template <bool HAS_VALUE>
 __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsigned* __restrict__ bstart,
                                                                const unsigned* __restrict__ pruns,
                                                                const PRec* __restrict__ prec,
-                                                               unsigned long long* pkstat, double* psum, int64_t per) {
+                                                               unsigned long long* pkstat, double* psum, IntHists H,
+                                                               unsigned long long* minmax, int64_t per) {
   __shared__ unsigned an[kHbRangeW], ar[kHbRangeW];
+  __shared__ unsigned lbins[kSmallBins];
   __shared__ double as[HAS_VALUE ? kHbRangeW : 1];
   __shared__ unsigned bex[kHbRangeThreads], bbase[kHbRangeThreads];
   __shared__ unsigned wsum[kHbRangeThreads / 64 + 1];
@@ -1125,6 +1229,8 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
     ar[p] = 0;
     if (HAS_VALUE) as[p] = 0.0;
   }
+  for (int i = threadIdx.x; i < kSmallBins; i += blockDim.x) lbins[i] = 0;
+  unsigned long long mn = ~0ULL, mx = 0ULL;
   const int64_t b0 = (int64_t)blockIdx.y * per;
   const int64_t b1 = b0 + per < t.nb ? b0 + per : t.nb;
   for (int64_t c0 = b0; c0 < b1; c0 += kHbRangeThreads) {  // workgroup-uniform
@@ -1132,8 +1238,11 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
     unsigned len = 0, base = 0;
     if (b < b1) {
       const unsigned s = pruns[b * (R + 1) + r], s1 = pruns[b * (R + 1) + r + 1];
-      base = bstart[b] + s;
-      len = s1 - s;
+      const unsigned rows = bstart[b + 1] - bstart[b];
+      if (s <= s1 && s1 <= rows) {  // a bucket's records lie inside its rows
+        base = bstart[b] + s;
+        len = s1 - s;
+      }
     }
     unsigned tot;
     const unsigned ex = hb_block_scan(len, wsum, &tot);  // its barriers also order the LDS clears
@@ -1152,10 +1261,22 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
       atomicAdd(an + p, 1u);
       atomicAdd(ar + p, rec.rows);
       if (HAS_VALUE) atomicAdd(as + p, rec.sum);
+      // Linf bins: the lanes holding the first active lane's value (most
+      // pairs have one row) add once, the others one by one
+      const unsigned long long act = __ballot(true);
+      const unsigned r0 = __shfl(rec.rows, __ffsll((long long)act) - 1, 64);
+      const unsigned long long same = __ballot(rec.rows == r0);
+      if (rec.rows != r0) int_hist_add(H, lbins, H_LINF, 0, rec.rows);
+      else if ((int)(threadIdx.x & 63) == __ffsll((long long)same) - 1) int_hist_add_n(H, lbins, H_LINF, 0, r0, __popcll(same));
+      const unsigned long long o = ord(rec.sum);
+      mn = o < mn ? o : mn;
+      mx = o > mx ? o : mx;
     }
     __syncthreads();
   }
+  block_minmax(mn, mx, minmax);  // contains __syncthreads
   __syncthreads();
+  flush_small(H, lbins, 0, H_LINF);
   for (int p = threadIdx.x; p < kHbRangeW; p += blockDim.x) {
     const unsigned n = an[p];
     if (!n) continue;
@@ -1536,7 +1657,9 @@ int hist_pairs_bucketed(const HCall& c, const int64_t* privacy_id, const int64_t
   else
     PDP_HLAUNCH("k_hb_l2", st, k_hb_l2<false>, dim3(g2), dim3(kHbL2Threads), 0, st, t, (const unsigned*)sbase,
                 (const unsigned long long*)key1, (const double*)val1, (const unsigned*)bcnt, bcur, key2, val2);
-  PDP_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)ctl, 1u, 1, st));  // mode: bucketed
+  // mode: 1 = pair-sum list, 2 = privacy-id buckets' range-grouped records (+ R in word 3)
+  PDP_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)ctl, pid_buckets && t.hb_R ? 2u : 1u, 1, st));
+  if (pid_buckets && t.hb_R) PDP_HIP_CHECK(hipMemsetD32Async((hipDeviceptr_t)(ctl + 3), (unsigned)t.hb_R, 1, st));
   unsigned long long* pidstat = (unsigned long long*)(ws + w.pidstat);
   unsigned long long* pkstat = (unsigned long long*)(ws + w.pkstat);
   double* psum = (double*)(ws + w.psum);
@@ -1572,10 +1695,10 @@ int hist_pairs_bucketed(const HCall& c, const int64_t* privacy_id, const int64_t
       const PRec* pr = prec;
       if (hv)
         PDP_HLAUNCH("k_hb_prange", st, k_hb_prange<true>, dim3((unsigned)t.hb_R, (unsigned)G), dim3(kHbRangeThreads),
-                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, per);
+                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, c.H, minmax, per);
       else
         PDP_HLAUNCH("k_hb_prange", st, k_hb_prange<false>, dim3((unsigned)t.hb_R, (unsigned)G), dim3(kHbRangeThreads),
-                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, per);
+                    0, st, t, (const unsigned*)bcnt, (const unsigned*)pruns, pr, pkstat, psum, c.H, minmax, per);
     }
     return PDP_OK;
   }
@@ -1699,7 +1822,9 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   int64_t gf = (mf + kFloatBlock - 1) / kFloatBlock;
   gf = gf < cus ? gf : cus;
   PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, (const Slot*)(ws + w.slots),
-              (const double*)(w.hb_pairsum ? ws + w.hb_pairsum : nullptr), (const unsigned*)(ws + w.hb_ctl), pkstat,
+              (const double*)(w.hb_pairsum ? ws + w.hb_pairsum : nullptr), (const unsigned*)(ws + w.hb_ctl),
+              (const unsigned*)(w.hb_bcnt ? ws + w.hb_bcnt : nullptr),
+              (const unsigned*)(w.hb_pruns ? ws + w.hb_pruns : nullptr), (const PRec*)(ws + w.slots), pkstat,
               psum, out->float_lowers, out->float_n_lowers, c.F);
   PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
               c.F, out->float_max, 0x1F);

@@ -202,8 +202,11 @@ def test_out_of_range_codes_raise():
 
 
 def test_full_size_invariants():
-    """1e8 rows (C2's shape): totals every histogram must satisfy, checked
-    against torch group-bys on the device."""
+    """1e8 rows (C2's shape, the bench's hist workload): totals every
+    histogram must satisfy, checked against torch group-bys on the device;
+    and the default privacy-id buckets give exactly the bins of the HBM pair
+    table (PDP_HIST_FORCE_PAIR_TABLE), which the small cases pin to the
+    oracle (quarter-integer values: every sum exact in any order)."""
     import torch
     d = _dev()
     n, U, P = 100_000_000, 1_000_000, 100_000
@@ -213,10 +216,17 @@ def test_full_size_invariants():
     val = torch.randint(-8, 9, (n,), device=d, generator=g).to(torch.float64) / 4
     raw = X.dataset_histograms(pid, pk, val, n_privacy_ids=U, n_partitions=P)
     h = CH.histograms_from_device(raw)
+    del raw
+    ref = CH.histograms_from_device(X.dataset_histograms(pid, pk, val, n_privacy_ids=U, n_partitions=P,
+                                                         force_pair_table=True))
+    for field in OH.HIST_FIELDS:
+        got = [(b.lower, b.upper, b.count, b.sum, b.max) for b in getattr(h, field).bins]
+        want = [(b.lower, b.upper, b.count, b.sum, b.max) for b in getattr(ref, field).bins]
+        assert got == want, field
     n_pairs = int(torch.unique(pid * P + pk).numel())
     n_pids = int(torch.unique(pid).numel())
     total = float(val.sum().item())
-    del pid, pk, raw
+    del pid, pk
     assert h.l1_contributions_histogram.total_sum() == n
     assert h.l1_contributions_histogram.total_count() == n_pids
     assert h.linf_contributions_histogram.total_sum() == n
