@@ -213,28 +213,39 @@ __device__ __forceinline__ double secure_laplace(const pdp_noise_params& np, uin
 // uses Google's approximate binomial probability (Secure Noise Generation,
 // Lemma 7).  Two Philox blocks per attempt: (x, y) geometric bits, z sign;
 // then (x, y) the uniform offset in [0, step), (z, w) the acceptance uniform.
+// one attempt (Philox blocks k, k + 1; k advances by 2): true and *md = the
+// binomial offset if accepted.  About 1 in 16 attempts is accepted, so a
+// kernel drawing many samples runs attempts, not samples, per loop trip
+// (k_select_gauss) to keep a wave's lanes busy.
+__device__ __forceinline__ bool gaussian_attempt(const pdp_noise_params& np, uint64_t seed, int64_t gidx,
+                                                 uint32_t slot, uint32_t& k, double* md_out) {
+  const uint64_t step = (uint64_t)np.step;
+  const U4 a = noise_block(seed, gidx, slot, k++);
+  const U4 b = noise_block(seed, gidx, slot, k++);
+  int geom;
+  if (a.x != 0xFFFFFFFFu) geom = __clz(~a.x);
+  else if (a.y != 0xFFFFFFFFu) geom = 32 + __clz(~a.y);
+  else geom = 64;  // probability 2^-64: capped
+  const int64_t two_sided = (a.z >> 31) ? (int64_t)geom : -(int64_t)geom - 1;
+  // floor(r * step / 2^64) for the 64 random bits r = (b.x, b.y); step < 2^32
+  const uint64_t hi_part = (uint64_t)b.x * step + (((uint64_t)b.y * step) >> 32);
+  const int64_t uni = (int64_t)(hi_part >> 32);
+  const int64_t m = (int64_t)step * two_sided + uni;
+  const double accept_u = u01(b.z, b.w);
+  const double md = (double)m;
+  *md_out = md;
+  if (fabs(md) > np.bound) return false;
+  const double prob = np.coef * exp(-2.0 * md * md / np.n) * np.corr;
+  return prob > 0.0 && accept_u < prob * (double)np.step * ldexp(1.0, geom) / 4.0;
+}
+
 __device__ __forceinline__ double secure_gaussian(const pdp_noise_params& np, uint64_t seed, int64_t gidx,
                                                   uint32_t slot) {
   uint32_t k = 0;
-  const uint64_t step = (uint64_t)np.step;
-  for (;;) {
-    const U4 a = noise_block(seed, gidx, slot, k++);
-    const U4 b = noise_block(seed, gidx, slot, k++);
-    int geom;
-    if (a.x != 0xFFFFFFFFu) geom = __clz(~a.x);
-    else if (a.y != 0xFFFFFFFFu) geom = 32 + __clz(~a.y);
-    else geom = 64;  // probability 2^-64: capped
-    const int64_t two_sided = (a.z >> 31) ? (int64_t)geom : -(int64_t)geom - 1;
-    // floor(r * step / 2^64) for the 64 random bits r = (b.x, b.y); step < 2^32
-    const uint64_t hi_part = (uint64_t)b.x * step + (((uint64_t)b.y * step) >> 32);
-    const int64_t uni = (int64_t)(hi_part >> 32);
-    const int64_t m = (int64_t)step * two_sided + uni;
-    const double accept_u = u01(b.z, b.w);
-    const double md = (double)m;
-    if (fabs(md) > np.bound) continue;
-    const double prob = np.coef * exp(-2.0 * md * md / np.n) * np.corr;
-    if (prob > 0.0 && accept_u < prob * (double)np.step * ldexp(1.0, geom) / 4.0) return md * np.granularity;
+  double md;
+  while (!gaussian_attempt(np, seed, gidx, slot, k, &md)) {
   }
+  return md * np.granularity;
 }
 
 // mechanism.add_noise(x): x snapped to the grid plus a grid-valued sample

@@ -75,6 +75,56 @@ __global__ void __launch_bounds__(kBlock) k_select(pdp_select_config cfg, const 
   }
 }
 
+// Laplace / Gaussian thresholding with Gaussian noise: the rejection sampler
+// takes ~16 attempts per sample (geometric), so a lane per partition leaves a
+// wave waiting ~74 attempts for its slowest lane.  Here each loop trip is one
+// attempt and a lane whose sample was accepted moves on to its next partition
+// (grid-stride), so the lanes' trips even out over ~20 partitions each.  Same
+// Philox blocks per partition as secure_add_noise, so the same draws.
+__global__ void __launch_bounds__(kBlock) k_select_gauss(pdp_select_config cfg, const int64_t* __restrict__ row_count,
+                                                         uint8_t* __restrict__ keep, double* __restrict__ noised) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const double g = cfg.noise.granularity;
+  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool fresh = true;
+  uint32_t k = 0;
+  double base = 0.0, shift = 0.0;
+  while (p < cfg.n_partitions) {
+    if (fresh) {
+      fresh = false;
+      k = 0;
+      const int64_t rc = row_count[p];
+      const int64_t mr = cfg.max_rows_per_privacy_id > 0 ? cfg.max_rows_per_privacy_id : 1;
+      int64_t n = (rc + mr - 1) / mr;
+      bool live = rc > 0;
+      int64_t sh = 0;
+      if (live && cfg.pre_threshold > 0) {
+        if (n < cfg.pre_threshold) live = false;
+        sh = cfg.pre_threshold - 1;
+        n -= sh;
+      }
+      if (!live) {
+        keep[p] = 0;
+        if (noised) noised[p] = __builtin_nan("");
+        p += stride;
+        fresh = true;
+        continue;
+      }
+      base = round_to_multiple((double)n, g);
+      shift = (double)sh;
+    }
+    double md;
+    if (gaussian_attempt(cfg.noise, cfg.seed, cfg.partition_offset + p, 0x53454C00u, k, &md)) {
+      const double v = base + md * g;
+      const bool kp = v > cfg.threshold;
+      keep[p] = kp;
+      if (noised) noised[p] = kp ? v + shift : __builtin_nan("");
+      p += stride;
+      fresh = true;
+    }
+  }
+}
+
 constexpr int kCompactItems = 16;
 constexpr int kCompactChunk = kBlock * kCompactItems;
 
@@ -336,9 +386,16 @@ int pdp_select_partitions(const pdp_select_config* cfg, const int64_t* row_count
     if (rc != PDP_OK) return rc;
   }
   if (cfg->n_partitions == 0) return PDP_OK;
+  const bool gauss = (cfg->strategy == PDP_SELECT_LAPLACE_THRESHOLDING ||
+                      cfg->strategy == PDP_SELECT_GAUSSIAN_THRESHOLDING) &&
+                     cfg->noise.kind == PDP_NOISE_GAUSSIAN && cfg->noise.granularity != 0.0;
   PDP_PROF_BEGIN("k_select", (hipStream_t)stream);
-  hipLaunchKernelGGL(k_select, dim3(grid_for(cfg->n_partitions)), dim3(kBlock), 0, (hipStream_t)stream,
-                     *cfg, row_count, keep, noised_count);
+  if (gauss)  // ~20 partitions per lane (a full chip: 2,048 workgroups of 4 waves)
+    hipLaunchKernelGGL(k_select_gauss, dim3(grid_for(cfg->n_partitions, 2048)), dim3(kBlock), 0, (hipStream_t)stream,
+                       *cfg, row_count, keep, noised_count);
+  else
+    hipLaunchKernelGGL(k_select, dim3(grid_for(cfg->n_partitions)), dim3(kBlock), 0, (hipStream_t)stream,
+                       *cfg, row_count, keep, noised_count);
   PDP_PROF_END((hipStream_t)stream);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
