@@ -283,12 +283,16 @@ def run_api_workload(args, workload, world, rank, device):
     n, U, P = args.rows or w["rows"], args.privacy_ids or w["privacy_ids"], w["partitions"]
     gen = gen_c4 if workload == "c4" else gen_c5
     pid, pk, value = gen(n, U, P, rank, device, 4000 if workload == "c4" else 5000)
-    pid += rank * U  # privacy ids of different ranks are different people
+    # local privacy-id codes k in [0, U), dataset-wide id r * U + k (as in
+    # gen_c3): a rank's table is dense in its own ids, so its bounding plan
+    # is the one-GPU plan (global codes in [0, U * world) would give 8x the
+    # buckets at N = 8, past the bucketed plan's limit: the global-sketch path)
     torch.cuda.synchronize()
-    # the default privacy_id_sharding="verify", once, before timing (the
-    # steps below pass "trusted": the check does not change between steps)
-    verify_ms = verify_sharding(pid, world)
-    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U * world, n_partitions=P)
+    # the default privacy_id_sharding="verify" on the dataset-wide ids, once,
+    # before timing (the steps below pass "trusted": the check does not
+    # change between steps)
+    verify_ms = verify_sharding(pid, world, rank * U)
+    table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U, n_partitions=P)
     strategy = {"truncated_geometric": pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC,
                 "gaussian": pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING,
                 "laplace": pdp.PartitionSelectionStrategy.LAPLACE_THRESHOLDING}[args.strategy]

@@ -576,10 +576,19 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
   const LinBins z0 = lin_bins(lowers, nl0);
+  // the last bin's maximum is the global maximum mx, and bin 0's is at least
+  // the global minimum mn when mn falls in bin 0: set up front, so the copies
+  // of a clipped value (mn / mx: ~5 % of the values each for N(5, 3) clipped
+  // to [0, 10]) send nothing; every other value goes through the filter
+  if (nl0 > 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+    atomicMax(F.omax + (z0.nb - 1), ord(z0.mx));
+    if (lin_bin(z0, z0.mn) == 0) atomicMax(F.omax, ord(z0.mn));
+  }
   auto add = [&](double v) {
     const int b = lin_bin(z0, v);
     atomicAdd(lcnt + b, 1u);
     atomicAdd(lsum + b, v);
+    if (b == z0.nb - 1 || (b == 0 && v == z0.mn)) return;
     const unsigned long long o = ord(v);
     const unsigned hi = (unsigned)(o >> 32);
     const unsigned cur = lmx[b];

@@ -144,7 +144,8 @@ def test_sieve_plan(lib):
     assert info.sieve == 0
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=1 << 20)), ctypes.byref(info)) == 0
     assert info.sieve == 1 << 15
-    assert lib.pdp_bound_plan(ctypes.byref(_cfg(n_privacy_ids=5000, sieve=4096)), ctypes.byref(info)) == 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(n_rows=1_000_000, n_privacy_ids=5000, sieve=4096)),
+                              ctypes.byref(info)) == 0
     assert info.sieve == 0  # one bucket level: no tile-local level 1
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(merge=N.MERGE_ATOMIC, sieve=4096)), ctypes.byref(info)) == 0
     assert info.sieve == 0  # the fix-up appends pair records: range merge only

@@ -41,7 +41,7 @@ def _run_codes(pid, pk, val, U=None, P=None, mode="auto"):
 
 
 @pytest.mark.parametrize("case", ["uniform", "zipf_pids", "heavy_pairs", "int_values", "no_values",
-                                  "wide_partitions", "zipf_partitions"])
+                                  "wide_partitions", "zipf_partitions", "clipped"])
 def test_pair_phases_agree_with_oracle(case):
     """The three pairs phases of pdp_hist.hip -- rows hashed into privacy-id
     buckets (default; pid counters in LDS, partition records summed per
@@ -52,7 +52,7 @@ def test_pair_phases_agree_with_oracle(case):
     super-buckets).  "zipf_pids" has privacy ids with 10^4..10^6 rows, whose
     privacy-id buckets overflow: the default call falls back to pair buckets."""
     rng = np.random.default_rng({"uniform": 11, "zipf_pids": 12, "heavy_pairs": 13, "int_values": 14,
-                                 "no_values": 15, "wide_partitions": 16, "zipf_partitions": 17}[case])
+                                 "no_values": 15, "wide_partitions": 16, "zipf_partitions": 17, "clipped": 18}[case])
     n = 3_000_000
     pid = rng.integers(0, 200_000, n)
     pk = rng.integers(0, 40_000, n)
@@ -70,6 +70,8 @@ def test_pair_phases_agree_with_oracle(case):
         val = rng.integers(-20, 60, n)
     if case == "no_values":
         val = None
+    if case == "clipped":  # the bench's values: ~5 % of the pair sums tie at each end
+        val = np.clip(np.round(rng.normal(5, 3, n) * 8) / 8, 0.0, 10.0)
     want = OH.dataset_histograms(pid, pk, np.zeros(n) if val is None else val)
     for mode in ("auto", "pair_hash", "pair_table"):
         got = _run_codes(pid, pk, val, mode=mode)

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Runs the bench once per library variant in abv (TAG = $1)
+# Runs the bench once per library variant in abv (TAG = $1; extra bench flags in $BENCH_ARGS)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -7,7 +7,7 @@ OUT=gpurun_out/${1:-variants}
 mkdir -p $OUT
 for so in abv/*.so; do
   v=$(basename $so .so)
-  PIPELINEDP_AMD_LIB=$PWD/$so timeout -k 10 240 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/$v.log 2>&1 || { echo "variant $v failed"; tail -5 $OUT/$v.log; exit 1; }
+  PIPELINEDP_AMD_LIB=$PWD/$so timeout -k 10 240 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline $BENCH_ARGS > $OUT/$v.log 2>&1 || { echo "variant $v failed"; tail -5 $OUT/$v.log; exit 1; }
   python3 - $OUT/$v.log $v <<'PY'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
