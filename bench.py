@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
+    ap.add_argument("--sieve-band", type=int, default=0,
+                    help="the sieve's side band (0 auto, -1 off; pdp_bound_config.sieve_band)")
     ap.add_argument("--sieve", type=int, default=0,
                     help="threshold sieve t * 2^16 (0 auto, -1 off; pdp_bound_config.sieve)")
     ap.add_argument("--strategy", choices=("truncated_geometric", "gaussian", "laplace"),
@@ -492,16 +494,26 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
     out = {}
     # level 1 reads the two key columns once and writes one record per row
     # that goes on (the tile-local form needs no histogram pass over ids)
-    out["k_sieve_l1" if plan.sieve else "k_scatter_l1"] = 16.0 * n + rec1 * cand
+    band = stats.get("band_rows", 0)
+    # (with the side band, level 1 also writes one (id, row) entry per band row)
+    out["k_sieve_l1" if plan.sieve else "k_scatter_l1"] = 16.0 * n + rec1 * cand + 8.0 * band
     out["k_scatter_l2"] = (rec1 + rec2) * cand
     # B1 streams the level-2 keys; kept rows' indices and values are
     # gathered; one record per kept pair out
     out["k_bucket_bound"] = key2 * cand + 12.0 * kept_rows + pair_rec * kept_pairs
     if plan.sieve:
-        # privacy ids in, (id, row) per fix-up row out; with no unresolved
-        # privacy id the rescan exits before reading anything
-        out["k_sieve_rescan"] = (8.0 * n + 8.0 * fix) if stats.get("unresolved_ids", 1) else 0.0
-        out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * fix      # list in, partition gathered, record out
+        fix2 = stats.get("fixup2_rows", 0)
+        if getattr(plan, "band", 0):
+            # the band lists in (when some id is unresolved), the ids still
+            # unresolved after them re-read from the privacy-id column
+            out["k_band_scan"] = 8.0 * band if stats.get("unresolved_ids", 1) else 0.0
+            out["k_sieve_rescan"] = (8.0 * n + 8.0 * fix2) if stats.get("unresolved2_ids", 1) else 0.0
+            out["k_bucket_fix2"] = key2 * fix2
+        else:
+            # privacy ids in, (id, row) per fix-up row out; with no unresolved
+            # privacy id the rescan exits before reading anything
+            out["k_sieve_rescan"] = (8.0 * n + 8.0 * fix) if stats.get("unresolved_ids", 1) else 0.0
+        out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * (fix + fix2)  # list in, partition gathered, record out
         out["k_bucket_fix"] = key2 * fix
     out["k_range_reduce"] = 2.0 * pair_rec * kept_pairs
     return out
@@ -572,7 +584,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
 
     P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
-    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format, sieve=args.sieve)
+    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
     acc = X.new_accumulators(P_pad, bounding, device)
     seed_base = parallel.broadcast_seeds((int.from_bytes(os.urandom(8), "little"),))[0]
 
@@ -582,7 +594,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                 t.zero_()
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
-                           check_keys=False, key_format=args.key_format, sieve=args.sieve)
+                           check_keys=False, key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
         mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
@@ -607,7 +619,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     # key-error check of the data once (outside the timed region)
     X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding, seed=1,
                        row_offset=rank * n, acc=acc, workspace=ws, check_keys=True,
-                       key_format=args.key_format, sieve=args.sieve)
+                       key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
     # per-kernel times from a second, untimed pass of the same steps: the HIP
     # events the profiler records around every launch (on its launch stream)
     # would otherwise sit inside the timed region
@@ -681,7 +693,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                        "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
                        "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(
                            plan.key_format, plan.key_format),
-                       "sieve": plan.sieve / 65536.0, "stats": stats},
+                       "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0, "stats": stats},
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,
     }

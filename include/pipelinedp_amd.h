@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 9
+#define PDP_ABI_VERSION 10
 
 /* error codes */
 #define PDP_OK 0
@@ -80,7 +80,10 @@ typedef struct pdp_bound_config {
                                 1..32768 = keep rows whose 32-bit pair hash is below sieve * 2^16
                                 (candidate fraction t = sieve / 2^16 <= 1/2) through the partition
                                 passes; privacy ids with < l0 candidate pairs are finished from a
-                                re-read of the privacy-id column */
+                                side band or a re-read of the privacy-id column */
+  int32_t sieve_band;        /* with the sieve: 0 = auto (level 1 also lists the rows whose pair hash
+                                is below 2t, and the fix-up reads that list; only ids with < l0
+                                pairs below 2t re-read the privacy-id column), < 0 = off */
 } pdp_bound_config;
 
 /* bounds up to int32; above 256 (l0, linf) the pair-table algorithm runs, and
@@ -135,6 +138,7 @@ typedef struct pdp_bound_plan_info {
   int64_t range_group; /* PDP_MERGE_RANGES: records per range-reduce work item */
   int32_t key_format;  /* resolved PDP_KEYS_* (BUCKETED) */
   int32_t sieve;       /* resolved threshold sieve, t = sieve / 2^16 (0 = off) */
+  int32_t band;        /* resolved side band, t2 = band / 2^16 (0 = off) */
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */
@@ -310,7 +314,9 @@ int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
 /* What the last pdp_bound_contributions (BUCKETED) moved, read from its
  * workspace (synchronises `stream`): rows that entered the partition passes
  * (every live row, or the sieve's candidates), privacy ids the sieve left
- * unresolved and the rows of those ids its fix-up re-read.  Diagnostics for
+ * unresolved and the rows of those ids its fix-up gathered (from the side
+ * band's list and the candidates, or the re-read), the band's rows, the ids
+ * the band left unresolved and their re-read rows.  Diagnostics for
  * the measurement (bench.py's algorithmic bytes); zeros for other
  * algorithms. */
 typedef struct pdp_bound_stats {
@@ -319,6 +325,11 @@ typedef struct pdp_bound_stats {
   int64_t fixup_rows;
   int32_t sieve;        /* resolved sieve (pdp_bound_plan_info.sieve) */
   uint32_t error_flags; /* pdp_bound_error_flags */
+  int64_t band_rows;    /* side band: rows level 1 listed (t <= pair hash < t2) */
+  int64_t unresolved2_ids; /* side band: ids still unresolved after it (< l0 pairs below t2) */
+  int64_t fixup2_rows;  /* their rows, from the re-read of the privacy-id column */
+  int32_t band;         /* resolved side band (pdp_bound_plan_info.band) */
+  int32_t reserved;
 } pdp_bound_stats;
 
 int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,

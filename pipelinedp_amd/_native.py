@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 9
+ABI_VERSION = 10
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
@@ -94,6 +94,7 @@ class BoundConfig(ctypes.Structure):
         ("rows_are_units", ctypes.c_int32),
         ("key_format", ctypes.c_int32),
         ("sieve", ctypes.c_int32),
+        ("sieve_band", ctypes.c_int32),
     ]
 
 
@@ -111,6 +112,7 @@ class BoundPlanInfo(ctypes.Structure):
         ("range_group", ctypes.c_int64),
         ("key_format", ctypes.c_int32),
         ("sieve", ctypes.c_int32),
+        ("band", ctypes.c_int32),
     ]
 
 
@@ -121,6 +123,11 @@ class BoundStats(ctypes.Structure):
         ("fixup_rows", ctypes.c_int64),
         ("sieve", ctypes.c_int32),
         ("error_flags", ctypes.c_uint32),
+        ("band_rows", ctypes.c_int64),
+        ("unresolved2_ids", ctypes.c_int64),
+        ("fixup2_rows", ctypes.c_int64),
+        ("band", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 

@@ -33,6 +33,7 @@
 //    updated with device-scope atomics.
 #include <algorithm>
 #include <type_traits>
+#include <vector>
 
 #include "pdp_internal.h"
 
@@ -141,8 +142,15 @@ static_assert(kTileRows / kSieveChunk <= kStagesPerTile ||
               "sieve flushes per tile");
 static_assert(kSieveCap <= 65535, "u16 run offsets");
 size_t sieve_stage_bytes(int key_format);  // LDS of the sieve's level-1 stage (after StageLds)
-inline bool sieve_hist_u16(int key_format, int64_t n_buckets) {
-  return (int64_t)sieve_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) > kL1LocalLds;
+// the side band (Plan.band): rows with t <= pair hash < t2 = 2t leave level 1
+// as (privacy id << 32 | row) in a per-tile list, through a per-wave LDS queue
+// written out 64 entries at a time; the fix-up reads that list instead of the
+// whole privacy-id column, and only a privacy id with fewer than l0 distinct
+// pairs below t2 still needs the rescan
+constexpr int kBandQueue = 128;
+constexpr int64_t kBandLds = (kL1Threads / 64) * kBandQueue * 8;
+inline bool sieve_hist_u16(int key_format, int64_t n_buckets, bool band) {
+  return (int64_t)sieve_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) + (band ? kBandLds : 0) > kL1LocalLds;
 }
 
 struct Plan {
@@ -167,8 +175,9 @@ struct Plan {
   int l1_local;         // tile-local level 1 (k_scatter_l1_local / k_scatter_l2_local), no histogram pass
   int64_t n_stages;     // level-1 stages of kL1Rows rows
   int sieve;            // threshold sieve: t = sieve / 2^16 (0 = off); k_sieve_l1 instead of k_scatter_l1_local
+  int band;             // side band: t2 = band / 2^16 (0 = off; else 2 * sieve, <= 1/2)
   int64_t n_slots1;     // level-1 blocks (stages, or sieve flush slots: n_tiles * kStagesPerTile)
-  int64_t buckets_out;  // buckets of pair records: n_buckets, 2 * n_buckets with the sieve (fix-up after)
+  int64_t buckets_out;  // buckets of pair records: n_buckets, x2 with the sieve (fix-up after), x3 with the band
   int l2_mult;          // tile groups per level-2 workgroup (1 without the sieve)
 };
 
@@ -298,8 +307,14 @@ Plan make_plan(const pdp_bound_config* c) {
     if (t <= 0.35) t16 = (int)std::ceil(t * 65536.0);
   }
   p.sieve = t16 > 0 ? t16 : 0;
+  p.band = 0;
+  if (p.sieve) {
+    const int t2 = 2 * p.sieve < kSieveMaxT16 ? 2 * p.sieve : kSieveMaxT16;
+    const bool fits = (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) + kBandLds <= kL1LocalLds;
+    if (t2 > p.sieve && fits && c->sieve_band >= 0) p.band = t2;
+  }
   p.n_slots1 = p.sieve ? p.n_tiles * kStagesPerTile : p.n_stages;
-  p.buckets_out = p.sieve ? 2 * p.n_buckets : p.n_buckets;
+  p.buckets_out = p.sieve ? (p.band ? 3 : 2) * p.n_buckets : p.n_buckets;
   p.l2_mult = 1;
   if (p.sieve) {
     // expected records of one (group of kL2GroupTiles tiles, super-bucket)
@@ -345,6 +360,10 @@ struct Ws {
   // bucket (-> starts) and their write cursors; the fix-up row list itself
   // reuses keys1 (dead after level 2), its bucket-ordered records keys2/rows2
   uint64_t sbase, unres_bits, unres_list, sctl, fix_cnt, fix_cur;
+  // side band: per-tile (pid << 32 | row) lists and their lengths; the ids
+  // still unresolved after the band fix-up (bitmap, list, {count, rows}) and
+  // their rescan's per-bucket counts / cursors
+  uint64_t band, band_cnt, unres2_bits, unres2_list, sctl2, fix_cnt2, fix_cur2;
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -375,7 +394,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
-    const bool u16 = p.sieve ? sieve_hist_u16(p.key_format, p.n_buckets) : l1_hist_u16(p.key_format, p.n_buckets);
+    const bool u16 = p.sieve ? sieve_hist_u16(p.key_format, p.n_buckets, p.band != 0) : l1_hist_u16(p.key_format, p.n_buckets);
     if (p.l1_local && u16) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
@@ -403,6 +422,15 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.sctl = off; off = align256(off + 16);
       w.fix_cnt = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
       w.fix_cur = off; off = align256(off + (uint64_t)p.n_buckets * 4);
+      if (p.band) {  // the band lists; the second fix-up's unresolved ids and counts
+        w.band = off; off = align256(off + (uint64_t)p.n_tiles * kTileRows * 8);
+        w.band_cnt = off; off = align256(off + (uint64_t)p.n_tiles * 4);
+        w.unres2_bits = off; off = align256(off + ids / 8);
+        w.unres2_list = off; off = align256(off + ids * 4);
+        w.sctl2 = off; off = align256(off + 16);
+        w.fix_cnt2 = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
+        w.fix_cur2 = off; off = align256(off + (uint64_t)p.n_buckets * 4);
+      }
     }
     if (p.super_bits > 0) {
       w.keys2 = off; off = align256(off + n * kb2);
@@ -487,6 +515,8 @@ struct KP {  // kernel parameters
   int l2_group_mult;    // tile groups per level-2 workgroup
   uint32_t sieve_t32;   // threshold sieve: candidate rows have pair_hash < sieve_t32 (0 = off)
   int sieve_mark;       // bucket kernel: mark privacy ids with < l0 candidate pairs unresolved
+  uint32_t band_t32;    // side band: level 1 lists rows with sieve_t32 <= pair_hash < band_t32 (0 = off)
+  int sieve_emit;       // bucket kernel (main launch, band on): unresolved ids' candidate rows -> fix_rec
 };
 
 KP make_kp(const pdp_bound_config* c, const Plan& p) {
@@ -511,6 +541,8 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.l2_group_mult = p.l2_mult;
   k.sieve_t32 = (uint32_t)p.sieve << 16;
   k.sieve_mark = p.sieve != 0;
+  k.band_t32 = (uint32_t)p.band << 16;
+  k.sieve_emit = p.band != 0;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -1360,10 +1392,20 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
 // the tile's unused slots get empty runs.  Rows with invalid keys set the
 // error word; dead rows (non-public partitions) are simply dropped.  The
 // tile's candidate counts per bucket feed the level-2 cursors as before.
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 #ifdef PDP_PHASE_CLOCK
 __device__ unsigned g_phase_l1, g_phase_l2, g_phase_bk;  // profiling builds: prints so far per kernel
 #endif
-template <int FMT, bool U16>
+// BAND: rows with sieve_t32 <= pair hash < band_t32 also go, as (privacy id
+// << 32 | row), to this tile's band list band[t * 65,536 ...], through a
+// per-wave LDS queue flushed 64 entries (512 contiguous bytes) at a time;
+// band_cnt[t] = the list's length
+template <int FMT, bool U16, bool BAND>
 __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
                                                          const int64_t* __restrict__ pk,
                                                          const uint8_t* __restrict__ allowed,
@@ -1371,7 +1413,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
                                                          unsigned* __restrict__ counts_tm2,
                                                          uint16_t* __restrict__ soff, unsigned* __restrict__ sbase,
                                                          L1Key<FMT>* __restrict__ keys1,
-                                                         unsigned* __restrict__ rows1, unsigned* err) {
+                                                         unsigned* __restrict__ rows1, unsigned* err,
+                                                         unsigned long long* __restrict__ band,
+                                                         unsigned* __restrict__ band_cnt) {
   using K = L1Key<FMT>;
   constexpr bool ROWS = !kPackedL1<FMT>;
   constexpr int Q = kSieveChunkItems;
@@ -1379,10 +1423,16 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   using SL = StageLds<K, kSmallDest, ROWS, kSieveItems, kL1Threads>;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
   unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);
-  __shared__ unsigned fill;
+  // BAND: the per-wave queues after the bucket counts (l1_hist_bytes)
+  unsigned long long* const bq =
+      stage_raw + (sizeof(SL) + 7) / 8 + (((U16 ? 2 : 4) * kp.n_buckets + 15) / 16 * 16) / 8;
+  __shared__ unsigned fill, bfill;
   const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
   for (int64_t b = threadIdx.x; b < n_words; b += blockDim.x) bh[b] = 0;
-  if (threadIdx.x == 0) fill = 0;
+  if (threadIdx.x == 0) {
+    fill = 0;
+    bfill = 0;
+  }
   __syncthreads();
   auto flush_counts = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
     for (int64_t wd = threadIdx.x; wd < n_words; wd += blockDim.x) {
@@ -1406,6 +1456,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   const unsigned long long below = (1ULL << lane) - 1;
   K* const blk = keys1 + t * kSieveTileStride;
   unsigned* const rblk = ROWS ? rows1 + t * kSieveTileStride : nullptr;
+  unsigned long long* const band_tile = BAND ? band + t * kTileRows : nullptr;
+  unsigned long long* const wq = bq + (threadIdx.x >> 6) * kBandQueue;
+  int qn = 0;            // wave-uniform: entries waiting in this wave's band queue
   unsigned written = 0;  // block-uniform: this tile's records already written
   int slot = 0;
   // the stage's `total` records -> counting sort by super-bucket -> block
@@ -1509,7 +1562,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
     // ahead go out, then append / flush -- two chunks of loads in flight
     auto body = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
       const bool more = c0 + kSieveChunk < t1;  // block-uniform
-      bool cand[Q];
+      bool cand[Q], bnd[Q];
       int d[Q];
       K x[Q];
       uint8_t pub[Q];  // public partitions: the rows' mask bytes, gathered together (one wait)
@@ -1528,7 +1581,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         // every term evaluated (no short circuit: no branch, no per-row load wait);
         // a non-public partition's rows are dropped
         bool c = valid & in_range & (pub[q] != 0);
-        c = c & (pair_hash(kp.seed, u[q], k[q]) < t32);
+        const uint32_t h = pair_hash(kp.seed, u[q], k[q]);
+        bnd[q] = BAND && (c & (h >= t32) & (h < kp.band_t32));
+        c = c & (h < t32);
         cand[q] = c;
         d[q] = (int)(u[q] >> mid_bits);
         if constexpr (FMT == PDP_KEYS_COMPACT) {
@@ -1564,6 +1619,29 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         }
         base += (unsigned)__popcll(m[q]);
       }
+      if constexpr (BAND) {  // band rows -> the wave's queue; 64 of them out at once
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          const unsigned long long mb = __ballot(bnd[q]);
+          if (mb == 0) continue;  // wave-uniform
+          const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+          if (bnd[q]) wq[qn + __popcll(mb & below)] = ((unsigned long long)(uint32_t)u[q] << 32) | (uint32_t)i;
+          qn += __popcll(mb);
+          if (qn >= 64) {
+            wave_lds_fence();
+            const unsigned long long e = wq[lane];
+            unsigned bb = 0;
+            if (lane == 0) bb = atomicAdd(&bfill, 64u);
+            bb = __shfl(bb, 0, 64);
+            band_tile[bb + lane] = e;
+            const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
+            wave_lds_fence();
+            if (lane + 64 < qn) wq[lane] = rest;
+            qn -= 64;
+            wave_lds_fence();
+          }
+        }
+      }
       __syncthreads();
       const unsigned f = fill;
       if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
@@ -1595,6 +1673,17 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   if (kp.keys_vec && t1 - t0 == kTileRows) run(std::true_type{});
   else run(std::false_type{});
   if (bad) atomicOr(err, 1u);
+  if constexpr (BAND) {  // the queues' rest; the tile's list length
+    wave_lds_fence();
+    if (qn > 0) {
+      unsigned bb = 0;
+      if (lane == 0) bb = atomicAdd(&bfill, (unsigned)qn);
+      bb = __shfl(bb, 0, 64);
+      if (lane < qn) band_tile[bb + lane] = wq[lane];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) band_cnt[t] = bfill;
+  }
 #ifdef PDP_PHASE_CLOCK
   if (threadIdx.x == 0 && blockIdx.x % 1999 == 5 && atomicAdd(&g_phase_l1, 1u) < 40u)
     printf("l1 tile %d slots %d records %u total %llu flush %llu (10 ns)\n", (int)t, slot, written,
@@ -1814,12 +1903,6 @@ struct WaveQueue {
   unsigned* row;            // [kQueueCap]
 };
 
-__device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // Streams the rows [begin, end) of one bucket: conv(record) gives the row's
 // pair key, pred(key) selects candidates, work(key, row) handles each
 // candidate on compacted wavefronts.  R = 16 / sizeof(K) rows per lane per
@@ -1986,24 +2069,54 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
                                                                  unsigned* __restrict__ cand_idx,
                                                                  unsigned* __restrict__ unres_bits,
                                                                  unsigned* __restrict__ unres_list,
-                                                                 unsigned* __restrict__ sctl, unsigned* __restrict__ err) {
+                                                                 unsigned* __restrict__ sctl, unsigned* __restrict__ err,
+                                                                 unsigned long long* __restrict__ fix_rec,
+                                                                 const unsigned* __restrict__ unres_prev) {
   extern __shared__ unsigned long long smem[];
 #ifdef PDP_PHASE_CLOCK
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
   if (threadIdx.x == 0) ph[0] = wall_clock64();
 #endif
-  // an empty bucket of the sieve's fix-up launch (most of them: only
-  // unresolved privacy ids have rows there) writes its empty runs and stops;
-  // the main launch's empty buckets still mark their privacy ids unresolved
-  if (!kp.sieve_mark && offsets[blockIdx.x] == offsets[blockIdx.x + 1]) {  // block-uniform
-    if (RANGES) {
-      unsigned* const run0 = rec.runs + (int64_t)blockIdx.x * (kp.n_ranges + 1);
-      for (int t = threadIdx.x; t <= kp.n_ranges; t += blockDim.x) run0[t] = 0;
-    }
-    return;
-  }
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
+  const int64_t b = blockIdx.x;
+  // threshold sieve: a privacy id of this bucket with fewer than l0
+  // candidate pairs (its sketch not full; `sketch` = false: every id) may
+  // have kept pairs among rows this launch did not see; mark it in the
+  // bitmap (a wave covers 64 ids = one u64 word; the bucket's ids are whole
+  // words) and list it.  unres_prev (the band's fix-up launch): only ids the
+  // main launch left unresolved can be.
+  auto mark = [&](bool sketch) {
+    const int lane = threadIdx.x & 63;
+    const int64_t id0 = b << kp.bucket_bits;
+    for (int64_t p0 = (int64_t)(threadIdx.x >> 6) * 64; p0 < S; p0 += blockDim.x) {
+      const int64_t id = id0 + p0 + lane;
+      bool un = id < kp.U;
+      if (sketch) un = un && smem[(int64_t)(l0 - 1) * S + p0 + lane] == kEmpty;  // sk is smem's first array
+      if (unres_prev != nullptr) un = un && ((unres_prev[id >> 5] >> (id & 31)) & 1u);
+      const unsigned long long m = __ballot(un);
+      if (lane == 0) reinterpret_cast<uint2*>(unres_bits)[(id0 + p0) >> 6] = make_uint2((unsigned)m, (unsigned)(m >> 32));
+      if (m) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(sctl, (unsigned)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (un) unres_list[base + __popcll(m & ((1ULL << lane) - 1))] = (unsigned)id;
+      }
+    }
+  };
+  // an empty bucket of a fix-up launch (most of them: only unresolved
+  // privacy ids have rows there) writes its empty runs and stops -- in the
+  // band's fix-up launch after marking its previously unresolved ids (none
+  // of their pairs is below t2); the main launch's empty buckets still mark
+  // their privacy ids unresolved
+  if ((!kp.sieve_mark || unres_prev != nullptr) && offsets[b] == offsets[b + 1]) {  // block-uniform
+    if (RANGES) {
+      unsigned* const run0 = rec.runs + b * (kp.n_ranges + 1);
+      for (int t = threadIdx.x; t <= kp.n_ranges; t += blockDim.x) run0[t] = 0;
+    }
+    if (kp.sieve_mark) mark(false);
+    return;
+  }
   const int64_t n_slots = S * l0;
   // LDS state is structure-of-arrays: entry j of privacy id p at [j * S + p]
   // (row-sketch entry t of slot s at [t * S*l0 + s]), so a wave's lanes, which
@@ -2039,7 +2152,6 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     for (int64_t t = threadIdx.x; t < 3 * n_slots; t += blockDim.x) tot[t] = 0.0;
   }
   __syncthreads();
-  const int64_t b = blockIdx.x;
   const int64_t begin = offsets[b];
   const int64_t end = offsets[b + 1];  // offsets has n_buckets + 1 entries
   const uint64_t bmask = (uint64_t)S - 1;
@@ -2083,38 +2195,38 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
         }
       });
   __syncthreads();
-  if (kp.sieve_mark) {
-    // threshold sieve: a privacy id with fewer than l0 candidate pairs (its
-    // sketch not full) may have kept pairs among its sieved-out rows; mark it
-    // in the bitmap (a wave covers 64 ids = one u64 word; the bucket's ids
-    // are whole words) and list it, and emit nothing for it here (B2 skips
-    // it): the fix-up recomputes it from all of its rows
-    const int lane = threadIdx.x & 63;
-    const int64_t id0 = b << kp.bucket_bits;
-    for (int64_t p0 = (int64_t)(threadIdx.x >> 6) * 64; p0 < S; p0 += blockDim.x) {
-      const bool un = id0 + p0 + lane < kp.U && sk[(int64_t)(l0 - 1) * S + p0 + lane] == kEmpty;
-      const unsigned long long m = __ballot(un);
-      if (lane == 0) reinterpret_cast<uint2*>(unres_bits)[(id0 + p0) >> 6] = make_uint2((unsigned)m, (unsigned)(m >> 32));
-      if (m) {
-        unsigned base = 0;
-        if (lane == 0) base = atomicAdd(sctl, (unsigned)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (un) unres_list[base + __popcll(m & ((1ULL << lane) - 1))] = (unsigned)(id0 + p0 + lane);
-      }
-    }
-  }
+  if (kp.sieve_mark) mark(true);  // emits nothing for its unresolved ids (B2 skips them): the fix-up's
   PDP_PHASE(2);
   // B2: rows of kept pairs, from B1's candidate list (key + row)
   const int flags = kp.clip.flags;
   stream_bucket<COMPACT ? 1 : kUnroll / 2, kRowLoad>(
       cand_key, cand_idx, begin, begin + ccount, wq, conv,
       [&](uint64_t x) {
+        // (dead keys: also the padding lanes' kEmpty, whose bits name no pid)
         if (dead_key(x, kp.rand_shift)) return false;
         const unsigned long long smax = sk[(l0 - 1) * S + (int64_t)((x >> kp.pk_bits) & bmask)];
+        // band: an unresolved id's candidate rows (every one of its records
+        // is on the list; the sieve dropped the dead ones) go to the fix-up
+        if (kp.sieve_emit && smax == kEmpty) return true;
         return x <= smax && !(kp.sieve_mark && smax == kEmpty);  // sieve: unresolved ids are the fix-up's
       },
       [&](uint64_t x, uint32_t ci)  {
       const int64_t pl = (x >> kp.pk_bits) & bmask;
+      if (kp.sieve_emit) {  // block-uniform: the main launch with the band
+        const bool un = sk[(l0 - 1) * S + pl] == kEmpty && ci < (uint64_t)kp.n;
+        const unsigned long long mu = __ballot(un);
+        if (mu) {  // wave-uniform
+          const int lead = __ffsll((long long)mu) - 1;
+          const int lane = threadIdx.x & 63;
+          unsigned base = 0;
+          if (lane == lead) base = atomicAdd(sctl + 1, (unsigned)__popcll(mu));
+          base = __shfl(base, lead, 64);
+          if (un)
+            fix_rec[base + __popcll(mu & ((1ULL << lane) - 1))] =
+                ((unsigned long long)(uint32_t)((b << kp.bucket_bits) | pl) << 32) | (unsigned long long)ci;
+        }
+        if (sk[(l0 - 1) * S + pl] == kEmpty) return;
+      }
       const int j = sketch_find_strided(sk + pl, l0, S, x);
       if (j < 0) return;
       const uint32_t r = ci;  // the candidate's row (B1 carried it)
@@ -2361,6 +2473,87 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
   if (use_bloom) run(std::true_type{});
   else run(std::false_type{});
   // the rest of the queue
+  wave_lds_fence();
+  if (qn > 0) {
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(sctl + 1, (unsigned)qn);
+    base = __shfl(base, 0, 64);
+    if (lane < qn) fix_rec[base + lane] = wq[lane];
+  }
+}
+
+// Fix-up step 1, side band: the tiles' band lists (privacy id << 32 | row,
+// written by k_sieve_l1<BAND>) instead of the whole privacy-id column, with
+// the same Bloom filter, per-wave queues and output (fix_rec, sctl[1]) as
+// k_sieve_rescan; the unresolved ids' candidate rows are already on fix_rec
+// (the main bucket launch put them there).  Every lane of a wave runs the
+// same trips (band_cnt[t] is block-uniform), so the queues stay wave-uniform.
+__global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsigned long long* __restrict__ band,
+                                                              const unsigned* __restrict__ band_cnt,
+                                                              const unsigned* __restrict__ unres_bits,
+                                                              const unsigned* __restrict__ unres_list,
+                                                              unsigned* __restrict__ sctl,
+                                                              unsigned long long* __restrict__ fix_rec) {
+  __shared__ unsigned bloom[kBloomWords];
+  __shared__ unsigned long long queue[kRescanThreads / 64][kRescanQueue];
+  const unsigned n_unres = sctl[0];
+  if (n_unres == 0) return;  // grid-uniform
+  const bool use_bloom = n_unres <= kBloomMaxIds;  // grid-uniform
+  for (int i = threadIdx.x; i < kBloomWords; i += blockDim.x) bloom[i] = 0;
+  __syncthreads();
+  for (unsigned i = threadIdx.x; use_bloom && i < n_unres; i += blockDim.x) {
+    const uint32_t h = bloom_hash(unres_list[i]);
+    atomicOr(bloom + bloom_word(h), bloom_bits(h));
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  unsigned long long* const wq = queue[threadIdx.x >> 6];
+  int qn = 0;
+  auto enqueue = [&](bool pos, unsigned long long e) {
+    const unsigned long long m = __ballot(pos);
+    if (m == 0) return;  // wave-uniform
+    if (pos) wq[qn + __popcll(m & below)] = e;
+    qn += __popcll(m);
+    if (qn >= 64) {
+      wave_lds_fence();
+      const unsigned long long x = wq[lane];
+      unsigned base = 0;
+      if (lane == 0) base = atomicAdd(sctl + 1, 64u);
+      base = __shfl(base, 0, 64);
+      fix_rec[base + lane] = x;
+      const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
+      wave_lds_fence();
+      if (lane + 64 < qn) wq[lane] = rest;
+      qn -= 64;
+      wave_lds_fence();
+    }
+  };
+  constexpr int KU = 4;  // entries per lane and trip, loaded together
+  const int64_t w0 = (int64_t)(threadIdx.x >> 6) * 64 * KU;
+  auto run = [&](auto bloom_tag) {
+    constexpr bool BLOOM = decltype(bloom_tag)::value;
+    for (int64_t t = blockIdx.x; t < kp.n_tiles; t += gridDim.x) {
+      const unsigned long long* __restrict__ bt = band + t * kTileRows;
+      unsigned cnt = band_cnt[t];
+      cnt = cnt <= (unsigned)kTileRows ? cnt : (unsigned)kTileRows;
+      for (int64_t j0 = w0; j0 < cnt; j0 += (int64_t)blockDim.x * KU) {  // wave-uniform trips
+        unsigned long long e[KU];
+#pragma unroll
+        for (int v = 0; v < KU; ++v) {
+          const int64_t j = j0 + v * 64 + lane;
+          e[v] = j < cnt ? bt[j] : ~0ULL;
+        }
+#pragma unroll
+        for (int v = 0; v < KU; ++v) {
+          const int64_t u = e[v] == ~0ULL ? -1 : (int64_t)(e[v] >> 32);
+          enqueue(u >= 0 && rescan_maybe<BLOOM>(kp, u, bloom, unres_bits), e[v]);
+        }
+      }
+    }
+  };
+  if (use_bloom) run(std::true_type{});
+  else run(std::false_type{});
   wave_lds_fence();
   if (qn > 0) {
     unsigned base = 0;
@@ -2991,10 +3184,21 @@ int launch_global_reduce(const KP& kp, hipStream_t st, const void* value, const 
   return PDP_OK;
 }
 
+// where a bucket launch marks unresolved ids (the main launch: the first
+// bitmap / list / counters; the band's fix-up launch: the second ones, only
+// ids in `prev`), and where the main launch with the band sends their rows
+struct Marks {
+  unsigned* bits;
+  unsigned* list;
+  unsigned* sctl;
+  const unsigned* prev;
+  unsigned long long* fix_rec;
+};
+
 template <int VK, bool KA>
 int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void* keys, const unsigned* rows,
                          const unsigned* offsets, const void* value, const pdp_partition_accumulators& acc,
-                         PairRecords rec, char* ws, const Ws& w, const char* name) {
+                         PairRecords rec, char* ws, const Ws& w, const char* name, const Marks& mk) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
   // PACKED: COMPACT records from level 2 on; PACKED_WIDE: WIDE ones
   const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
@@ -3005,14 +3209,16 @@ int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void
   PDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes));
   void* cand_key = ws + w.cand_key;
   unsigned* cand_idx = (unsigned*)(ws + w.cand_idx);
-  unsigned* unres_bits = w.unres_bits ? (unsigned*)(ws + w.unres_bits) : nullptr;
-  unsigned* unres_list = w.unres_list ? (unsigned*)(ws + w.unres_list) : nullptr;
-  unsigned* sctl = w.sctl ? (unsigned*)(ws + w.sctl) : nullptr;
+  unsigned* unres_bits = mk.bits;
+  unsigned* unres_list = mk.list;
+  unsigned* sctl = mk.sctl;
   unsigned* err = (unsigned*)(ws + w.err);
+  unsigned long long* fix_rec = mk.fix_rec;
+  const unsigned* prev = mk.prev;
   void* args[] = {(void*)&kp,       (void*)&keys,       (void*)&rows,       (void*)&offsets,
                   (void*)&value,    (void*)&acc,        (void*)&rec,        (void*)&cand_key,
                   (void*)&cand_idx, (void*)&unres_bits, (void*)&unres_list, (void*)&sctl,
-                  (void*)&err};
+                  (void*)&err,      (void*)&fix_rec,    (void*)&prev};
   PDP_PROF_BEGIN(name, st);
   PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
   PDP_PROF_END(st);
@@ -3033,60 +3239,98 @@ PairRecords pair_records(char* ws, const Ws& w) {
 }
 
 // Sampling (every bucket kernel): the main launch over the level-2 records;
-// with the sieve, the fix-up of the unresolved privacy ids (rescan of the
-// privacy-id column, scatter into bucket order, a second launch whose pair
-// records follow the main ones: buckets [n_buckets, 2 n_buckets) of `rec`).
+// with the sieve, the fix-up of the unresolved privacy ids (their rows
+// gathered, scattered into bucket order, a second launch whose pair records
+// follow the main ones: buckets [n_buckets, 2 n_buckets) of `rec`).  The
+// rows come from a rescan of the privacy-id column, or with the band from
+// the band lists plus the candidate rows the main launch sent; the band's
+// fix-up launch marks the ids still short of l0 pairs, whose rows a rescan
+// then gathers for a third launch (buckets [2 n_buckets, 3 n_buckets)).
+// Every step past the main launch reads its counts on the device, so an
+// empty fix-up costs a few near-empty launches and no host round trip.
 template <int VK, bool KA>
 int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
                    const uint8_t* allowed, const void* value, const pdp_partition_accumulators& acc, char* ws,
                    const Ws& w) {
   const PairRecords rec = pair_records(ws, w);
+  unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
+  Marks m1{w.unres_bits ? (unsigned*)(ws + w.unres_bits) : nullptr,
+           w.unres_list ? (unsigned*)(ws + w.unres_list) : nullptr, w.sctl ? (unsigned*)(ws + w.sctl) : nullptr,
+           nullptr, p.band ? fix_rec : nullptr};
   int rc = launch_bucket_kernel<VK, KA>(kp, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
-                                        (const unsigned*)(ws + w.counts), value, acc, rec, ws, w, "k_bucket_bound");
+                                        (const unsigned*)(ws + w.counts), value, acc, rec, ws, w, "k_bucket_bound", m1);
   if (rc != PDP_OK || !p.sieve) return rc;
+  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
+  const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
+  // one fix-up: rows listed in fix_rec (sctl[1] of them) -> exact test ->
+  // bucket order -> a bucket launch over them into record segment `seg`
+  auto fixup = [&](unsigned* bits, unsigned* sctl, unsigned* fix_cnt, unsigned* fix_cur, int seg, const Marks& mk,
+                   int mark, const char* name) -> int {
+    PDP_PROF_BEGIN("k_fix_filter", st);
+    hipLaunchKernelGGL(k_fix_filter, dim3(grid_for(kp.n, 1024)), dim3(kBlock), 0, st, kp, (const unsigned*)bits,
+                       (const unsigned*)sctl, fix_rec, fix_cnt);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    int r = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts
+    if (r != PDP_OK) return r;
+    const unsigned fix_grid = grid_for(kp.n, 2048);
+    PDP_PROF_BEGIN("k_fix_scatter", st);
+    if (compact)
+      hipLaunchKernelGGL(k_fix_scatter<true>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    else
+      hipLaunchKernelGGL(k_fix_scatter<false>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    KP kf = kp;
+    kf.sieve_mark = mark;
+    kf.sieve_emit = 0;
+    PairRecords fr = rec;
+    fr.runs += seg * p.n_buckets * (p.n_ranges + 1);
+    fr.key += seg * p.n_buckets * n_slots;
+    if (fr.f0) fr.f0 += seg * p.n_buckets * n_slots;
+    if (fr.f1) fr.f1 += seg * p.n_buckets * n_slots;
+    if (fr.f2) fr.f2 += seg * p.n_buckets * n_slots;
+    return launch_bucket_kernel<VK, KA>(kf, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
+                                        (const unsigned*)fix_cnt, value, acc, fr, ws, w, name, mk);
+  };
+  auto rescan = [&](const unsigned* bits, const unsigned* list, unsigned* sctl) {
+    PDP_PROF_BEGIN("k_sieve_rescan", st);
+    if (kp.keys_vec)
+      hipLaunchKernelGGL(k_sieve_rescan<true>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid, bits, list,
+                         sctl, fix_rec);
+    else
+      hipLaunchKernelGGL(k_sieve_rescan<false>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid, bits, list,
+                         sctl, fix_rec);
+    PDP_PROF_END(st);
+  };
   unsigned* sctl = (unsigned*)(ws + w.sctl);
   unsigned* fix_cnt = (unsigned*)(ws + w.fix_cnt);
-  unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
-  PDP_PROF_BEGIN("k_sieve_rescan", st);
-  if (kp.keys_vec)
-    hipLaunchKernelGGL(k_sieve_rescan<true>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid,
-                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_rec);
-  else
-    hipLaunchKernelGGL(k_sieve_rescan<false>, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp, pid,
-                       (const unsigned*)(ws + w.unres_bits), (const unsigned*)(ws + w.unres_list), sctl, fix_rec);
+  unsigned* fix_cur = (unsigned*)(ws + w.fix_cur);
+  const Marks none{m1.bits, m1.list, m1.sctl, nullptr, nullptr};
+  if (!p.band) {
+    rescan(m1.bits, m1.list, sctl);
+    PDP_HIP_CHECK(hipGetLastError());
+    return fixup(m1.bits, sctl, fix_cnt, fix_cur, 1, none, 0, "k_bucket_fix");
+  }
+  // the band: its lists (Bloom filter unless too many ids) -> fix-up launch
+  // that marks the ids still unresolved -> their rescan -> a third launch
+  PDP_PROF_BEGIN("k_band_scan", st);
+  hipLaunchKernelGGL(k_band_scan, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp,
+                       (const unsigned long long*)(ws + w.band), (const unsigned*)(ws + w.band_cnt),
+                       (const unsigned*)m1.bits, (const unsigned*)m1.list, sctl, fix_rec);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
-  PDP_PROF_BEGIN("k_fix_filter", st);
-  hipLaunchKernelGGL(k_fix_filter, dim3(grid_for(kp.n, 1024)), dim3(kBlock), 0, st, kp,
-                     (const unsigned*)(ws + w.unres_bits), (const unsigned*)sctl, fix_rec, fix_cnt);
-  PDP_PROF_END(st);
-  PDP_HIP_CHECK(hipGetLastError());
-  rc = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts
+  unsigned* sctl2 = (unsigned*)(ws + w.sctl2);
+  const Marks m2{(unsigned*)(ws + w.unres2_bits), (unsigned*)(ws + w.unres2_list), sctl2, m1.bits, nullptr};
+  rc = fixup(m1.bits, sctl, fix_cnt, fix_cur, 1, m2, 1, "k_bucket_fix");
   if (rc != PDP_OK) return rc;
-  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
-  const unsigned fix_grid = grid_for(kp.n, 2048);
-  PDP_PROF_BEGIN("k_fix_scatter", st);
-  if (compact)
-    hipLaunchKernelGGL(k_fix_scatter<true>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
-                       (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt,
-                       (unsigned*)(ws + w.fix_cur), (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
-  else
-    hipLaunchKernelGGL(k_fix_scatter<false>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
-                       (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt,
-                       (unsigned*)(ws + w.fix_cur), (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
-  PDP_PROF_END(st);
+  rescan(m2.bits, m2.list, sctl2);
   PDP_HIP_CHECK(hipGetLastError());
-  KP kf = kp;
-  kf.sieve_mark = 0;  // every row of these privacy ids is here
-  PairRecords fr = rec;
-  const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
-  fr.runs += p.n_buckets * (p.n_ranges + 1);
-  fr.key += p.n_buckets * n_slots;
-  if (fr.f0) fr.f0 += p.n_buckets * n_slots;
-  if (fr.f1) fr.f1 += p.n_buckets * n_slots;
-  if (fr.f2) fr.f2 += p.n_buckets * n_slots;
-  return launch_bucket_kernel<VK, KA>(kf, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
-                                      (const unsigned*)fix_cnt, value, acc, fr, ws, w, "k_bucket_fix");
+  return fixup(m2.bits, sctl2, (unsigned*)(ws + w.fix_cnt2), (unsigned*)(ws + w.fix_cur2), 2, m2, 0, "k_bucket_fix2");
 }
 
 // PDP_MERGE_RANGES: the pair records of every bucket (p.buckets_out of them)
@@ -3204,7 +3448,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = !kPackedL1<FMT>;
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
-  const bool u16 = p.sieve ? sieve_hist_u16(FMT, p.n_buckets) : l1_hist_u16(FMT, p.n_buckets);
+  const bool u16 = p.sieve ? sieve_hist_u16(FMT, p.n_buckets, p.band != 0) : l1_hist_u16(FMT, p.n_buckets);
   unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
@@ -3213,11 +3457,16 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
   if constexpr (FMT != PDP_KEYS_WIDE) {
     if (p.sieve) {
-      const size_t lds1 = (sieve_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
-      const void* l1 = u16 ? (const void*)k_sieve_l1<FMT, true> : (const void*)k_sieve_l1<FMT, false>;
+      const size_t lds1 = (sieve_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16) +
+                          (p.band ? (size_t)kBandLds : 0);
+      const void* l1 = p.band ? (u16 ? (const void*)k_sieve_l1<FMT, true, true> : (const void*)k_sieve_l1<FMT, false, true>)
+                              : (u16 ? (const void*)k_sieve_l1<FMT, true, false> : (const void*)k_sieve_l1<FMT, false, false>);
       PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
+      unsigned long long* band = p.band ? (unsigned long long*)(ws + w.band) : nullptr;
+      unsigned* band_cnt = p.band ? (unsigned*)(ws + w.band_cnt) : nullptr;
       void* args1[] = {(void*)&kp,   (void*)&pid,   (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
-                       (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err};
+                       (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err,
+                       (void*)&band, (void*)&band_cnt};
       PDP_PROF_BEGIN("k_sieve_l1", st);
       PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
       PDP_PROF_END(st);
@@ -3445,6 +3694,7 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->range_group = p.range_group;
   info->key_format = p.key_format;
   info->sieve = p.sieve;
+  info->band = p.band;
   return PDP_OK;
 }
 
@@ -3524,6 +3774,11 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cnt, 0, ((uint64_t)p.n_buckets + 1) * 4, st));
     PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cur, 0, (uint64_t)p.n_buckets * 4, st));
   }
+  if (p.band) {
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.sctl2, 0, 16, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cnt2, 0, ((uint64_t)p.n_buckets + 1) * 4, st));
+    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cur2, 0, (uint64_t)p.n_buckets * 4, st));
+  }
   const pdp_partition_accumulators none{};
   return dispatch<Buckets>(cfg->value_kind, cfg->linf == 0, kp, p, st, privacy_id, partition_key, pk_allowed, value,
                            none, ws, w);
@@ -3544,11 +3799,22 @@ int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uin
   const bool bucketed = !pairs_mode(cfg) && p.algorithm == PDP_ALGO_BUCKETED && cfg->n_rows > 0;
   if (bucketed) PDP_HIP_CHECK(hipMemcpyAsync(&rows, ws + w.counts + (uint64_t)p.n_buckets * 4, 4, hipMemcpyDeviceToHost, st));
   if (bucketed && p.sieve) PDP_HIP_CHECK(hipMemcpyAsync(ctl, ws + w.sctl, 8, hipMemcpyDeviceToHost, st));
+  unsigned ctl2[2] = {0, 0};
+  std::vector<unsigned> bc;
+  if (bucketed && p.band) {
+    PDP_HIP_CHECK(hipMemcpyAsync(ctl2, ws + w.sctl2, 8, hipMemcpyDeviceToHost, st));
+    bc.resize((size_t)p.n_tiles);
+    PDP_HIP_CHECK(hipMemcpyAsync(bc.data(), ws + w.band_cnt, (size_t)p.n_tiles * 4, hipMemcpyDeviceToHost, st));
+  }
   PDP_HIP_CHECK(hipStreamSynchronize(st));
   out->rows_partitioned = rows;
   out->unresolved_ids = ctl[0];
   out->fixup_rows = ctl[1];
   out->sieve = bucketed ? p.sieve : 0;
+  out->band = bucketed ? p.band : 0;
+  for (unsigned v : bc) out->band_rows += v;
+  out->unresolved2_ids = ctl2[0];
+  out->fixup2_rows = ctl2[1];
   return PDP_OK;
 }
 

@@ -200,7 +200,8 @@ def _acc_struct(acc) -> N.PartitionAccumulators:
 
 def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, seed: int,
                  row_offset: int = 0, algorithm: int = N.ALGO_AUTO,
-                 merge: int = N.MERGE_AUTO, key_format: int = N.KEYS_AUTO, sieve: int = 0) -> N.BoundConfig:
+                 merge: int = N.MERGE_AUTO, key_format: int = N.KEYS_AUTO, sieve: int = 0,
+                 sieve_band: int = 0) -> N.BoundConfig:
     c = N.BoundConfig()
     c.n_rows = int(n_rows)
     c.n_privacy_ids = int(n_privacy_ids)
@@ -222,14 +223,16 @@ def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, se
     c.rows_are_units = 1 if bounding.rows_are_units else 0
     c.key_format = int(key_format)
     c.sieve = int(sieve)
+    c.sieve_band = int(sieve_band)
     return c
 
 
 def bound_plan(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec,
                algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
-               key_format: int = N.KEYS_AUTO, sieve: int = 0) -> N.BoundPlanInfo:
+               key_format: int = N.KEYS_AUTO, sieve: int = 0, sieve_band: int = 0) -> N.BoundPlanInfo:
     """Execution plan the library resolves for this shard (no device work)."""
-    cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge, key_format, sieve)
+    cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge, key_format, sieve,
+                       sieve_band)
     info = N.BoundPlanInfo()
     N.check(N.lib().pdp_bound_plan(ctypes.byref(cfg), ctypes.byref(info)), "pdp_bound_plan")
     return info
@@ -252,7 +255,9 @@ class BoundWorkspace:
         N.check(N.lib().pdp_bound_stats_read(ctypes.byref(self.last_cfg), _ptr(self.buf), self.buf.numel(),
                                              ctypes.byref(out), _stream(stream)), "pdp_bound_stats_read")
         return {"rows_partitioned": out.rows_partitioned, "unresolved_ids": out.unresolved_ids,
-                "fixup_rows": out.fixup_rows, "sieve": out.sieve, "error_flags": out.error_flags}
+                "fixup_rows": out.fixup_rows, "sieve": out.sieve, "error_flags": out.error_flags,
+                "band_rows": out.band_rows, "unresolved2_ids": out.unresolved2_ids,
+                "fixup2_rows": out.fixup2_rows, "band": out.band}
 
     def get(self, nbytes: int, device):
         torch = _torch()
@@ -266,7 +271,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                      acc=None, workspace: Optional[BoundWorkspace] = None, stream=None,
                      check_keys: bool = True, timer: Optional["StageTimer"] = None,
                      algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
-                     key_format: int = N.KEYS_AUTO, sieve: int = 0):
+                     key_format: int = N.KEYS_AUTO, sieve: int = 0, sieve_band: int = 0):
     """Bounds contributions of one shard and ADDS its per-partition accumulators.
 
     pid, pk: int64 device tensors of length n (dense keys; pid may be None
@@ -300,7 +305,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")
     cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
-                       key_format, sieve)
+                       key_format, sieve, sieve_band)
     nbytes = ctypes.c_uint64(0)
     N.check(lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)),
             "pdp_bound_workspace_bytes")

@@ -40,14 +40,16 @@ def _spec(case):
                           middle=mid, min_sum=pp[0] if pp else 0.0, max_sum=pp[1] if pp else 0.0)
 
 
-def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format=0, row_offset=0):
+def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format=0, row_offset=0, band=0,
+         workspace=None):
     import torch
     from pipelinedp_amd import executor as X
     tv = None if val is None else torch.as_tensor(val).to(device)
     ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
     acc = X.bound_and_reduce(torch.as_tensor(pid).to(device), torch.as_tensor(pk).to(device), tv,
                              n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, allowed=ta,
-                             key_format=key_format, sieve=sieve, row_offset=row_offset)
+                             key_format=key_format, sieve=sieve, row_offset=row_offset, sieve_band=band,
+                             workspace=workspace)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
@@ -73,8 +75,10 @@ def test_sieve_matches_oracle_at_every_threshold(device, case):
     for sieve in SIEVES:
         plan = X.bound_plan(n, U, P, spec, sieve=sieve)
         assert plan.sieve == sieve, (sieve, plan.sieve)
-        got = _run(device, pid, pk, val, U, P, spec, seed, sieve)
-        _compare(got, want, scale)
+        assert plan.band == (min(2 * sieve, 32768) if sieve < 32768 else 0)
+        for band in (0, -1):  # the side band (ids with < l0 pairs below 2t: the rescan), and without it
+            got = _run(device, pid, pk, val, U, P, spec, seed, sieve, band=band)
+            _compare(got, want, scale)
     off = _run(device, pid, pk, val, U, P, spec, seed, -1)
     assert X.bound_plan(n, U, P, spec, sieve=-1).sieve == 0
     _compare(off, want, scale)
@@ -131,11 +135,45 @@ def test_sieve_c3_shape_slice(device):
     pk = np.minimum(rng.zipf(1.1, n) - 1, P - 1).astype(np.int64)
     val = rng.random(n) * 10.0
     plan = X.bound_plan(n, U, P, spec)
-    assert 0 < plan.sieve < 16384  # auto: t ~ 0.15
+    assert 0 < plan.sieve < 16384 and plan.band == 2 * plan.sieve  # auto: t ~ 0.15, band to 2t
     seed = 77
     want = _want(pid, pk, val, U, P, spec, seed)
     scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
-    _compare(_run(device, pid, pk, val, U, P, spec, seed, 0), want, scale)
+    ws = X.BoundWorkspace()
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 0, workspace=ws), want, scale)
+    st = ws.stats()
+    # ~t of the rows went on as candidates and ~t more to the band; ids
+    # short of l0 candidate pairs are finished from the band (at C3's ~100
+    # rows per id none is short of l0 pairs below 2t: no rescan)
+    assert 0.1 * n < st["rows_partitioned"] < 0.2 * n and 0.1 * n < st["band_rows"] < 0.2 * n, st
+    assert st["unresolved_ids"] > 0 and st["unresolved2_ids"] == 0 and st["fixup2_rows"] == 0, st
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 0, band=-1), want, scale)
+
+
+def test_band_with_ids_short_of_pairs(device):
+    """Ids with one to three rows next to ~100-row ids: the short ones stay
+    unresolved after the band (fewer than l0 distinct pairs below 2t, or at
+    all), so the band's fix-up launch marks them and the privacy-id column is
+    re-read for them (the third bucket launch); equal to the oracle."""
+    from pipelinedp_amd import executor as X
+    spec = _spec((3, 2, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    U, P = 120_000, 50_000
+    rng = np.random.default_rng(31)
+    big = rng.integers(0, 100_000, 100 * 100_000)
+    small = np.repeat(np.arange(100_000, U), rng.integers(1, 4, U - 100_000))
+    pid = rng.permutation(np.concatenate([big, small]))
+    n = len(pid)
+    pk = rng.integers(0, P, n)
+    val = rng.random(n) * 10.0
+    plan = X.bound_plan(n, U, P, spec, sieve=6000)
+    assert plan.sieve == 6000 and plan.band == 12000
+    seed = 5150
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    ws = X.BoundWorkspace()
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 6000, workspace=ws), want, scale)
+    st = ws.stats()
+    assert st["unresolved2_ids"] > 10_000 and st["fixup2_rows"] >= st["unresolved2_ids"], st
 
 
 @pytest.mark.parametrize("sieve", [-1, 4096])
