@@ -81,9 +81,10 @@ typedef struct pdp_bound_config {
                                 (candidate fraction t = sieve / 2^16 <= 1/2) through the partition
                                 passes; privacy ids with < l0 candidate pairs are finished from a
                                 side band or a re-read of the privacy-id column */
-  int32_t sieve_band;        /* with the sieve: 0 = auto (level 1 also lists the rows whose pair hash
-                                is below 2t, and the fix-up reads that list; only ids with < l0
-                                pairs below 2t re-read the privacy-id column), < 0 = off */
+  int32_t sieve_band;        /* with the sieve, the side band: level 1 also lists the rows whose pair
+                                hash is in [t, 2t), and the fix-up reads that list; only ids with
+                                < l0 pairs below 2t re-read the privacy-id column.  0 = auto (on
+                                for t <= 1/4), > 0 = on, < 0 = off (identical results) */
 } pdp_bound_config;
 
 /* bounds up to int32; above 256 (l0, linf) the pair-table algorithm runs, and

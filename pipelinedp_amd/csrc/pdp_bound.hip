@@ -311,7 +311,12 @@ Plan make_plan(const pdp_bound_config* c) {
   if (p.sieve) {
     const int t2 = 2 * p.sieve < kSieveMaxT16 ? 2 * p.sieve : kSieveMaxT16;
     const bool fits = (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) + kBandLds <= kL1LocalLds;
-    if (t2 > p.sieve && fits && c->sieve_band >= 0) p.band = t2;
+    // auto: only below t = 1/4 -- there an id short of l0 candidate pairs,
+    // and with it the 8 B/row rescan, is likely (C3: t = 0.154, ~1,600 of 1e7
+    // ids; C2's t = 0.325 leaves none, and the band would only cost level 1
+    // its writes: 1.43 -> 1.52 ms, profiles/r03/ab/ab4_band.txt)
+    const bool want = c->sieve_band > 0 || (c->sieve_band == 0 && p.sieve <= kSieveMaxT16 / 2);
+    if (t2 > p.sieve && fits && want) p.band = t2;
   }
   p.n_slots1 = p.sieve ? p.n_tiles * kStagesPerTile : p.n_stages;
   p.buckets_out = p.sieve ? (p.band ? 3 : 2) * p.n_buckets : p.n_buckets;
@@ -1591,6 +1596,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         } else {  // PACKED / PACKED_WIDE
           x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
         }
+        // a band row is no candidate: its key slot carries its privacy id
+        // past the prefetch below, which reuses u[] / k[]
+        if constexpr (BAND) x[q] = bnd[q] ? (K)(uint32_t)u[q] : x[q];
       }
       if constexpr (FULL) {
         const int64_t cp = c0 + kSieveBufs * kSieveChunk < t1 ? c0 + kSieveBufs * kSieveChunk : t1 - kSieveChunk;
@@ -1625,7 +1633,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
           const unsigned long long mb = __ballot(bnd[q]);
           if (mb == 0) continue;  // wave-uniform
           const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
-          if (bnd[q]) wq[qn + __popcll(mb & below)] = ((unsigned long long)(uint32_t)u[q] << 32) | (uint32_t)i;
+          if (bnd[q]) wq[qn + __popcll(mb & below)] = ((unsigned long long)(uint32_t)x[q] << 32) | (uint32_t)i;
           qn += __popcll(mb);
           if (qn >= 64) {
             wave_lds_fence();
