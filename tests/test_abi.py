@@ -149,6 +149,17 @@ def test_sieve_plan(lib):
     assert info.sieve == 0  # one bucket level: no tile-local level 1
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(merge=N.MERGE_ATOMIC, sieve=4096)), ctypes.byref(info)) == 0
     assert info.sieve == 0  # the fix-up appends pair records: range merge only
+    # the side band: auto for t <= 1/4 at t2 = 2t (C3 yes, C2 no), forced on / off
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3)), ctypes.byref(info)) == 0
+    assert info.band == 2 * info.sieve
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve_band=-1)), ctypes.byref(info)) == 0
+    assert info.band == 0 and info.sieve > 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg()), ctypes.byref(info)) == 0  # C2
+    assert info.band == 0
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(sieve_band=1)), ctypes.byref(info)) == 0
+    assert info.band == 1 << 15  # 2t capped at 1/2
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=-1)), ctypes.byref(info)) == 0
+    assert info.band == 0
     # the sieve's workspace holds the fix-up state and twice the pair records
     on, off = ctypes.c_uint64(0), ctypes.c_uint64(0)
     assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(**c3)), ctypes.byref(on)) == 0
