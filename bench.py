@@ -631,6 +631,15 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     kept_pairs = int(acc["privacy_id_count"].sum().item())  # last step, this rank
     kept_rows = int(acc["count"].sum().item())
     stats = ws.stats()
+    # run-to-run spread: up to 10 more steps, each timed on its own (synced),
+    # outside the timed region (their seeds differ, as the timed steps' do)
+    samples = []
+    for i in range(min(args.steps, 10)):
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        step(args.warmup + 2 * args.steps + i)
+        torch.cuda.synchronize()
+        samples.append((time.perf_counter() - ts) * 1e3)
     api = api_timing(args, workload, pid, pk, value, U, P, ws) if (world == 1 and args.api) else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -696,6 +705,9 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                        "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0, "stats": stats},
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,
+        "step_ms_spread": ({"n": len(samples), "min": min(samples), "median": float(np.median(samples)),
+                            "max": max(samples), "what": "steps timed one by one after the timed region"}
+                           if samples else None),
     }
 
 
@@ -770,6 +782,7 @@ def main():
         "bound_plan": r["bound_plan"],
         "partitions_kept": r["partitions_kept"],
         "privacy_id_verify_ms": r.get("privacy_id_verify_ms"),
+        "step_ms_spread": r.get("step_ms_spread"),
         "api": r["api"],
         "cpu_baseline": cpu[0] if cpu else None,
         "cpu_baseline_strong": cpu[1] if cpu else None,
