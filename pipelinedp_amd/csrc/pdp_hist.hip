@@ -610,22 +610,22 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
       for (int u = 0; u < U; ++u)
         if (i0 + u * stride < np) add(v[u]);
     }
-  } else if (nl0 > 0 && hb_ctl[0] == 2) {  // the privacy-id buckets' pair records: a wave per bucket
-    const int64_t R = hb_ctl[3];
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = stride >> 6;
-    for (int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; b < t.nb; b += nw) {
-      const unsigned a = hb_bstart[b], rows = hb_bstart[b + 1] - a;
-      unsigned c = hb_pruns[b * (R + 1) + R];
-      c = c <= rows ? c : 0u;
-      for (unsigned j0 = lane; j0 < c; j0 += U * 64) {
-        double v[U];
+  } else if (nl0 > 0 && hb_ctl[0] == 2) {
+    // the privacy-id buckets' pair records: every bucket's row span holds its
+    // pairs, then records marked pk = ~0 (k_hb_pid_pairs), so one flat,
+    // coalesced pass over [0, valid rows) reads them all
+    const int64_t np = hb_bstart[t.nb];
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < np; i0 += U * stride) {
+      PRec r[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = j0 + u * 64 < c ? hb_prec[a + j0 + u * 64].sum : 0.0;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (j0 + u * 64 < c) add(v[u]);
+      for (int u = 0; u < U; ++u) {
+        r[u].pk = ~0u;
+        r[u].sum = 0.0;
+        if (i0 + u * stride < np) r[u] = hb_prec[i0 + u * stride];
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (r[u].pk != ~0u) add(r[u].sum);
     }
   } else if (nl0 > 0) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += stride) {
@@ -1206,6 +1206,8 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
     const unsigned pid = pkey[i];
     if (pid != ~0u) pidstat[pid] = pst[i];
   }
+  if (RANGES)  // the rest of the bucket's row span: no pair (k_h_float reads the span flat)
+    for (int64_t j = a + rstart[R] + threadIdx.x; j < e; j += blockDim.x) prec[j].pk = ~0u;
   if (!RANGES) {
     flush_small(H, lbins, 0, H_LINF);
     block_minmax(mn, mx, minmax);  // contains __syncthreads (workgroup-uniform branch)
