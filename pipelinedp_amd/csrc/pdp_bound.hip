@@ -2626,20 +2626,26 @@ __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __
 // ceil(total_r / C) items plus a sentinel at a base taken with one atomicAdd
 // (ranges land in any order); entry k + 1 holds item k's end.  Entry:
 // {r | sentinel << 31, first bucket, first record position within the range}.
+// last_ids (the band's second fix-up): its id count; 0 leaves the last
+// `last_buckets` buckets (that launch's record segment) empty, so they are
+// not read
 __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsigned* __restrict__ runs,
                                                               uint4* __restrict__ items,
-                                                              unsigned* __restrict__ n_items) {
+                                                              unsigned* __restrict__ n_items,
+                                                              const unsigned* __restrict__ last_ids,
+                                                              int64_t last_buckets) {
   __shared__ unsigned wsum[kRangeThreads / 64 + 1];
   __shared__ unsigned s_base;
   const int r = blockIdx.x;
   const int64_t stride = kp.n_ranges + 1;
+  const int64_t n_buckets = last_ids != nullptr && *last_ids == 0u ? kp.n_buckets - last_buckets : kp.n_buckets;
   auto len_of = [&](int64_t b) -> unsigned {
-    if (b >= kp.n_buckets) return 0u;
+    if (b >= n_buckets) return 0u;
     const unsigned* run = runs + b * stride + r;
     return run[1] - run[0];
   };
   unsigned total = 0;
-  for (int64_t c = 0; c < kp.n_buckets; c += blockDim.x) {
+  for (int64_t c = 0; c < n_buckets; c += blockDim.x) {
     unsigned t;
     block_excl_scan(len_of(c + threadIdx.x), wsum, &t);
     total += t;
@@ -2653,9 +2659,9 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
   const unsigned base = s_base;
   if (threadIdx.x == 0) items[base] = make_uint4((unsigned)r, 0u, 0u, 0u);
   if (threadIdx.x == 0 && total % C != 0)
-    items[base + K] = make_uint4((unsigned)r | 0x80000000u, (unsigned)kp.n_buckets, total, 0u);
+    items[base + K] = make_uint4((unsigned)r | 0x80000000u, (unsigned)n_buckets, total, 0u);
   unsigned carry = 0;
-  for (int64_t c = 0; c < kp.n_buckets; c += blockDim.x) {
+  for (int64_t c = 0; c < n_buckets; c += blockDim.x) {
     const int64_t b = c + threadIdx.x;
     const unsigned len = len_of(b);
     unsigned t;
@@ -3356,8 +3362,9 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     unsigned* n_items = (unsigned*)(ws + w.rr_count);
     PDP_HIP_CHECK(hipMemsetAsync(n_items, 0, 4, st));
     PDP_PROF_BEGIN("k_range_plan", st);
+    const unsigned* last_ids = p.band ? (const unsigned*)(ws + w.sctl2) : nullptr;
     hipLaunchKernelGGL(k_range_plan, dim3((unsigned)p.n_ranges), dim3(kRangeThreads), 0, st, kp,
-                       (const unsigned*)rec.runs, items, n_items);
+                       (const unsigned*)rec.runs, items, n_items, last_ids, (int64_t)p.n_buckets);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     if (!p.two_level) {
