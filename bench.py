@@ -89,6 +89,11 @@ def parse():
                     help="the sieve's side band (0 auto, -1 off; pdp_bound_config.sieve_band)")
     ap.add_argument("--sieve", type=int, default=0,
                     help="threshold sieve t * 2^16 (0 auto, -1 off; pdp_bound_config.sieve)")
+    ap.add_argument("--sieve-threads", type=int, default=0,
+                    help="the sieve's level-1 workgroup: 0 auto, 512 or 1024 (pdp_bound_config.sieve_threads)")
+    ap.add_argument("--merge", type=int, default=0, help="PDP_MERGE_* (0 auto, 1 atomic, 2 ranges)")
+    ap.add_argument("--seed", type=int, default=20261017,
+                    help="sampling seed base: step i uses seed + i, so a run is reproducible (c2 / c3)")
     ap.add_argument("--strategy", choices=("truncated_geometric", "gaussian", "laplace"),
                     default="truncated_geometric",
                     help="c4 / c5: AggregateParams.partition_selection_strategy (SURVEY §8(d) C4 names "
@@ -179,8 +184,8 @@ def cpu_baselines(workload, sample_rows):
 
 def gen_c3(n, U, P, rank, world, device, seed):
     """This rank's shard: its U privacy ids as local codes k in [0, U) --
-    the dataset-wide id of code k on rank r is r * U + k (privacy_id_identity),
-    so ranks hold disjoint ids -- and Zipf(1.1) pk."""
+    the dataset-wide id of code k on rank r is owned_identities(...)[k], so
+    ranks hold disjoint, hash-owned ids -- and Zipf(1.1) pk."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed + rank)
@@ -200,7 +205,7 @@ def gen_c3(n, U, P, rank, world, device, seed):
 
 
 def gen_c2(n, U, P, rank, device, seed):
-    """Local privacy-id codes as in gen_c3 (dataset-wide id r * U + k)."""
+    """Local privacy-id codes as in gen_c3 (dataset-wide ids: owned_identities)."""
     import torch
     g = torch.Generator(device=device)
     g.manual_seed(seed + rank)
@@ -254,21 +259,47 @@ def gen_c5(n, U, P, rank, device, seed):
     return pid, pk, value
 
 
-def verify_sharding(ids, world, base=0):
-    """The library's default privacy_id_sharding="verify" on this rank's
-    dataset-wide ids base + ids (ColumnarBackend._shard_privacy_ids: the distinct ids,
-    one all-to-all to their owner ranks, ValueError on an id held by two
-    ranks), run once before the timed region; returns its wall time in ms
-    (None at N = 1, where there is nothing to verify)."""
+def owned_identities(U, world, rank, device):
+    """Dataset-wide privacy-id identities of rank r's local codes k in [0, U):
+    the k-th non-negative integer that parallel.owner_of assigns to r, so the
+    ranks' ids are disjoint and hash-owned (as parallel.shard_by_privacy_id
+    or the "shuffle" mode leave them)."""
+    import torch
+    from pipelinedp_amd import parallel
+    n = int(U * world * 1.05) + 4096
+    while True:
+        c = torch.arange(n, device=device, dtype=torch.int64)
+        mine = c[parallel.owner_of(c, world) == rank]
+        if mine.numel() >= U:
+            return mine[:U].clone()
+        n *= 2
+
+
+def verify_sharding(ids, world, rank, U):
+    """The library's default privacy_id_sharding="verify"
+    (parallel.verify_privacy_id_sharding) on this rank's per-row dataset-wide
+    identities, run once before the timed region: one owner check per row and
+    a flag all-reduce (the id exchange only if some rank holds an id it does
+    not own).  Returns {ms, path} (None at N = 1, nothing to verify)."""
     import torch
     from pipelinedp_amd import parallel
     if world == 1:
         return None
+    ident = owned_identities(U, world, rank, ids.device)[ids]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    parallel.check_privacy_ids_disjoint(torch.unique(ids) + base)
+    path = parallel.verify_privacy_id_sharding(ident)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) * 1e3
+    ms = (time.perf_counter() - t0) * 1e3
+    del ident
+    return {"ms": ms, "path": path, "rows": int(ids.numel())}
+
+
+def tuning_of(args):
+    """The bench's data-movement knobs (identical results) as ColumnarBackend tuning."""
+    t = dict(key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band,
+             sieve_threads=args.sieve_threads, merge=args.merge)
+    return {k: v for k, v in t.items() if v}
 
 
 def run_api_workload(args, workload, world, rank, device):
@@ -285,15 +316,15 @@ def run_api_workload(args, workload, world, rank, device):
     n, U, P = args.rows or w["rows"], args.privacy_ids or w["privacy_ids"], w["partitions"]
     gen = gen_c4 if workload == "c4" else gen_c5
     pid, pk, value = gen(n, U, P, rank, device, 4000 if workload == "c4" else 5000)
-    # local privacy-id codes k in [0, U), dataset-wide id r * U + k (as in
-    # gen_c3): a rank's table is dense in its own ids, so its bounding plan
+    # local privacy-id codes k in [0, U), dataset-wide ids owned_identities
+    # (as in gen_c3): a rank's table is dense in its own ids, so its bounding plan
     # is the one-GPU plan (global codes in [0, U * world) would give 8x the
     # buckets at N = 8, past the bucketed plan's limit: the global-sketch path)
     torch.cuda.synchronize()
     # the default privacy_id_sharding="verify" on the dataset-wide ids, once,
     # before timing (the steps below pass "trusted": the check does not
     # change between steps)
-    verify_ms = verify_sharding(pid, world, rank * U)
+    verify_ms = verify_sharding(pid, world, rank, U)
     table = pdp.ColumnTable({"pid": pid, "pk": pk, "v": value}, n_privacy_ids=U, n_partitions=P)
     strategy = {"truncated_geometric": pdp.PartitionSelectionStrategy.TRUNCATED_GEOMETRIC,
                 "gaussian": pdp.PartitionSelectionStrategy.GAUSSIAN_THRESHOLDING,
@@ -314,10 +345,11 @@ def run_api_workload(args, workload, world, rank, device):
                              partition_extractor=pdp.ColumnExtractor("pk"),
                              value_extractor=pdp.ColumnExtractor("v"))
     ws = X.BoundWorkspace()
+    tune = tuning_of(args)
 
     def step():
         acc = pdp.NaiveBudgetAccountant(total_epsilon=EPS, total_delta=DELTA)
-        backend = CB.ColumnarBackend(privacy_id_sharding="trusted", workspace=ws)
+        backend = CB.ColumnarBackend(privacy_id_sharding="trusted", workspace=ws, tuning=tune)
         sink = pdp.DPEngine(acc, backend).aggregate(table, params, ext)
         acc.compute_budgets()
         return len(sink.collect()), backend
@@ -372,8 +404,11 @@ def run_api_workload(args, workload, world, rank, device):
         "kernels": {k: {"ms": kernel_ms[k], "launches_per_step": launches[k]} for k in kernel_ms},
         "bound_plan": None if info is None else {
             "algorithm": info.algorithm, "bucket_bits": info.bucket_bits, "n_buckets": info.n_buckets,
-            "lds_bytes": info.lds_bytes,
-            "key_format": {1: "wide", 2: "compact", 3: "packed"}.get(info.key_format, info.key_format)},
+            "lds_bytes": info.lds_bytes, "merge": info.merge, "sieve": info.sieve / 65536.0,
+            "band": info.band / 65536.0, "tuning": tune,
+            "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(info.key_format,
+                                                                                     info.key_format)},
+        "seed": None,
         "partitions_kept": kept,
         "privacy_id_verify_ms": verify_ms,
     }
@@ -577,16 +612,17 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         bounding, selection, ops = build_plan(C2["l0"], C2["linf"])
         pid, pk, value = gen_c2(n, U, P, rank, device, 1000)
     torch.cuda.synchronize()
-    # rank r holds the dataset-wide ids r * U + [0, U): checked once with the
-    # library's default verify (it raises on an id held by two ranks); the
-    # kernels take the local codes (ids relative to the rank's base)
-    verify_ms = verify_sharding(pid, world, rank * U)
+    # rank r holds the dataset-wide ids owned_identities(U, world, r): checked
+    # once with the library's default verify (it raises on an id held by two
+    # ranks); the kernels take the local codes
+    verify_ms = verify_sharding(pid, world, rank, U)
 
     P_pad, _ = parallel.partition_slices(P, world)
     ws = X.BoundWorkspace()
-    plan = X.bound_plan(n, U, P_pad, bounding, key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
+    tune = tuning_of(args)
+    plan = X.bound_plan(n, U, P_pad, bounding, **tune)
     acc = X.new_accumulators(P_pad, bounding, device)
-    seed_base = parallel.broadcast_seeds((int.from_bytes(os.urandom(8), "little"),))[0]
+    seed_base = args.seed
 
     def step(i):
         for t in acc.values():
@@ -594,7 +630,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                 t.zero_()
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
-                           check_keys=False, key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
+                           check_keys=False, **tune)
         mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
@@ -618,8 +654,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     elapsed = time.perf_counter() - t0
     # key-error check of the data once (outside the timed region)
     X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding, seed=1,
-                       row_offset=rank * n, acc=acc, workspace=ws, check_keys=True,
-                       key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band)
+                       row_offset=rank * n, acc=acc, workspace=ws, check_keys=True, **tune)
     # per-kernel times from a second, untimed pass of the same steps: the HIP
     # events the profiler records around every launch (on its launch stream)
     # would otherwise sit inside the timed region
@@ -702,7 +737,9 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                        "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
                        "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(
                            plan.key_format, plan.key_format),
-                       "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0, "stats": stats},
+                       "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0,
+                       "sieve_threads": plan.sieve_threads, "stats": stats},
+        "seed": args.seed,
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,
         "step_ms_spread": ({"n": len(samples), "min": min(samples), "median": float(np.median(samples)),
@@ -780,8 +817,9 @@ def main():
         "path_roofline": r["path_roofline"],
         "kernels": r["kernels"],
         "bound_plan": r["bound_plan"],
+        "seed": r.get("seed"),
         "partitions_kept": r["partitions_kept"],
-        "privacy_id_verify_ms": r.get("privacy_id_verify_ms"),
+        "privacy_id_verify": r.get("privacy_id_verify_ms"),
         "step_ms_spread": r.get("step_ms_spread"),
         "api": r["api"],
         "cpu_baseline": cpu[0] if cpu else None,

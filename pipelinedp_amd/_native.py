@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 10
+ABI_VERSION = 11
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "pdp_dataset_histograms_preaggregated_weight_offsets",
     "pdp_dataset_histograms_weight_bins",
     "pdp_bound_error_flags",
+    "pdp_owner_mismatches",
     "pdp_bound_stats_read",
     "pdp_profiler_enable",
     "pdp_profiler_report",
@@ -95,6 +96,7 @@ class BoundConfig(ctypes.Structure):
         ("key_format", ctypes.c_int32),
         ("sieve", ctypes.c_int32),
         ("sieve_band", ctypes.c_int32),
+        ("sieve_threads", ctypes.c_int32),
     ]
 
 
@@ -113,6 +115,7 @@ class BoundPlanInfo(ctypes.Structure):
         ("key_format", ctypes.c_int32),
         ("sieve", ctypes.c_int32),
         ("band", ctypes.c_int32),
+        ("sieve_threads", ctypes.c_int32),
     ]
 
 
@@ -243,6 +246,7 @@ def signatures():
         "pdp_dataset_histograms_preaggregated_weight_offsets": (ctypes.c_int, [i64, i64, P(u64), P(u64), P(u64)]),
         "pdp_dataset_histograms_weight_bins": (ctypes.c_int, [vp, vp, i64, P(HistogramBins), vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
+        "pdp_owner_mismatches": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),
         "pdp_bound_stats_read": (ctypes.c_int, [P(BoundConfig), vp, u64, P(BoundStats), vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),

@@ -434,7 +434,7 @@ def shard_rows_by_privacy_id(mode, pid_t, pk_t, val_t, pid_enc):
     table = None if pid_enc.decode is None else \
         torch.as_tensor(parallel.key_identities(pid_enc.decode)).to(pid_t.device)
     if mode == "verify":
-        parallel.check_privacy_ids_disjoint(torch.unique(pid_t) if table is None else table)
+        parallel.verify_privacy_id_sharding(pid_t if table is None else table)
         return pid_t, pk_t, val_t, pid_enc
     ident = pid_t if table is None else table[pid_t]
     ident, (pk_t, val_t) = parallel.shuffle_by_privacy_id(ident, [pk_t, val_t])
@@ -442,6 +442,18 @@ def shard_rows_by_privacy_id(mode, pid_t, pk_t, val_t, pid_enc):
     pid_t = inv.to(torch.int64).contiguous()
     return pid_t, pk_t.contiguous(), None if val_t is None else val_t.contiguous(), \
         C.EncodedKeys(pid_t, max(int(uniq.numel()), 1), None)
+
+
+def parse_tuning(text: str) -> dict:
+    """"k=v,k=v" (PIPELINEDP_AMD_TUNING) -> {k: int(v)} over ColumnarBackend.TUNING_KEYS."""
+    out = {}
+    for item in filter(None, (t.strip() for t in text.split(","))):
+        k, sep, v = item.partition("=")
+        if not sep or k.strip() not in ColumnarBackend.TUNING_KEYS:
+            raise ValueError(f"PIPELINEDP_AMD_TUNING: bad item {item!r} (keys: "
+                             f"{', '.join(ColumnarBackend.TUNING_KEYS)})")
+        out[k.strip()] = int(v)
+    return out
 
 
 class ColumnarBackend(pipeline_backend.PipelineBackend):
@@ -461,10 +473,17 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
         skips the check (the caller guarantees it).
       workspace: an executor.BoundWorkspace to reuse (the bounding kernels'
         device workspace; by default each backend keeps its own across runs).
+      tuning: data-movement knobs of the bounding kernels, all of which keep
+        the results identical (pdp_bound_config: algorithm, merge,
+        key_format, sieve, sieve_band, sieve_threads); default {} = the
+        library's plan.  The environment variable PIPELINEDP_AMD_TUNING
+        ("sieve=16384,merge=1") supplies defaults for it.
     """
 
+    TUNING_KEYS = ("algorithm", "merge", "key_format", "sieve", "sieve_band", "sieve_threads")
+
     def __init__(self, device=None, seed: Optional[int] = None, privacy_id_sharding: str = "verify",
-                 workspace=None):
+                 workspace=None, tuning: Optional[dict] = None):
         if privacy_id_sharding not in ("verify", "shuffle", "trusted"):
             raise ValueError(f"privacy_id_sharding must be 'verify', 'shuffle' or 'trusted', "
                              f"got {privacy_id_sharding!r}")
@@ -472,6 +491,11 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
         self._seed = seed
         self._pid_sharding = privacy_id_sharding
         self._workspace = workspace
+        self._tuning = parse_tuning(os.environ.get("PIPELINEDP_AMD_TUNING", ""))
+        for k, v in (tuning or {}).items():
+            if k not in self.TUNING_KEYS:
+                raise ValueError(f"unknown tuning key {k!r} (one of {', '.join(self.TUNING_KEYS)})")
+            self._tuning[k] = int(v)
         self.last_plan_info = None
 
     # ---------------------------------------------------- recorded ops --
@@ -681,10 +705,11 @@ class AggregateRun:
         else:
             if self.backend._workspace is None:
                 self.backend._workspace = X.BoundWorkspace()
+            tune = self.backend._tuning
             acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=n_pid, n_partitions=P,
                                      bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset,
-                                     workspace=self.backend._workspace)
-            self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec)
+                                     workspace=self.backend._workspace, **tune)
+            self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec, **tune)
         return acc, spec, pk_enc, allowed
 
     def _selection(self):

@@ -32,6 +32,7 @@
 //    k_pair_sketch / k_pair_rows / k_reduce_pairs: the same sketches in HBM,
 //    updated with device-scope atomics.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -112,11 +113,36 @@ inline bool l1_hist_u16(int key_format, int64_t n_buckets) {
 // the list in front of the exact bitmap), a scatter into bucket order and a
 // second bucket-kernel launch whose pair records follow the main ones.
 // Kept pairs and rows are exactly those of the unsieved path.
+#ifndef PDP_SIEVE_BUFS
+#define PDP_SIEVE_BUFS 2
+#endif
+#ifndef PDP_SIEVE_EARLY
+#define PDP_SIEVE_EARLY 0
+#endif
 constexpr int kSieveChunkItems = 4;                            // rows per thread and chunk
-constexpr int kSieveBufs = 2;  // full tiles: chunks of loads in flight (register buffers)
-constexpr int kSieveChunk = kL1Threads * kSieveChunkItems;     // rows filtered per chunk
-constexpr int kSieveCap = 12288;                               // candidate slots of the LDS stage
-constexpr int kSieveItems = kSieveCap / kL1Threads;            // per thread at a flush
+constexpr int kSieveBufs = PDP_SIEVE_BUFS;  // full tiles: chunks of loads in flight (register buffers)
+constexpr int kSieveItems = 12;  // stage slots per thread (records each thread handles at a flush)
+// Two workgroup shapes (Plan.sieve_threads):
+//  1,024 threads, a 12,288-candidate stage, 8 flush slots per tile: one
+//    workgroup per CU (~150 KiB of LDS), whose flush (LDS counting sort +
+//    block write) stalls the CU's loads;
+//  512 threads, a 6,144-candidate stage, 16 flush slots per tile, <= 80 KiB of
+//    LDS: two workgroups per CU, so one's flush overlaps the other's loads.
+template <int TH>
+struct SieveShape {
+  static constexpr int kChunk = TH * kSieveChunkItems;  // rows filtered per chunk
+  static constexpr int kCap = TH * kSieveItems;         // candidate slots of the LDS stage
+  static constexpr int kSlots = TH == 1024 ? 8 : 16;    // flush blocks per tile, at most
+  static constexpr int kSlotBits = TH == 1024 ? 3 : 4;
+  // a tile flushes at most once per chunk, and every flush but its last holds
+  // > kCap - kChunk records, so its blocks fit the kSlots level-1 slots
+  static_assert((1 << kSlotBits) == kSlots, "slot bits");
+  static_assert(kTileRows / kChunk <= kSlots || kTileRows / (kCap - kChunk + 1) + 1 <= kSlots,
+                "sieve flushes per tile");
+  static_assert(kCap <= 65535, "u16 run offsets");
+};
+constexpr int kSieveThreads2 = 512;
+constexpr int64_t kSieveLds2 = 80 * 1024 - 256;  // two 512-thread workgroups per CU
 // a tile's flush blocks lie back to back from tile * kSieveTileStride
 constexpr int64_t kSieveTileStride = kTileRows;
 constexpr int kSieveMaxT16 = 1 << 15;                          // t <= 1/2
@@ -131,26 +157,22 @@ constexpr int kRescanBlocks = 1024;
 // tile groups per level-2 workgroup with the sieve, at most: the plan takes
 // as many as keep a workgroup's expected records (tiles x candidates per tile
 // / super-buckets) within one LDS window (kL2Target), since a second window
-// holding a few hundred records costs as much latency as a full one
+// holding a few hundred records costs as much latency as a full one; and no
+// more than one level-1 slot per level-2 thread
 constexpr int kSieveL2Groups = 4;
 constexpr double kL2Target = 7000.0;
-// a tile flushes at most once per chunk, and every flush but its last holds
-// > kSieveCap - kSieveChunk records, so its blocks fit the kStagesPerTile
-// level-1 slots
-static_assert(kTileRows / kSieveChunk <= kStagesPerTile ||
-                  kTileRows / (kSieveCap - kSieveChunk + 1) + 1 <= kStagesPerTile,
-              "sieve flushes per tile");
-static_assert(kSieveCap <= 65535, "u16 run offsets");
-size_t sieve_stage_bytes(int key_format);  // LDS of the sieve's level-1 stage (after StageLds)
+size_t sieve_stage_bytes(int key_format, int threads);  // LDS of the sieve's level-1 stage (after StageLds)
 // the side band (Plan.band): rows with t <= pair hash < t2 = 2t leave level 1
 // as (privacy id << 32 | row) in a per-tile list, through a per-wave LDS queue
 // written out 64 entries at a time; the fix-up reads that list instead of the
 // whole privacy-id column, and only a privacy id with fewer than l0 distinct
 // pairs below t2 still needs the rescan
 constexpr int kBandQueue = 128;
-constexpr int64_t kBandLds = (kL1Threads / 64) * kBandQueue * 8;
-inline bool sieve_hist_u16(int key_format, int64_t n_buckets, bool band) {
-  return (int64_t)sieve_stage_bytes(key_format) + l1_hist_bytes(n_buckets, false) + (band ? kBandLds : 0) > kL1LocalLds;
+inline int64_t sieve_band_lds(int threads) { return (threads / 64) * kBandQueue * 8; }
+// LDS of a sieve workgroup: stage, bucket counts (u32, or u16 pairs), band queues
+inline int64_t sieve_lds(int key_format, int threads, int64_t n_buckets, bool u16, bool band) {
+  return ((int64_t)sieve_stage_bytes(key_format, threads) + 7) / 8 * 8 + l1_hist_bytes(n_buckets, u16) +
+         (band ? sieve_band_lds(threads) : 0);
 }
 
 struct Plan {
@@ -176,9 +198,12 @@ struct Plan {
   int64_t n_stages;     // level-1 stages of kL1Rows rows
   int sieve;            // threshold sieve: t = sieve / 2^16 (0 = off); k_sieve_l1 instead of k_scatter_l1_local
   int band;             // side band: t2 = band / 2^16 (0 = off; else 2 * sieve, <= 1/2)
-  int64_t n_slots1;     // level-1 blocks (stages, or sieve flush slots: n_tiles * kStagesPerTile)
+  int64_t n_slots1;     // level-1 blocks (stages, or sieve flush slots: n_tiles << slot_bits)
   int64_t buckets_out;  // buckets of pair records: n_buckets, x2 with the sieve (fix-up after), x3 with the band
   int l2_mult;          // tile groups per level-2 workgroup (1 without the sieve)
+  int sieve_threads;    // k_sieve_l1 workgroup: 1,024 or 512 threads (SieveShape)
+  int slot_bits;        // level-1 blocks per tile = 2^slot_bits (kStagesPerTile, or SieveShape::kSlots)
+  int hist_u16;         // tile-local level 1 counts buckets in u16 halves (counts_tm / counts_tm2)
 };
 
 int64_t per_pid_lds(const pdp_bound_config* c) {
@@ -291,7 +316,7 @@ Plan make_plan(const pdp_bound_config* c) {
   // words per bucket, and the sieve's larger LDS stage must fit
   const bool sieve_ok = p.algorithm == PDP_ALGO_BUCKETED && p.l1_local && p.merge == PDP_MERGE_RANGES &&
                         p.bucket_bits >= 6 && p.key_format != PDP_KEYS_WIDE &&
-                        (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) <= kL1LocalLds &&
+                        sieve_lds(p.key_format, kL1Threads, p.n_buckets, true, false) <= kL1LocalLds &&
                         p.n_tiles * kSieveTileStride < ((int64_t)1 << 32) &&
                         c->n_privacy_ids < ((int64_t)1 << 32) - 1;  // fix-up lists hold 32-bit ids
   int t16 = 0;
@@ -310,7 +335,7 @@ Plan make_plan(const pdp_bound_config* c) {
   p.band = 0;
   if (p.sieve) {
     const int t2 = 2 * p.sieve < kSieveMaxT16 ? 2 * p.sieve : kSieveMaxT16;
-    const bool fits = (int64_t)sieve_stage_bytes(p.key_format) + l1_hist_bytes(p.n_buckets, true) + kBandLds <= kL1LocalLds;
+    const bool fits = sieve_lds(p.key_format, kL1Threads, p.n_buckets, true, true) <= kL1LocalLds;
     // auto: only below t = 1/4 -- there an id short of l0 candidate pairs,
     // and with it the 8 B/row rescan, is likely (C3: t = 0.154, ~1,600 of 1e7
     // ids; C2's t = 0.325 leaves none, and the band would only cost level 1
@@ -318,7 +343,27 @@ Plan make_plan(const pdp_bound_config* c) {
     const bool want = c->sieve_band > 0 || (c->sieve_band == 0 && p.sieve <= kSieveMaxT16 / 2);
     if (t2 > p.sieve && fits && want) p.band = t2;
   }
-  p.n_slots1 = p.sieve ? p.n_tiles * kStagesPerTile : p.n_stages;
+  // the sieve's workgroup: 1,024 threads (auto), or on request two 512-thread
+  // ones per CU when their LDS fits (C3: 6.86 vs 6.56 ms, level 1 3.51 vs
+  // 3.44 ms and level 2 0.97 vs 0.80 ms over twice the flush blocks,
+  // profiles/r04/ab/ab1_sieve_threads.txt)
+  p.sieve_threads = kL1Threads;
+  p.hist_u16 = p.l1_local ? (int)l1_hist_u16(p.key_format, p.n_buckets) : 0;
+  if (p.sieve) {
+    const bool band = p.band != 0;
+    p.hist_u16 = sieve_lds(p.key_format, kL1Threads, p.n_buckets, false, band) > kL1LocalLds;
+    const bool u16_2 = sieve_lds(p.key_format, kSieveThreads2, p.n_buckets, false, band) > kSieveLds2;
+    const bool fits2 = sieve_lds(p.key_format, kSieveThreads2, p.n_buckets, u16_2, band) <= kSieveLds2;
+    if (fits2 && c->sieve_threads == kSieveThreads2) {
+      p.sieve_threads = kSieveThreads2;
+      p.hist_u16 = u16_2;
+    }
+  }
+  p.slot_bits = p.sieve_threads == kSieveThreads2 ? SieveShape<kSieveThreads2>::kSlotBits
+                                                   : SieveShape<kL1Threads>::kSlotBits;
+  if (!p.sieve) p.slot_bits = 3;
+  static_assert(kStagesPerTile == 8, "non-sieve level-1 stages per tile = 2^3");
+  p.n_slots1 = p.sieve ? p.n_tiles << p.slot_bits : p.n_stages;
   p.buckets_out = p.sieve ? (p.band ? 3 : 2) * p.n_buckets : p.n_buckets;
   p.l2_mult = 1;
   if (p.sieve) {
@@ -326,7 +371,9 @@ Plan make_plan(const pdp_bound_config* c) {
     const double per_group = (double)kL2GroupTiles * (double)kTileRows * ((double)p.sieve / 65536.0) /
                              (double)(p.n_supers > 0 ? p.n_supers : 1);
     int m = (int)(kL2Target / (per_group > 1.0 ? per_group : 1.0));
-    p.l2_mult = m < 1 ? 1 : (m > kSieveL2Groups ? kSieveL2Groups : m);
+    const int m_max = kL2Threads / (kL2GroupTiles << p.slot_bits);  // one slot per level-2 thread
+    const int cap = kSieveL2Groups < m_max ? kSieveL2Groups : m_max;
+    p.l2_mult = m < 1 ? 1 : (m > cap ? cap : m);
   }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
     p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
@@ -365,6 +412,10 @@ struct Ws {
   // bucket (-> starts) and their write cursors; the fix-up row list itself
   // reuses keys1 (dead after level 2), its bucket-ordered records keys2/rows2
   uint64_t sbase, unres_bits, unres_list, sctl, fix_cnt, fix_cur;
+  // the fix-up's (id << 32 | row) list: the level-1 region (keys1, and rows1
+  // right after it for COMPACT records), dead after level 2; fix_cap entries
+  // (>= n_rows: every list holds distinct rows)
+  uint64_t fix_rec, fix_cap;
   // side band: per-tile (pid << 32 | row) lists and their lengths; the ids
   // still unresolved after the band fix-up (bitmap, list, {count, rows}) and
   // their rescan's per-bucket counts / cursors
@@ -399,7 +450,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
-    const bool u16 = p.sieve ? sieve_hist_u16(p.key_format, p.n_buckets, p.band != 0) : l1_hist_u16(p.key_format, p.n_buckets);
+    const bool u16 = p.hist_u16 != 0;
     if (p.l1_local && u16) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
@@ -418,6 +469,11 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
                                 : (p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n);
     w.keys1 = off; off = align256(off + n1 * (packed ? 8 : kb1));
     if (!packed) { w.rows1 = off; off = align256(off + n1 * 4); }
+    if (p.sieve) {  // the fix-up list reuses [keys1, end of rows1), at least 8 B per row
+      if (off - w.keys1 < 8 * n) off = w.keys1 + align256(8 * n);
+      w.fix_rec = w.keys1;
+      w.fix_cap = (off - w.keys1) / 8;
+    }
     if (p.l1_local) { w.soff = off; off = align256(off + (uint64_t)p.n_slots1 * (p.n_supers + 1) * 2); }
     if (p.sieve) {
       const uint64_t ids = (uint64_t)p.n_buckets << p.bucket_bits;
@@ -473,6 +529,13 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
   return w;
 }
 
+// PDP_DEBUG_CORRUPT_RECORDS deliberately corrupts the level-2 records: only
+// accepted when the process asked for test hooks
+bool test_hooks_enabled() {
+  const char* v = std::getenv("PIPELINEDP_AMD_TEST_HOOKS");
+  return v != nullptr && v[0] == '1';
+}
+
 int validate(const pdp_bound_config* c) {
   if (c == nullptr) return set_error(PDP_E_INVALID, "config is NULL");
   if (c->n_rows < 0 || c->n_rows >= ((int64_t)1 << 32))
@@ -497,6 +560,10 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad merge");
   if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED_WIDE)
     return set_error(PDP_E_INVALID, "bad key_format");
+  if (c->sieve_threads != 0 && c->sieve_threads != kSieveThreads2 && c->sieve_threads != kL1Threads)
+    return set_error(PDP_E_INVALID, "sieve_threads must be 0, 512 or 1024");
+  if ((c->flags & PDP_DEBUG_CORRUPT_RECORDS) && !test_hooks_enabled())
+    return set_error(PDP_E_INVALID, "PDP_DEBUG_CORRUPT_RECORDS is a test hook: set PIPELINEDP_AMD_TEST_HOOKS=1");
   if (pairs_mode(c)) return pairs_validate(c);
   if (make_plan(c).algorithm < 0)
     return set_error(PDP_E_UNSUPPORTED, "bucketed algorithm / range merge / compact keys infeasible for this l0/linf/U/P");
@@ -522,6 +589,8 @@ struct KP {  // kernel parameters
   int sieve_mark;       // bucket kernel: mark privacy ids with < l0 candidate pairs unresolved
   uint32_t band_t32;    // side band: level 1 lists rows with sieve_t32 <= pair_hash < band_t32 (0 = off)
   int sieve_emit;       // bucket kernel (main launch, band on): unresolved ids' candidate rows -> fix_rec
+  int slot_bits;        // level-1 blocks per tile = 2^slot_bits (Plan.slot_bits)
+  int64_t fix_cap;      // sieve: entries the fix-up row list (fix_rec, Ws.fix_rec) holds
 };
 
 KP make_kp(const pdp_bound_config* c, const Plan& p) {
@@ -548,6 +617,8 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.sieve_mark = p.sieve != 0;
   k.band_t32 = (uint32_t)p.band << 16;
   k.sieve_emit = p.band != 0;
+  k.slot_bits = p.slot_bits;
+  k.fix_cap = 0;  // set from the layout (Ws.fix_cap) where the fix-up runs
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -866,13 +937,18 @@ size_t l1_stage_bytes(int key_format) {
   }
 }
 
-size_t sieve_stage_bytes(int key_format) {
+template <int TH>
+size_t sieve_stage_bytes_t(int key_format) {
   switch (key_format) {
-    case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kSieveItems, kL1Threads>);
+    case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kSieveItems, TH>);
     case PDP_KEYS_PACKED:
-    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kSieveItems, kL1Threads>);
-    default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kSieveItems, kL1Threads>);
+    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kSieveItems, TH>);
+    default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kSieveItems, TH>);
   }
+}
+size_t sieve_stage_bytes(int key_format, int threads) {
+  return threads == kSieveThreads2 ? sieve_stage_bytes_t<kSieveThreads2>(key_format)
+                                   : sieve_stage_bytes_t<kL1Threads>(key_format);
 }
 
 // phase 1: histogram + local rank (dest < 0 = drop the row)
@@ -1410,8 +1486,8 @@ __device__ unsigned g_phase_l1, g_phase_l2, g_phase_bk;  // profiling builds: pr
 // << 32 | row), to this tile's band list band[t * 65,536 ...], through a
 // per-wave LDS queue flushed 64 entries (512 contiguous bytes) at a time;
 // band_cnt[t] = the list's length
-template <int FMT, bool U16, bool BAND>
-__global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
+template <int FMT, bool U16, bool BAND, int TH>
+__global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
                                                          const int64_t* __restrict__ pk,
                                                          const uint8_t* __restrict__ allowed,
                                                          unsigned* __restrict__ counts_tm,
@@ -1422,10 +1498,13 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
                                                          unsigned long long* __restrict__ band,
                                                          unsigned* __restrict__ band_cnt) {
   using K = L1Key<FMT>;
+  using SS = SieveShape<TH>;
   constexpr bool ROWS = !kPackedL1<FMT>;
   constexpr int Q = kSieveChunkItems;
+  constexpr int kSieveChunk = SS::kChunk;
+  constexpr int kSieveCap = SS::kCap;
   extern __shared__ unsigned long long stage_raw[];
-  using SL = StageLds<K, kSmallDest, ROWS, kSieveItems, kL1Threads>;
+  using SL = StageLds<K, kSmallDest, ROWS, kSieveItems, TH>;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
   unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);
   // BAND: the per-wave queues after the bucket counts (l1_hist_bytes)
@@ -1433,14 +1512,15 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
       stage_raw + (sizeof(SL) + 7) / 8 + (((U16 ? 2 : 4) * kp.n_buckets + 15) / 16 * 16) / 8;
   __shared__ unsigned fill, bfill;
   const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
-  for (int64_t b = threadIdx.x; b < n_words; b += blockDim.x) bh[b] = 0;
+  for (int64_t b = threadIdx.x; b < n_words; b += TH) bh[b] = 0;
+  for (int B = threadIdx.x; B < (int)kp.n_supers; B += TH) s.hist[B] = 0;
   if (threadIdx.x == 0) {
     fill = 0;
     bfill = 0;
   }
   __syncthreads();
   auto flush_counts = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
-    for (int64_t wd = threadIdx.x; wd < n_words; wd += blockDim.x) {
+    for (int64_t wd = threadIdx.x; wd < n_words; wd += TH) {
       const unsigned v = bh[wd];
       bh[wd] = 0;
       if constexpr (U16) {
@@ -1474,28 +1554,10 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
 #ifdef PDP_PHASE_CLOCK
     const unsigned long long f0 = wall_clock64();
 #endif
-    // runs per super-bucket: LDS histogram, one-wave scan
-    for (int B = threadIdx.x; B < nd; B += blockDim.x) s.hist[B] = 0;
-    __syncthreads();
-    // runs per super-bucket, and the tile's candidates per bucket (counted
-    // here, on the compacted stage, rather than per row)
-    // (each entry's rank in its run is taken here, so the scatter below
-    // needs no second round of contended LDS atomics)
-    const uint64_t mid_mask = ((uint64_t)1 << mid_bits) - 1;
-    unsigned rk[kSieveItems];
-#pragma unroll
-    for (int j = 0; j < kSieveItems; ++j) {
-      const unsigned e = threadIdx.x + (unsigned)j * blockDim.x;
-      rk[j] = 0;
-      if (e >= total) continue;
-      const unsigned dd = s.dest[e];
-      rk[j] = atomicAdd(s.hist + dd, 1u);
-      const int64_t bkt = ((int64_t)dd << kp.super_bits) |
-                          (int64_t)((((uint64_t)s.keys[e] >> kp.pk_bits) & mid_mask) >> kp.bucket_bits);
-      if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
-      else atomicAdd(bh + bkt, 1u);
-    }
-    __syncthreads();
+    // the stage's runs per super-bucket were counted as its records were
+    // appended (s.hist; the tile's bucket counts too), so the flush is a
+    // one-wave scan and one pass that places each record through an LDS
+    // cursor per run: little work while the CU's loads are stalled
     if (threadIdx.x < 64) {
       unsigned carry = 0;
       for (int base = 0; base < nd; base += 64) {
@@ -1505,24 +1567,25 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
           const unsigned up = __shfl_up(incl, off, 64);
           if (lane >= off) incl += up;
         }
-        if (base + lane < nd) s.start[base + lane] = carry + incl - v;
+        if (base + lane < nd) s.start[base + lane] = s.gcur[base + lane] = written + carry + incl - v;
         carry += __shfl(incl, 63, 64);
       }
     }
     __syncthreads();
+    for (int B = threadIdx.x; B < nd; B += TH) s.hist[B] = 0;  // the next stage's counts (not read below)
     // every record straight to its run: the block (<= kSieveCap records) is
     // written whole by this workgroup, so its partial lines merge in L2
 #pragma unroll
     for (int j = 0; j < kSieveItems; ++j) {
-      const unsigned e = threadIdx.x + (unsigned)j * blockDim.x;
+      const unsigned e = threadIdx.x + (unsigned)j * TH;
       if (e >= total) continue;
-      const unsigned pos = written + s.start[s.dest[e]] + rk[j];
+      const unsigned pos = atomicAdd(s.gcur + s.dest[e], 1u);
       blk[pos] = s.keys[e];
       if (ROWS) rblk[pos] = s.rows[e];
     }
-    const int64_t sl = t * kStagesPerTile + slot;
-    for (int B = threadIdx.x; B <= nd; B += blockDim.x)
-      soff[sl * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] : total);
+    const int64_t sl = t * SS::kSlots + slot;
+    for (int B = threadIdx.x; B <= nd; B += TH)
+      soff[sl * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] - written : total);
     if (threadIdx.x == 0) {
       sbase[sl] = written;
       fill = 0;
@@ -1547,7 +1610,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
     auto load = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
 #pragma unroll
       for (int q = 0; q < Q; q += 2) {
-        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x);
+        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH);
         if constexpr (FULL) {
           const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
           const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
@@ -1563,48 +1626,65 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         }
       }
     };
-    // one chunk: filter, then (its registers free) the loads of the chunk two
-    // ahead go out, then append / flush -- two chunks of loads in flight
+    // one chunk: its keys narrowed to 32 bits and range-checked (sieve plans
+    // have U < 2^32 - 1 and P < 2^32), which frees the load registers, so the
+    // loads of the chunk two ahead go out before the hashing; then filter,
+    // append / flush -- two chunks of loads in flight almost all the time
     auto body = [&](int64_t c0, int64_t (&u)[Q], int64_t (&k)[Q]) {
       const bool more = c0 + kSieveChunk < t1;  // block-uniform
-      bool cand[Q], bnd[Q];
-      int d[Q];
-      K x[Q];
-      uint8_t pub[Q];  // public partitions: the rows' mask bytes, gathered together (one wait)
-#pragma unroll
-      for (int q = 0; q < Q; ++q) pub[q] = 1;
-      if (allowed != nullptr) {  // block-uniform
-#pragma unroll
-        for (int q = 0; q < Q; ++q) pub[q] = allowed[(uint64_t)k[q] < (uint64_t)kp.P ? k[q] : 0];
-      }
+      bool cand[Q], bnd[Q], ok[Q];
+      uint32_t ul[Q], kl[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
-        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+        const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1);
         const bool valid = FULL || i < t1;
         const bool in_range = (uint64_t)u[q] < (uint64_t)kp.U && (uint64_t)k[q] < (uint64_t)kp.P;
-        bad |= valid && !in_range;
-        // every term evaluated (no short circuit: no branch, no per-row load wait);
-        // a non-public partition's rows are dropped
-        bool c = valid & in_range & (pub[q] != 0);
-        const uint32_t h = pair_hash(kp.seed, u[q], k[q]);
-        bnd[q] = BAND && (c & (h >= t32) & (h < kp.band_t32));
-        c = c & (h < t32);
-        cand[q] = c;
-        d[q] = (int)(u[q] >> mid_bits);
+        bad |= valid & !in_range;
+        ok[q] = valid & in_range;
+        ul[q] = (uint32_t)u[q];
+        kl[q] = (uint32_t)k[q];
+      }
+      if (allowed != nullptr) {  // block-uniform; the mask bytes gathered and used before the prefetch
+        uint8_t pub[Q];          // (one in-order vmcnt: a later use would wait for the prefetch too)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) pub[q] = allowed[ok[q] ? kl[q] : 0u];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) ok[q] = ok[q] & (pub[q] != 0);  // a non-public partition's rows are dropped
+      }
+      // two buffers: the next loads go out now; three or more: after the
+      // append / flush below, so that a flush runs with the other buffers'
+      // loads in flight and this one's registers free (the register peak)
+      constexpr bool kEarly = !FULL || kSieveBufs < 3 || PDP_SIEVE_EARLY;
+      auto prefetch = [&]() {
+        if constexpr (FULL) {
+          const int64_t cp = c0 + kSieveBufs * kSieveChunk < t1 ? c0 + kSieveBufs * kSieveChunk : t1 - kSieveChunk;
+          load(cp, u, k);
+        } else {
+          if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
+        }
+      };
+      if constexpr (kEarly) prefetch();
+      int d[Q];
+      K x[Q];
+      const uint32_t mid_mask = (uint32_t)(((uint64_t)1 << mid_bits) - 1);
+      const uint32_t row0 = (uint32_t)(c0 - t0) + 2u * threadIdx.x;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        // every term evaluated (no short circuit: no branch); the pair hash
+        // of an id below 2^32 (pid_hash's high word is zero)
+        const uint32_t h = pair_hash_from((ul[q] ^ (uint32_t)kp.seed) * 0x9E3779B1U, kp.seed, (int64_t)kl[q]);
+        bnd[q] = BAND && (ok[q] & (h >= t32) & (h < kp.band_t32));
+        cand[q] = ok[q] & (h < t32);
+        d[q] = mid_bits < 32 ? (int)(ul[q] >> mid_bits) : 0;
+        const uint32_t mid = ul[q] & mid_mask;
         if constexpr (FMT == PDP_KEYS_COMPACT) {
-          x[q] = (K)compact_key(kp, u[q], k[q], false);
-        } else {  // PACKED / PACKED_WIDE
-          x[q] = (K)packed_key(kp, u[q], k[q], (uint32_t)(i - t0), false);
+          x[q] = (K)((mid << kp.pk_bits) | kl[q]);
+        } else {  // PACKED / PACKED_WIDE: (row within the tile | mid | partition)
+          const uint32_t tile_row = row0 + (uint32_t)((q / 2) * 2 * TH) + (uint32_t)(q & 1);
+          x[q] = (K)(((uint64_t)tile_row << kPackedRowShift) | ((uint64_t)mid << kp.pk_bits) | (uint64_t)kl[q]);
         }
         // a band row is no candidate: its key slot carries its privacy id
-        // past the prefetch below, which reuses u[] / k[]
-        if constexpr (BAND) x[q] = bnd[q] ? (K)(uint32_t)u[q] : x[q];
-      }
-      if constexpr (FULL) {
-        const int64_t cp = c0 + kSieveBufs * kSieveChunk < t1 ? c0 + kSieveBufs * kSieveChunk : t1 - kSieveChunk;
-        load(cp, u, k);
-      } else {
-        if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
+        if constexpr (BAND) x[q] = bnd[q] ? (K)ul[q] : x[q];
       }
       // append this wave's candidates at one reserved range of the stage
       unsigned long long m[Q];
@@ -1623,7 +1703,12 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
           const unsigned pos = base + (unsigned)__popcll(m[q] & below);
           s.keys[pos] = x[q];
           s.dest[pos] = (typename SL::D)d[q];
-          if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1));
+          if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1));
+          // the stage's run lengths and the tile's bucket counts (bucket = id >> bucket_bits)
+          atomicAdd(s.hist + d[q], 1u);
+          const unsigned bkt = ul[q] >> kp.bucket_bits;
+          if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+          else atomicAdd(bh + bkt, 1u);
         }
         base += (unsigned)__popcll(m[q]);
       }
@@ -1632,7 +1717,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
         for (int q = 0; q < Q; ++q) {
           const unsigned long long mb = __ballot(bnd[q]);
           if (mb == 0) continue;  // wave-uniform
-          const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * blockDim.x) + (q & 1);
+          const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1);
           if (bnd[q]) wq[qn + __popcll(mb & below)] = ((unsigned long long)(uint32_t)x[q] << 32) | (uint32_t)i;
           qn += __popcll(mb);
           if (qn >= 64) {
@@ -1654,20 +1739,24 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
       const unsigned f = fill;
       if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
       else __syncthreads();  // every thread has read `fill` before the next chunk's appends
+      if constexpr (!kEarly) prefetch();
       if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
         flush_counts(counts_tm + t * kp.n_buckets);
         __syncthreads();
       }
     };
     if constexpr (FULL) {  // a fixed trip count: the same loads are pending on every path
-      static_assert((kTileRows / kSieveChunk) % kSieveBufs == 0, "chunk groups per tile");
+      constexpr int kChunks = (int)(kTileRows / kSieveChunk);
+      constexpr int kRest = kChunks % kSieveBufs;  // chunks after the last whole ring turn
       int64_t ub[kSieveBufs][Q], kb[kSieveBufs][Q];
 #pragma unroll
       for (int b = 0; b < kSieveBufs; ++b) load(t0 + (int64_t)b * kSieveChunk, ub[b], kb[b]);
-      for (int j = 0; j < (int)(kTileRows / kSieveChunk); j += kSieveBufs) {
+      for (int j = 0; j < kChunks - kRest; j += kSieveBufs) {
 #pragma unroll
         for (int b = 0; b < kSieveBufs; ++b) body(t0 + (int64_t)(j + b) * kSieveChunk, ub[b], kb[b]);
       }
+#pragma unroll
+      for (int b = 0; b < kRest; ++b) body(t0 + (int64_t)(kChunks - kRest + b) * kSieveChunk, ub[b], kb[b]);
     } else {  // the last tile, unaligned columns: two chunks in flight
       int64_t ua[Q], ka[Q], ub[Q], kb[Q];
       if (t0 < t1) load(t0, ua, ka);
@@ -1698,9 +1787,9 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
            wall_clock64() - t_start, fl_ticks);
 #endif
   // the tile's unused slots: empty runs
-  for (int j = slot; j < kStagesPerTile; ++j) {
-    const int64_t sl = t * kStagesPerTile + j;
-    for (int B = threadIdx.x; B <= nd; B += blockDim.x) soff[sl * (nd + 1) + B] = 0;
+  for (int j = slot; j < SS::kSlots; ++j) {
+    const int64_t sl = t * SS::kSlots + j;
+    for (int B = threadIdx.x; B <= nd; B += TH) soff[sl * (nd + 1) + B] = 0;
     if (threadIdx.x == 0) sbase[sl] = written;
   }
   __syncthreads();
@@ -1709,7 +1798,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
   } else {
     flush_counts(counts_tm + t * kp.n_buckets);
     if constexpr (U16)
-      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.n_buckets + b] = 0;
+      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.n_buckets + b] = 0;
   }
 }
 
@@ -1720,7 +1809,7 @@ __global__ void __launch_bounds__(kL1Threads) k_sieve_l1(KP kp, const int64_t* _
 // LDS map (the run of every record, in the stage's destination-tag array
 // before the counting sort reuses it) lets each thread address its own
 // records, so all of a thread's loads go out together.  Cursors as in
-// k_scatter_l2; PACKED rows are (stage / kStagesPerTile) * 65,536 + tile row.
+// k_scatter_l2; PACKED rows are (stage >> slot_bits) * 65,536 + tile row.
 // level-2 key of a packed level-1 record w (bit 63 dead): COMPACT u32
 // (bit 31 dead | local pid | partition) or, PACKED_WIDE, the same fields in a u64
 template <typename KO>
@@ -1783,8 +1872,16 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   const int64_t g = (kx / nd) * 8 + (lin & 7);
   const int B = (int)(kx % nd);
   if (g >= n_grp) return;  // block-uniform
-  const int64_t S0 = g * kL2Runs * M;
-  const int64_t n_all = kp.n_slots1 - S0 < (int64_t)kL2Runs * M ? kp.n_slots1 - S0 : (int64_t)kL2Runs * M;
+  const int64_t runs = ((int64_t)kL2GroupTiles << kp.slot_bits) * M;  // level-1 slots of the workgroup
+  const int64_t S0 = g * runs;
+  const int64_t n_all = kp.n_slots1 - S0 < runs ? kp.n_slots1 - S0 : runs;
+  // this workgroup's bucket write cursors: loaded first, so that their
+  // latency overlaps the run table's loads below (thread t < 2^super_bits)
+  const int nsub = 1 << kp.super_bits;
+  const int64_t s_first = (int64_t)B << kp.super_bits;
+  unsigned cur0 = 0;
+  if ((int)threadIdx.x < nsub && s_first + threadIdx.x < kp.n_buckets)
+    cur0 = bucket_start[s_first + threadIdx.x] + gcur[g * M * kp.n_buckets + s_first + threadIdx.x];
   unsigned len = 0, src = 0;
   if ((int64_t)threadIdx.x < n_all) {
     // block sl starts at sl * kL1Rows, or (sieve, sbase != NULL) at its
@@ -1792,7 +1889,7 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
     const int64_t sl = S0 + threadIdx.x;
     const uint16_t* o = soff + sl * (nd + 1) + B;
     len = (unsigned)o[1] - (unsigned)o[0];
-    src = (sbase != nullptr ? (unsigned)((sl / kStagesPerTile) * kSieveTileStride) + sbase[sl]
+    src = (sbase != nullptr ? (unsigned)((sl >> kp.slot_bits) * kSieveTileStride) + sbase[sl]
                             : (unsigned)(sl * kL1Rows)) + o[0];
   }
   unsigned total, nnz;
@@ -1804,9 +1901,8 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   }
   if (threadIdx.x == 0) rbeg[nnz] = total;
   const int nr = (int)nnz;
-  const int nsub = 1 << kp.super_bits;
-  const int64_t s_first = (int64_t)B << kp.super_bits;
-  for (int t = threadIdx.x; t < nsub; t += blockDim.x) {
+  if ((int)threadIdx.x < nsub) s.gcur[threadIdx.x] = cur0;
+  for (int t = threadIdx.x + blockDim.x; t < nsub; t += blockDim.x) {
     const int64_t b = s_first + t;
     s.gcur[t] = b < kp.n_buckets ? bucket_start[b] + gcur[g * M * kp.n_buckets + b] : 0u;
   }
@@ -2229,9 +2325,9 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
           unsigned base = 0;
           if (lane == lead) base = atomicAdd(sctl + 1, (unsigned)__popcll(mu));
           base = __shfl(base, lead, 64);
-          if (un)
-            fix_rec[base + __popcll(mu & ((1ULL << lane) - 1))] =
-                ((unsigned long long)(uint32_t)((b << kp.bucket_bits) | pl) << 32) | (unsigned long long)ci;
+          const int64_t at = (int64_t)base + __popcll(mu & ((1ULL << lane) - 1));
+          if (un && at < kp.fix_cap)
+            fix_rec[at] = ((unsigned long long)(uint32_t)((b << kp.bucket_bits) | pl) << 32) | (unsigned long long)ci;
         }
         if (sk[(l0 - 1) * S + pl] == kEmpty) return;
       }
@@ -2427,7 +2523,7 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
       unsigned base = 0;
       if (lane == 0) base = atomicAdd(sctl + 1, 64u);
       base = __shfl(base, 0, 64);
-      fix_rec[base + lane] = e;
+      if (base + lane < kp.fix_cap) fix_rec[base + lane] = e;
       const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
       wave_lds_fence();
       if (lane + 64 < qn) wq[lane] = rest;
@@ -2486,7 +2582,7 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
     unsigned base = 0;
     if (lane == 0) base = atomicAdd(sctl + 1, (unsigned)qn);
     base = __shfl(base, 0, 64);
-    if (lane < qn) fix_rec[base + lane] = wq[lane];
+    if (lane < qn && base + lane < kp.fix_cap) fix_rec[base + lane] = wq[lane];
   }
 }
 
@@ -2529,7 +2625,7 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
       unsigned base = 0;
       if (lane == 0) base = atomicAdd(sctl + 1, 64u);
       base = __shfl(base, 0, 64);
-      fix_rec[base + lane] = x;
+      if (base + lane < kp.fix_cap) fix_rec[base + lane] = x;
       const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
       wave_lds_fence();
       if (lane + 64 < qn) wq[lane] = rest;
@@ -2567,7 +2663,7 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
     unsigned base = 0;
     if (lane == 0) base = atomicAdd(sctl + 1, (unsigned)qn);
     base = __shfl(base, 0, 64);
-    if (lane < qn) fix_rec[base + lane] = wq[lane];
+    if (lane < qn && base + lane < kp.fix_cap) fix_rec[base + lane] = wq[lane];
   }
 }
 
@@ -2577,8 +2673,12 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
 __global__ void __launch_bounds__(kBlock) k_fix_filter(KP kp, const unsigned* __restrict__ unres_bits,
                                                        const unsigned* __restrict__ sctl,
                                                        unsigned long long* __restrict__ fix_rec,
-                                                       unsigned* __restrict__ fix_cnt) {
-  const int64_t total = sctl[1];
+                                                       unsigned* __restrict__ fix_cnt, unsigned* err) {
+  // a list longer than its region cannot happen (each list holds distinct
+  // rows); were it to, error bit 1 says so instead of reading past the region
+  const int64_t listed = sctl[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && listed > kp.fix_cap) atomicOr(err, 2u);
+  const int64_t total = listed < kp.fix_cap ? listed : kp.fix_cap;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t u = fix_rec[i] >> 32;
     if ((unres_bits[u >> 5] >> (u & 31)) & 1u) atomicAdd(fix_cnt + (u >> kp.bucket_bits), 1u);
@@ -2598,7 +2698,7 @@ __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __
                                                         const unsigned* __restrict__ fix_start,
                                                         unsigned* __restrict__ fix_cur,
                                                         RecKey<COMPACT>* __restrict__ keys, unsigned* __restrict__ rows) {
-  const int64_t total = sctl[1];
+  const int64_t total = (int64_t)sctl[1] < kp.fix_cap ? (int64_t)sctl[1] : kp.fix_cap;
   const uint64_t lmask = ((uint64_t)1 << kp.bucket_bits) - 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t e = fix_rec[i];
@@ -3267,7 +3367,7 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
                    const uint8_t* allowed, const void* value, const pdp_partition_accumulators& acc, char* ws,
                    const Ws& w) {
   const PairRecords rec = pair_records(ws, w);
-  unsigned long long* fix_rec = (unsigned long long*)(ws + w.keys1);  // level-1 blocks are dead
+  unsigned long long* fix_rec = (unsigned long long*)(ws + w.fix_rec);  // level-1 blocks are dead
   Marks m1{w.unres_bits ? (unsigned*)(ws + w.unres_bits) : nullptr,
            w.unres_list ? (unsigned*)(ws + w.unres_list) : nullptr, w.sctl ? (unsigned*)(ws + w.sctl) : nullptr,
            nullptr, p.band ? fix_rec : nullptr};
@@ -3282,7 +3382,7 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
                    int mark, const char* name) -> int {
     PDP_PROF_BEGIN("k_fix_filter", st);
     hipLaunchKernelGGL(k_fix_filter, dim3(grid_for(kp.n, 1024)), dim3(kBlock), 0, st, kp, (const unsigned*)bits,
-                       (const unsigned*)sctl, fix_rec, fix_cnt);
+                       (const unsigned*)sctl, fix_rec, fix_cnt, (unsigned*)(ws + w.err));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     int r = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts
@@ -3463,7 +3563,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   using K2 = L2Key<FMT>;
   constexpr bool ROWS1 = !kPackedL1<FMT>;
   unsigned* counts_tm = (unsigned*)(ws + w.counts_tm);
-  const bool u16 = p.sieve ? sieve_hist_u16(FMT, p.n_buckets, p.band != 0) : l1_hist_u16(FMT, p.n_buckets);
+  const bool u16 = p.hist_u16 != 0;
   unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
@@ -3472,10 +3572,15 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
   if constexpr (FMT != PDP_KEYS_WIDE) {
     if (p.sieve) {
-      const size_t lds1 = (sieve_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16) +
-                          (p.band ? (size_t)kBandLds : 0);
-      const void* l1 = p.band ? (u16 ? (const void*)k_sieve_l1<FMT, true, true> : (const void*)k_sieve_l1<FMT, false, true>)
-                              : (u16 ? (const void*)k_sieve_l1<FMT, true, false> : (const void*)k_sieve_l1<FMT, false, false>);
+      const int th = p.sieve_threads;
+      const size_t lds1 = (size_t)sieve_lds(FMT, th, p.n_buckets, u16, p.band != 0);
+      auto pick = [&](auto th_tag) -> const void* {
+        constexpr int TH = decltype(th_tag)::value;
+        return p.band ? (u16 ? (const void*)k_sieve_l1<FMT, true, true, TH> : (const void*)k_sieve_l1<FMT, false, true, TH>)
+                      : (u16 ? (const void*)k_sieve_l1<FMT, true, false, TH> : (const void*)k_sieve_l1<FMT, false, false, TH>);
+      };
+      const void* l1 = th == kSieveThreads2 ? pick(std::integral_constant<int, kSieveThreads2>{})
+                                            : pick(std::integral_constant<int, kL1Threads>{});
       PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
       unsigned long long* band = p.band ? (unsigned long long*)(ws + w.band) : nullptr;
       unsigned* band_cnt = p.band ? (unsigned*)(ws + w.band_cnt) : nullptr;
@@ -3483,7 +3588,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
                        (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err,
                        (void*)&band, (void*)&band_cnt};
       PDP_PROF_BEGIN("k_sieve_l1", st);
-      PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
+      PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(th), args1, lds1, st));
       PDP_PROF_END(st);
       PDP_HIP_CHECK(hipGetLastError());
     }
@@ -3710,6 +3815,7 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->key_format = p.key_format;
   info->sieve = p.sieve;
   info->band = p.band;
+  info->sieve_threads = p.sieve ? p.sieve_threads : 0;
   return PDP_OK;
 }
 
@@ -3740,6 +3846,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   if (pairs_mode(cfg)) return pairs_bound(cfg, privacy_id, partition_key, value, pk_allowed, ws, st);
   KP kp = make_kp(cfg, p);
   kp.keys_vec = ((((uintptr_t)privacy_id) | ((uintptr_t)partition_key)) & 15) == 0;
+  kp.fix_cap = (int64_t)w.fix_cap;
   unsigned* err = (unsigned*)(ws + w.err);
   PDP_HIP_CHECK(hipMemsetAsync(err, 0, 16, st));
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH) {

@@ -63,9 +63,52 @@ void profiler_end(hipStream_t stream) {
   g_open_start = nullptr;
 }
 
+namespace {
+// parallel.owner_of: the rank that owns a privacy-id identity
+__device__ __forceinline__ int owner_of(int64_t z, int world) {
+  z = (int64_t)((uint64_t)(z ^ (z >> 31)) * 0x9E3779B97F4A7C15ULL);
+  z ^= z >> 29;
+  int64_t r = z % world;
+  return (int)(r < 0 ? r + world : r);
+}
+
+// grid-stride, 16-byte loads where aligned; one atomic per wave with a mismatch
+__global__ void __launch_bounds__(kBlock) k_owner_mismatches(const int64_t* __restrict__ ids, int64_t n, int world,
+                                                             int rank, unsigned* out) {
+  unsigned bad = 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const bool vec = ((uintptr_t)ids & 15) == 0;
+  const int64_t n2 = vec ? n / 2 : 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n2; i += stride) {
+    const longlong2 v = reinterpret_cast<const longlong2*>(ids)[i];
+    bad += (owner_of(v.x, world) != rank) + (owner_of(v.y, world) != rank);
+  }
+  for (int64_t i = 2 * n2 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    bad += owner_of(ids[i], world) != rank;
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(out, bad);
+}
+}  // namespace
+
 }  // namespace pdp
 
 extern "C" {
+
+int pdp_owner_mismatches(const int64_t* ids, int64_t n, int32_t world, int32_t rank, uint32_t* mismatches,
+                         void* stream) {
+  if (mismatches == nullptr || n < 0 || (n > 0 && ids == nullptr) || world < 1 || rank < 0 || rank >= world)
+    return pdp::set_error(PDP_E_INVALID, "pdp_owner_mismatches: bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  PDP_HIP_CHECK(hipMemsetAsync(mismatches, 0, 4, st));
+  if (n == 0) return PDP_OK;
+  const int64_t want = (n + 2 * pdp::kBlock - 1) / (2 * pdp::kBlock);
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  hipLaunchKernelGGL(pdp::k_owner_mismatches, dim3(grid), dim3(pdp::kBlock), 0, st, ids, n, (int)world, (int)rank,
+                     mismatches);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
 
 int pdp_abi_version(void) { return PDP_ABI_VERSION; }
 

@@ -26,10 +26,13 @@ def partition_slices(n_partitions: int, world: int) -> Tuple[int, int]:
     return padded, padded // world
 
 
-def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None):
+def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None, narrow_ints: bool = True):
     """Sums the dense accumulators of all ranks and returns (this rank's
     slice of every accumulator, global index of the slice's first partition).
-    Accumulator tensors must have the padded length partition_slices(...)[0]."""
+    Accumulator tensors must have the padded length partition_slices(...)[0].
+    narrow_ints: int64 fields (counts, privacy-id counts, int sums) travel as
+    int32 when the global maximum proves no sum can overflow (exact either
+    way; half the bytes of those fields over xGMI)."""
     import torch
     import torch.distributed as dist
     world, rank = world_info(group)
@@ -53,12 +56,25 @@ def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None):
             by_dtype.setdefault(t.dtype, []).append(name)
     for dtype, names in by_dtype.items():
         stacked = torch.stack([acc[n].reshape(world, slice_len) for n in names], dim=1).contiguous()
+        wire = stacked
+        if dtype == torch.int64 and narrow_ints:
+            # counts and privacy-id counts travel as int32 when no sum over
+            # ranks can reach 2^31: every rank's entries lie in [0, m] with m
+            # the global maximum (one all-reduce of 8 bytes), so every sum of
+            # `world` of them is <= world * m (sums of fp accumulators stay fp64)
+            lo_hi = torch.stack([(-stacked).max(), stacked.max()]) if stacked.numel() else \
+                torch.zeros(2, dtype=torch.int64, device=stacked.device)
+            lo_hi = lo_hi.to(_coll_device(group))
+            dist.all_reduce(lo_hi, op=dist.ReduceOp.MAX, group=group)
+            if int(lo_hi[0]) <= 0 and world * int(lo_hi[1]) < 2 ** 31:
+                wire = stacked.to(torch.int32)
         if backend == "nccl":
-            part = torch.empty((len(names), slice_len), dtype=dtype, device=stacked.device)
-            dist.reduce_scatter_tensor(part.view(-1), stacked.view(-1), op=dist.ReduceOp.SUM, group=group)
+            part = torch.empty((len(names), slice_len), dtype=wire.dtype, device=stacked.device)
+            dist.reduce_scatter_tensor(part.view(-1), wire.view(-1), op=dist.ReduceOp.SUM, group=group)
         else:  # gloo (CPU tests): all-reduce then keep the owned chunk
-            dist.all_reduce(stacked, op=dist.ReduceOp.SUM, group=group)
-            part = stacked[rank].clone()
+            dist.all_reduce(wire, op=dist.ReduceOp.SUM, group=group)
+            part = wire[rank].clone()
+        part = part.to(dtype)
         for i, n in enumerate(names):
             out[n] = part[i]
     return out, rank * slice_len
@@ -69,12 +85,10 @@ def shard_by_privacy_id(privacy_ids, world: int, rank: int):
     for callers that shard their own input before building a ColumnTable."""
     import numpy as np
     pid = np.asarray(privacy_ids)
-    if pid.dtype.kind in "iu":
-        h = (pid.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(32)
-        return (h % np.uint64(world)) == np.uint64(rank)
-    import hashlib
-    return np.fromiter((int(hashlib.blake2b(repr(p).encode(), digest_size=8).hexdigest(), 16) % world == rank
-                        for p in pid), dtype=bool, count=len(pid))
+    if pid.dtype.kind not in "iu":  # other keys: their identities (key_identities), as the library hashes them
+        pid = key_identities(pid)
+    # owner_of: data sharded by this helper passes the "verify" fast path
+    return owner_of_np(pid, world) == rank
 
 
 def _coll_device(group=None):
@@ -380,14 +394,68 @@ def key_identities(keys) -> "np.ndarray":
     return hash_array(arr, categorize=False).view(np.int64)
 
 
-def _owner(ident, world: int):
+def owner_of(ident, world: int):
     """Rank that owns an identity: a SplitMix64-style mix mod world (so that
-    structured ids, e.g. multiples of the world size, still spread)."""
+    structured ids, e.g. multiples of the world size, still spread); the
+    kernel twin is pdp_owner_mismatches (pipelinedp_amd.h)."""
     import torch
     z = ident.to(torch.int64)
     z = (z ^ (z >> 31)) * -7046029254386353131  # 0x9E3779B97F4A7C15 as int64
     z = z ^ (z >> 29)
     return torch.remainder(z, world)
+
+
+_owner = owner_of
+
+
+def owner_of_np(ident, world: int):
+    """NumPy twin of owner_of (int64 wrap-around, arithmetic shifts)."""
+    import numpy as np
+    z = np.asarray(ident).astype(np.int64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> 31)) * np.int64(-7046029254386353131)
+    z = z ^ (z >> 29)
+    return np.mod(z, world)
+
+
+def ids_hash_owned(ident, world: int, rank: int) -> bool:
+    """True when every identity in `ident` (int64 tensor) has owner_of == rank:
+    one pass of pdp_owner_mismatches on a GPU tensor, torch ops on a CPU one."""
+    import torch
+    if ident.numel() == 0:
+        return True
+    if ident.is_cuda:
+        import ctypes
+        from pipelinedp_amd import _native as N
+        ids = ident.to(torch.int64).contiguous()
+        out = torch.empty(1, dtype=torch.int32, device=ids.device)
+        st = torch.cuda.current_stream(ids.device).cuda_stream
+        N.check(N.lib().pdp_owner_mismatches(ctypes.c_void_p(ids.data_ptr()), ids.numel(), world, rank,
+                                             ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(st)),
+                "pdp_owner_mismatches")
+        return int(out.item()) == 0
+    return bool((owner_of(ident, world) == rank).all())
+
+
+def verify_privacy_id_sharding(ident, group=None) -> str:
+    """ColumnarBackend privacy_id_sharding="verify": raises ValueError when a
+    privacy id (int64 identity; rows or distinct keys) is on more than one
+    rank.  Fast path: every rank holds only ids it owns (owner_of, one pass
+    over the ids and one all-reduce of a flag) -- then no id can be on two
+    ranks; otherwise the distinct ids are exchanged
+    (check_privacy_ids_disjoint).  Returns "single", "owned" or "exchanged"."""
+    import torch
+    import torch.distributed as dist
+    world, rank = world_info(group)
+    if world == 1:
+        return "single"
+    ok = ids_hash_owned(ident, world, rank)
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=_coll_device(group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag.item()):
+        return "owned"
+    check_privacy_ids_disjoint(torch.unique(ident), group)
+    return "exchanged"
 
 
 def _exchange(parts_by_dest, counts, group):

@@ -275,3 +275,29 @@ def test_dataset_histograms_arguments(lib):
     assert rc == -4 and b"63 bits" in lib.pdp_last_error()
     rc = lib.pdp_dataset_histograms(None, None, None, N.VALUE_F64, 10, 100, 10, ctypes.byref(fake), None, 0, None)
     assert rc == -1 and b"workspace" in lib.pdp_last_error()
+
+
+def test_debug_corrupt_flag_needs_test_hooks(lib, monkeypatch):
+    """PDP_DEBUG_CORRUPT_RECORDS (it overwrites level-2 records on purpose)
+    is rejected unless PIPELINEDP_AMD_TEST_HOOKS=1."""
+    nbytes = ctypes.c_uint64(0)
+    cfg = _cfg(flags=N.ACC_NSUM | N.DEBUG_CORRUPT_RECORDS)
+    monkeypatch.delenv("PIPELINEDP_AMD_TEST_HOOKS", raising=False)
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)) == -1
+    assert b"test hook" in lib.pdp_last_error()
+    monkeypatch.setenv("PIPELINEDP_AMD_TEST_HOOKS", "1")
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)) == 0
+
+
+def test_sieve_threads_plan(lib):
+    """sieve_threads: 0 (auto) and 1024 resolve to 1,024-thread level-1
+    workgroups, 512 to two per CU when their LDS fits; other values fail."""
+    info = N.BoundPlanInfo()
+    c3 = dict(n_rows=1_000_000_000, n_privacy_ids=10_000_000, n_partitions=1_000_000, l0=2, linf=1)
+    for want, got in ((0, 1024), (1024, 1024), (512, 512)):
+        assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve_threads=want)), ctypes.byref(info)) == 0
+        assert info.sieve > 0 and info.sieve_threads == got
+    assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=-1)), ctypes.byref(info)) == 0
+    assert info.sieve_threads == 0
+    nbytes = ctypes.c_uint64(0)
+    assert lib.pdp_bound_workspace_bytes(ctypes.byref(_cfg(**c3, sieve_threads=256)), ctypes.byref(nbytes)) == -1

@@ -41,7 +41,7 @@ def _spec(case):
 
 
 def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format=0, row_offset=0, band=0,
-         workspace=None):
+         workspace=None, threads=0):
     import torch
     from pipelinedp_amd import executor as X
     tv = None if val is None else torch.as_tensor(val).to(device)
@@ -49,7 +49,7 @@ def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format
     acc = X.bound_and_reduce(torch.as_tensor(pid).to(device), torch.as_tensor(pk).to(device), tv,
                              n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, allowed=ta,
                              key_format=key_format, sieve=sieve, row_offset=row_offset, sieve_band=band,
-                             workspace=workspace)
+                             workspace=workspace, sieve_threads=threads)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
@@ -77,8 +77,11 @@ def test_sieve_matches_oracle_at_every_threshold(device, case):
         assert plan.sieve == sieve, (sieve, plan.sieve)
         assert plan.band == (min(2 * sieve, 32768) if sieve < 32768 else 0)
         for band in (0, -1):  # the side band (ids with < l0 pairs below 2t: the rescan), and without it
-            got = _run(device, pid, pk, val, U, P, spec, seed, sieve, band=band)
-            _compare(got, want, scale)
+            # both level-1 workgroup shapes (512 threads, 16 flush slots per
+            # tile; 1,024 threads, 8 slots)
+            for threads in (512, 1024):
+                got = _run(device, pid, pk, val, U, P, spec, seed, sieve, band=band, threads=threads)
+                _compare(got, want, scale)
     off = _run(device, pid, pk, val, U, P, spec, seed, -1)
     assert X.bound_plan(n, U, P, spec, sieve=-1).sieve == 0
     _compare(off, want, scale)
@@ -176,8 +179,35 @@ def test_band_with_ids_short_of_pairs(device):
     assert st["unresolved2_ids"] > 10_000 and st["fixup2_rows"] >= st["unresolved2_ids"], st
 
 
+@pytest.mark.parametrize("threads", [512, 1024])
+def test_sieve_every_row_a_candidate(device, threads):
+    """Tiles whose every row is a candidate (each row's pair hash below t =
+    1/2): the stage flushes at every chance, so a tile fills all of its
+    flush slots (16 for 512 threads, 8 for 1,024); equal to the oracle."""
+    from pipelinedp_amd import executor as X
+    spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    U, P = 300_000, 4096  # > 64 buckets: two partition levels, the sieve's precondition
+    seed = 8080
+    rng = np.random.default_rng(12)
+    cu = rng.integers(0, U, 400_000)
+    ck = rng.integers(0, P, 400_000)
+    low = O.pair_hash(seed, cu, ck) < np.uint32(1 << 31)
+    cu, ck = cu[low], ck[low]
+    idx = rng.integers(0, len(cu), 3 * 65536 + 999)
+    pid, pk = cu[idx], ck[idx]
+    n = len(pid)
+    val = rng.random(n) * 10.0
+    plan = X.bound_plan(n, U, P, spec, sieve=32768, sieve_threads=threads)
+    assert plan.sieve == 32768 and plan.sieve_threads == threads
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    ws = X.BoundWorkspace()
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 32768, workspace=ws, threads=threads), want, scale)
+    assert ws.stats()["rows_partitioned"] == n
+
+
 @pytest.mark.parametrize("sieve", [-1, 4096])
-def test_malformed_records_are_flagged_not_read(device, sieve):
+def test_malformed_records_are_flagged_not_read(device, sieve, monkeypatch):
     """PDP_DEBUG_CORRUPT_RECORDS overwrites bucket 0's level-2 records with
     the all-ones partition (>= P) and bucket 1's with an out-of-range row: the
     bucket kernel sets the error word (bound_and_reduce raises) instead of
@@ -191,6 +221,10 @@ def test_malformed_records_are_flagged_not_read(device, sieve):
                           max_value=base.max_value, middle=base.middle)
     U, P, n = 200_000, 3001, 1_000_000
     pid, pk, val = _gen(1, n, U, P, spec.value_kind)
+    monkeypatch.delenv("PIPELINEDP_AMD_TEST_HOOKS", raising=False)
+    with pytest.raises(RuntimeError, match="test hook"):  # rejected outside test mode
+        _run(device, pid, pk, val, U, P, spec, 5, sieve)
+    monkeypatch.setenv("PIPELINEDP_AMD_TEST_HOOKS", "1")
     with pytest.raises(ValueError, match="outside the dense key range"):
         _run(device, pid, pk, val, U, P, spec, 5, sieve)
     torch.cuda.synchronize()  # the device is still healthy

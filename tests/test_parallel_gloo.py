@@ -85,6 +85,21 @@ def test_partition_slices_and_validation():
     assert parallel.exchange_accumulators(acc) == (acc, 0)  # not initialised: one rank
 
 
+def test_owner_of_numpy_matches_torch():
+    """shard_by_privacy_id (NumPy) and the library's owner_of (torch; the
+    kernel pdp_owner_mismatches) agree, negative and large ids included, so
+    data sharded by the helper passes the "verify" fast path."""
+    import torch
+    rng = np.random.default_rng(9)
+    ids = np.concatenate([rng.integers(-2**63, 2**63 - 1, 5000, dtype=np.int64), np.arange(-50, 50),
+                          np.array([2**63 - 1, -2**63], dtype=np.int64)])
+    for world in (2, 3, 8):
+        np.testing.assert_array_equal(parallel.owner_of_np(ids, world),
+                                      parallel.owner_of(torch.as_tensor(ids), world).numpy())
+        m = parallel.shard_by_privacy_id(ids, world, 1)
+        np.testing.assert_array_equal(m, parallel.owner_of_np(ids, world) == 1)
+
+
 def test_shard_by_privacy_id_partitions_rows():
     pid = np.arange(10_000)
     masks = [parallel.shard_by_privacy_id(pid, 4, r) for r in range(4)]
@@ -114,6 +129,16 @@ def _dict_worker(rank, port, results):
         seeds = parallel.broadcast_seeds((rank + 1, rank + 2, rank + 3))
         assert seeds == (1, 2, 3)
         assert parallel.all_ranks_any(rank == 1) is True
+        # int64 accumulators narrowed to int32 on the wire only when no sum
+        # over ranks can reach 2^31: 2^30 on both ranks stays int64 (exact)
+        import torch
+        big = {"count": torch.full((4,), 2 ** 30, dtype=torch.int64),
+               "privacy_id_count": torch.arange(4, dtype=torch.int64),
+               "sum": torch.full((4,), -5, dtype=torch.int64), "normalized_sum": None}
+        got, first = parallel.exchange_accumulators(big)
+        assert got["count"].dtype == torch.int64 and got["count"].tolist() == [2 ** 31] * 2
+        assert got["privacy_id_count"].tolist() == [2 * (first + i) for i in range(2)]
+        assert got["sum"].tolist() == [-10, -10] and got["normalized_sum"] is None
         results[rank] = "ok"
     except Exception as e:
         results[rank] = repr(e)
@@ -176,6 +201,22 @@ def _pid_worker(rank, port, results):
         try:
             shard_rows_by_privacy_id("verify", pid, pk, val, enc)
             results[rank] = "row-sharded ids not detected"
+            return
+        except ValueError as e:
+            assert "more than one rank" in str(e)
+        # the verify fast path: hash-owned ids pass with one flag all-reduce,
+        # disjoint ids that are not hash-owned go through the id exchange
+        assert parallel.verify_privacy_id_sharding(got_pid) == "owned"
+        assert shard_rows_by_privacy_id("verify", got_pid, got_pk, got_val, enc)[0] is got_pid
+        assert parallel.verify_privacy_id_sharding(torch.arange(rank * 700, rank * 700 + 700)) == "exchanged"
+        try:  # one rank hash-owned, the other holding an id of rank 0's: still caught
+            mine_ids = got_pid if rank == 0 else torch.cat([got_pid, got_pid.new_tensor([0, 1, 2, 3, 4, 5])])
+            allin0 = [None] * WORLD
+            dist.all_gather_object(allin0, sorted(set(got_pid.tolist())))
+            if rank == 1:
+                mine_ids = torch.cat([got_pid, torch.as_tensor(allin0[0][:3])])
+            parallel.verify_privacy_id_sharding(mine_ids)
+            results[rank] = "overlap behind the fast path not detected"
             return
         except ValueError as e:
             assert "more than one rank" in str(e)

@@ -114,6 +114,75 @@ __global__ void __launch_bounds__(256) k_grid2(const longlong2* __restrict__ a, 
   if (acc == 0x1234567) out[0] = 1;
 }
 
+
+// F: the level-1 skeleton -- 1,024 threads per 65,536-row tile, two int64
+// columns, Q = 4 rows per thread per chunk in a ring of B register buffers
+// (the next loads issued right after a chunk is consumed), dynamic LDS to
+// pin one workgroup per CU, optionally a barrier per chunk (BAR) and the
+// pair hash + a wave-compacted LDS append of ~15 % of rows (WORK)
+template <int B, bool BAR, bool WORK>
+__global__ void __launch_bounds__(1024) k_l1sim(const long long* __restrict__ a, const long long* __restrict__ b,
+                                                size_t n, unsigned* out) {
+  extern __shared__ unsigned long long stage[];
+  __shared__ unsigned fill;
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  const size_t t0 = (size_t)blockIdx.x * 65536, t1 = t0 + 65536 < n ? t0 + 65536 : n;
+  if (t1 - t0 < 65536) return;
+  constexpr int Q = 4, CH = 1024 * Q, NCH = 65536 / CH;
+  long long u[B][Q], k[B][Q];
+  auto load = [&](int c, long long (&uu)[Q], long long (&kk)[Q]) {
+    const size_t c0 = t0 + (size_t)(c < NCH ? c : NCH - 1) * CH;
+#pragma unroll
+    for (int q = 0; q < Q; q += 2) {
+      const size_t i = c0 + 2 * (threadIdx.x + (size_t)(q / 2) * 1024);
+      const longlong2 x = *reinterpret_cast<const longlong2*>(a + i);
+      const longlong2 y = *reinterpret_cast<const longlong2*>(b + i);
+      uu[q] = x.x; uu[q + 1] = x.y; kk[q] = y.x; kk[q + 1] = y.y;
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < B; ++j) load(j, u[j], k[j]);
+  unsigned acc = 0;
+  const int lane = threadIdx.x & 63;
+  for (int c = 0; c < NCH; c += B) {
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      unsigned ul[Q], kl[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) { ul[q] = (unsigned)u[j][q] ^ (unsigned)(u[j][q] >> 32); kl[q] = (unsigned)k[j][q]; }
+      load(c + j + B, u[j], k[j]);
+      if (WORK) {
+        bool cand[Q];
+        unsigned long long m[Q];
+        unsigned nw = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          unsigned h = (ul[q] ^ 0x1234567u) * 0x9E3779B1u;
+          h = h ^ (kl[q] * 0xC2B2AE3Du + 77u);
+          h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+          cand[q] = h < 0x26000000u;
+          m[q] = __ballot(cand[q]);
+          nw += (unsigned)__popcll(m[q]);
+        }
+        unsigned base = 0;
+        if (lane == 0 && nw) base = atomicAdd(&fill, nw);
+        base = __shfl(base, 0, 64) & 8191u;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          if (cand[q]) stage[(base + (unsigned)__popcll(m[q] & ((1ULL << lane) - 1))) & 8191u] = ((unsigned long long)ul[q] << 32) | kl[q];
+          base += (unsigned)__popcll(m[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) acc ^= ul[q] ^ kl[q];
+      }
+      if (BAR) __syncthreads();
+    }
+  }
+  if (acc == 0x1234567 || fill == 0x7654321) out[0] = 1;
+}
+
 template <typename F>
 double time_it(F&& launch) {
   hipEvent_t a, b;
@@ -171,6 +240,17 @@ int main() {
     auto rep2 = [&](const char* name, double ms) { printf("%-28s %8.3f ms %8.1f GB/s\n", name, ms, gb / (ms * 1e-3)); };
     rep2("tiles2 Q=4 (level-1 shape)", time_it([&] { hipLaunchKernelGGL((k_tiles2<4>), dim3(tiles), dim3(1024), 0, 0, a, b, n, out); }));
     rep2("tiles2 Q=8", time_it([&] { hipLaunchKernelGGL((k_tiles2<8>), dim3(tiles), dim3(1024), 0, 0, a, b, n, out); }));
+    const size_t lds = 150 * 1024;
+#define SIM(NAME, ...)                                                                                   \
+    CHECK(hipFuncSetAttribute((const void*)(__VA_ARGS__), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    rep2(NAME, time_it([&] { hipLaunchKernelGGL((__VA_ARGS__), dim3(tiles), dim3(1024), lds, 0, a, b, n, out); }))
+    SIM("l1sim B2", k_l1sim<2, false, false>);
+    SIM("l1sim B3", k_l1sim<3, false, false>);
+    SIM("l1sim B2 bar", k_l1sim<2, true, false>);
+    SIM("l1sim B2 bar work", k_l1sim<2, true, true>);
+    SIM("l1sim B3 bar work", k_l1sim<3, true, true>);
+    SIM("l1sim B2 work", k_l1sim<2, false, true>);
+    SIM("l1sim B4", k_l1sim<4, false, false>);
     rep2("grid2 U=4 g=2048", time_it([&] { hipLaunchKernelGGL(k_grid2, dim3(2048), dim3(256), 0, 0, (const longlong2*)a,
                                                                (const longlong2*)b, n / 2, out); }));
   }
