@@ -426,6 +426,7 @@ struct Ws {
   // two-level merge: fine-range totals / starts (+ scan scratch), write cursors,
   // the records re-sorted by fine range, fine work items and their count
   uint64_t fine_total, fine_chunks, fine_cur, stg_key, stg_f0, stg_f1, stg_f2, fine_items, fine_count;
+  uint64_t item_hist;  // two-level: per coarse work item, its records per fine range (k_split_count)
   uint64_t total;
 };
 
@@ -522,6 +523,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
         if (w.rec_f2) { w.stg_f2 = off; off = align256(off + recs * 8); }
         w.fine_items = off; off = align256(off + (uint64_t)p.fine_items * 16);
         w.fine_count = off; off = align256(off + 16);
+        const uint64_t F = (uint64_t)1 << (p.range_bits - kRangeBits);
+        w.item_hist = off; off = align256(off + (uint64_t)p.n_groups * F * 4);
       }
     }
   }
@@ -1531,21 +1534,34 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       }
     }
   };
-  const int64_t t = blockIdx.x;
+  // persistent: workgroup g takes tiles g, g + G, ... (G = gridDim.x, about
+  // one per CU), so a tile's last chunks prefetch the next tile's first ones
+  // and no tile starts with its loads' latency exposed
   const int nd = (int)kp.n_supers;
-  const int64_t t0 = t * kTileRows;
-  const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+  int64_t t = 0, t0 = 0, t1 = 0, next_t0 = -1;  // the tile; the next one's first row (-1: none)
   const int mid_bits = kp.bucket_bits + kp.super_bits;
   const uint32_t t32 = kp.sieve_t32;
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ULL << lane) - 1;
-  K* const blk = keys1 + t * kSieveTileStride;
-  unsigned* const rblk = ROWS ? rows1 + t * kSieveTileStride : nullptr;
-  unsigned long long* const band_tile = BAND ? band + t * kTileRows : nullptr;
+  K* blk = nullptr;
+  unsigned* rblk = nullptr;
+  unsigned long long* band_tile = nullptr;
   unsigned long long* const wq = bq + (threadIdx.x >> 6) * kBandQueue;
   int qn = 0;            // wave-uniform: entries waiting in this wave's band queue
   unsigned written = 0;  // block-uniform: this tile's records already written
   int slot = 0;
+  bool split = false;    // U16: the tile's counts in two halves (counts_tm, counts_tm2)
+  auto begin_tile = [&](int64_t tt) {
+    t = tt;
+    t0 = tt * kTileRows;
+    t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
+    blk = keys1 + tt * kSieveTileStride;
+    rblk = ROWS ? rows1 + tt * kSieveTileStride : nullptr;
+    band_tile = BAND ? band + tt * kTileRows : nullptr;
+    written = 0;
+    slot = 0;
+    split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
+  };
   // the stage's `total` records -> counting sort by super-bucket -> block
 #ifdef PDP_PHASE_CLOCK
   unsigned long long fl_ticks = 0, t_start = wall_clock64();
@@ -1597,9 +1613,47 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     fl_ticks += wall_clock64() - f0;
 #endif
   };
-  // U16: the tile's counts in two halves (counts_tm, counts_tm2)
-  const bool split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
   bool bad = false;  // a key outside [0, U) x [0, P): flagged once per thread at the end
+  // end of a tile: the band queues' rest and the list length, the unused
+  // flush slots, the bucket counts; leaves the LDS state zeroed for the next
+  auto end_tile = [&]() {
+    if constexpr (BAND) {
+      wave_lds_fence();
+      if (qn > 0) {
+        unsigned bb = 0;
+        if (lane == 0) bb = atomicAdd(&bfill, (unsigned)qn);
+        bb = __shfl(bb, 0, 64);
+        if (lane < qn) band_tile[bb + lane] = wq[lane];
+        qn = 0;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        band_cnt[t] = bfill;
+        bfill = 0;
+      }
+    }
+#ifdef PDP_PHASE_CLOCK
+    if (threadIdx.x == 0 && blockIdx.x % 97 == 5 && atomicAdd(&g_phase_l1, 1u) < 40u)
+      printf("l1 tile %d slots %d records %u total %llu flush %llu (10 ns)\n", (int)t, slot, written,
+             wall_clock64() - t_start, fl_ticks);
+    t_start = wall_clock64();
+    fl_ticks = 0;
+#endif
+    for (int j = slot; j < SS::kSlots; ++j) {
+      const int64_t sl = t * SS::kSlots + j;
+      for (int B = threadIdx.x; B <= nd; B += TH) soff[sl * (nd + 1) + B] = 0;
+      if (threadIdx.x == 0) sbase[sl] = written;
+    }
+    __syncthreads();
+    if (split) {
+      flush_counts(counts_tm2 + t * kp.n_buckets);
+    } else {
+      flush_counts(counts_tm + t * kp.n_buckets);
+      if constexpr (U16)
+        for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.n_buckets + b] = 0;
+    }
+    __syncthreads();
+  };
   // FULL (a whole tile of 16-byte aligned columns): every load is an
   // unconditional 16-byte load and the prefetch address is clamped into the
   // tile, so no branch surrounds a load and the compiler keeps two chunks of
@@ -1656,8 +1710,9 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       // loads in flight and this one's registers free (the register peak)
       constexpr bool kEarly = !FULL || kSieveBufs < 3 || PDP_SIEVE_EARLY;
       auto prefetch = [&]() {
-        if constexpr (FULL) {
-          const int64_t cp = c0 + kSieveBufs * kSieveChunk < t1 ? c0 + kSieveBufs * kSieveChunk : t1 - kSieveChunk;
+        if constexpr (FULL) {  // past the tile: the next tile's chunk, else clamped (no branch)
+          const int64_t ahead = c0 + kSieveBufs * kSieveChunk;
+          const int64_t cp = ahead < t1 ? ahead : (next_t0 >= 0 ? next_t0 + (ahead - t1) : t1 - kSieveChunk);
           load(cp, u, k);
         } else {
           if (c0 + 2 * kSieveChunk < t1) load(c0 + 2 * kSieveChunk, u, k);
@@ -1749,14 +1804,22 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       constexpr int kChunks = (int)(kTileRows / kSieveChunk);
       constexpr int kRest = kChunks % kSieveBufs;  // chunks after the last whole ring turn
       int64_t ub[kSieveBufs][Q], kb[kSieveBufs][Q];
+      const int64_t n_full = kp.n / kTileRows;  // tiles of kTileRows rows (16-byte aligned columns)
+      if ((int64_t)blockIdx.x >= n_full) return;  // block-uniform
 #pragma unroll
-      for (int b = 0; b < kSieveBufs; ++b) load(t0 + (int64_t)b * kSieveChunk, ub[b], kb[b]);
-      for (int j = 0; j < kChunks - kRest; j += kSieveBufs) {
+      for (int b = 0; b < kSieveBufs; ++b)
+        load((int64_t)blockIdx.x * kTileRows + (int64_t)b * kSieveChunk, ub[b], kb[b]);
+      for (int64_t tt = blockIdx.x; tt < n_full; tt += gridDim.x) {
+        begin_tile(tt);
+        next_t0 = tt + gridDim.x < n_full ? (tt + gridDim.x) * kTileRows : -1;
+        for (int j = 0; j < kChunks - kRest; j += kSieveBufs) {
 #pragma unroll
-        for (int b = 0; b < kSieveBufs; ++b) body(t0 + (int64_t)(j + b) * kSieveChunk, ub[b], kb[b]);
+          for (int b = 0; b < kSieveBufs; ++b) body(t0 + (int64_t)(j + b) * kSieveChunk, ub[b], kb[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < kRest; ++b) body(t0 + (int64_t)(kChunks - kRest + b) * kSieveChunk, ub[b], kb[b]);
+        end_tile();
       }
-#pragma unroll
-      for (int b = 0; b < kRest; ++b) body(t0 + (int64_t)(kChunks - kRest + b) * kSieveChunk, ub[b], kb[b]);
     } else {  // the last tile, unaligned columns: two chunks in flight
       int64_t ua[Q], ka[Q], ub[Q], kb[Q];
       if (t0 < t1) load(t0, ua, ka);
@@ -1767,39 +1830,15 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       }
     }
   };
-  if (kp.keys_vec && t1 - t0 == kTileRows) run(std::true_type{});
-  else run(std::false_type{});
+  if (kp.keys_vec) run(std::true_type{});
+  // the rest: a partial last tile, or every tile when the columns are unaligned
+  for (int64_t tt = (kp.keys_vec ? kp.n / kTileRows : 0) + blockIdx.x; tt < kp.n_tiles; tt += gridDim.x) {
+    begin_tile(tt);
+    next_t0 = -1;
+    run(std::false_type{});
+    end_tile();
+  }
   if (bad) atomicOr(err, 1u);
-  if constexpr (BAND) {  // the queues' rest; the tile's list length
-    wave_lds_fence();
-    if (qn > 0) {
-      unsigned bb = 0;
-      if (lane == 0) bb = atomicAdd(&bfill, (unsigned)qn);
-      bb = __shfl(bb, 0, 64);
-      if (lane < qn) band_tile[bb + lane] = wq[lane];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) band_cnt[t] = bfill;
-  }
-#ifdef PDP_PHASE_CLOCK
-  if (threadIdx.x == 0 && blockIdx.x % 1999 == 5 && atomicAdd(&g_phase_l1, 1u) < 40u)
-    printf("l1 tile %d slots %d records %u total %llu flush %llu (10 ns)\n", (int)t, slot, written,
-           wall_clock64() - t_start, fl_ticks);
-#endif
-  // the tile's unused slots: empty runs
-  for (int j = slot; j < SS::kSlots; ++j) {
-    const int64_t sl = t * SS::kSlots + j;
-    for (int B = threadIdx.x; B <= nd; B += TH) soff[sl * (nd + 1) + B] = 0;
-    if (threadIdx.x == 0) sbase[sl] = written;
-  }
-  __syncthreads();
-  if (split) {
-    flush_counts(counts_tm2 + t * kp.n_buckets);
-  } else {
-    flush_counts(counts_tm + t * kp.n_buckets);
-    if constexpr (U16)
-      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.n_buckets + b] = 0;
-  }
 }
 
 // Level 2 over tile-local level-1 blocks: workgroup (group g of kL2GroupTiles
@@ -2962,7 +3001,8 @@ constexpr int kFinePerCoarseMax = 1 << 13;  // 2^(range_bits - kRangeBits) <= 2^
 // added to fine_total with one atomic per touched fine range
 __global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecords rec, const uint4* __restrict__ items,
                                                               const unsigned* __restrict__ n_items,
-                                                              unsigned* __restrict__ fine_total) {
+                                                              unsigned* __restrict__ fine_total,
+                                                              unsigned* __restrict__ item_hist) {
   __shared__ unsigned long long start[kRangeThreads];
   __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
   __shared__ unsigned lh[kFinePerCoarseMax];
@@ -2987,20 +3027,28 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecord
               },
               [] {});
   __syncthreads();
-  for (int t = threadIdx.x; t < F; t += blockDim.x)
-    if (lh[t] && f0 + t < kp.n_fine_ranges) atomicAdd(fine_total + f0 + t, lh[t]);
+  // the item's histogram for k_split_scatter, which then reserves its slots
+  // once per fine range instead of once per round
+  for (int t = threadIdx.x; t < F; t += blockDim.x) {
+    const bool in = f0 + t < kp.n_fine_ranges;
+    item_hist[(int64_t)blockIdx.x * F + t] = in ? lh[t] : 0u;
+    if (lh[t] && in) atomicAdd(fine_total + f0 + t, lh[t]);
+  }
 }
 
-// records of an item -> the fine-range-sorted arrays: per round an LDS rank
-// per fine range, one atomic per touched fine range reserves its slots at
-// fine_cur (initialised to the fine-range starts), then the records move
+// records of an item -> the fine-range-sorted arrays: the item reserves its
+// slots of every fine range once (its histogram from k_split_count, one
+// device atomic per touched fine range), then each record takes the next slot
+// of its fine range from an LDS cursor (a returning LDS atomic) -- no
+// barriers between the batches, so their loads overlap
 __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairRecords rec, PairRecords stg,
                                                                 const uint4* __restrict__ items,
                                                                 const unsigned* __restrict__ n_items,
-                                                                unsigned* __restrict__ fine_cur) {
+                                                                unsigned* __restrict__ fine_cur,
+                                                                const unsigned* __restrict__ item_hist) {
   __shared__ unsigned long long start[kRangeThreads];
   __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
-  __shared__ unsigned lh[kFinePerCoarseMax];
+  __shared__ unsigned lcur[kFinePerCoarseMax];
   if (blockIdx.x >= *n_items) return;
   const uint4 it = items[blockIdx.x];
   if (it.x >> 31) return;
@@ -3009,42 +3057,34 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairReco
   const int r = (int)it.x;
   const int F = 1 << (kp.range_bits - kRangeBits);
   const int64_t f0 = (int64_t)r << (kp.range_bits - kRangeBits);
-  for (int t = threadIdx.x; t < F; t += blockDim.x) lh[t] = 0;
+  for (int t = threadIdx.x; t < F; t += blockDim.x) {
+    const unsigned c = item_hist[(int64_t)blockIdx.x * F + t];
+    lcur[t] = c ? atomicAdd(fine_cur + f0 + t, c) : 0u;
+  }
   __syncthreads();
   item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
               [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
                 unsigned long long key[4];
-                int f[4];
-                unsigned rank[4];
-                bool live[4];
+                double v0[4], v1[4], v2[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                   key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
-                  const uint64_t fu = (key[u] >> (32 + kRangeBits)) - (uint64_t)f0;
-                  live[u] = ok[u] && fu < (uint64_t)F;  // a malformed record is skipped (k_split_count too)
-                  f[u] = live[u] ? (int)fu : 0;
-                  rank[u] = live[u] ? atomicAdd(lh + f[u], 1u) : 0u;
+                  v0[u] = (ok[u] && stg.f0) ? rec.f0[idx[u]] : 0.0;
+                  v1[u] = (ok[u] && stg.f1) ? rec.f1[idx[u]] : 0.0;
+                  v2[u] = (ok[u] && stg.f2) ? rec.f2[idx[u]] : 0.0;
                 }
-                __syncthreads();
-                // reserve: lh[t] -> this round's base of fine range t (then 0)
-                for (int t = threadIdx.x; t < F; t += blockDim.x) {
-                  const unsigned c = lh[t];
-                  lh[t] = c ? atomicAdd(fine_cur + f0 + t, c) : 0u;
-                }
-                __syncthreads();
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                  if (!live[u]) continue;
-                  const uint64_t o = (uint64_t)lh[f[u]] + rank[u];
+                  const uint64_t fu = (key[u] >> (32 + kRangeBits)) - (uint64_t)f0;
+                  if (!ok[u] || fu >= (uint64_t)F) continue;  // a malformed record is skipped (k_split_count too)
+                  const uint64_t o = atomicAdd(lcur + (int)fu, 1u);
                   stg.key[o] = key[u];
-                  if (stg.f0) stg.f0[o] = rec.f0[idx[u]];
-                  if (stg.f1) stg.f1[o] = rec.f1[idx[u]];
-                  if (stg.f2) stg.f2[o] = rec.f2[idx[u]];
+                  if (stg.f0) stg.f0[o] = v0[u];
+                  if (stg.f1) stg.f1[o] = v1[u];
+                  if (stg.f2) stg.f2[o] = v2[u];
                 }
-                __syncthreads();
-                for (int t = threadIdx.x; t < F; t += blockDim.x) lh[t] = 0;
               },
-              [] { __syncthreads(); });
+              [] {});
 }
 
 // fine work items: fine range f's records [start_f, start_f+1) in chunks of
@@ -3094,35 +3134,51 @@ __global__ void __launch_bounds__(kRangeThreads) k_fine_reduce(KP kp, PairRecord
     }
     __syncthreads();
   }
-  for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
-    const uint64_t o = a + i;
-    const unsigned long long key = stg.key[o];
-    if ((int64_t)(key >> 32) >= kp.P || (key >> 32) - (uint64_t)p0 >= (uint64_t)kRangeParts) {  // malformed
-      atomicOr(err, 1u);
-      continue;
+  // RB records per thread loaded together, then summed
+  constexpr int RB = 4;
+  for (unsigned i0 = threadIdx.x; i0 < len; i0 += RB * blockDim.x) {
+    unsigned long long kk[RB];
+    double w0[RB], w1[RB], w2[RB];
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const unsigned i = i0 + u * blockDim.x;
+      const uint64_t o = a + (i < len ? i : 0u);
+      kk[u] = i < len ? stg.key[o] : ~0ull;
+      w0[u] = (i < len && f0) ? stg.f0[o] : 0.0;
+      w1[u] = (i < len && f1) ? stg.f1[o] : 0.0;
+      w2[u] = (i < len && f2) ? stg.f2[o] : 0.0;
     }
-    const double v0 = f0 ? stg.f0[o] : 0.0, v1 = f1 ? stg.f1[o] : 0.0, v2 = f2 ? stg.f2[o] : 0.0;
-    if (direct) {
-      const int64_t p = (int64_t)(key >> 32);
-      atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
-      if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key);
-      if (f0) {
-        if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(v0));
-        else unsafeAtomicAdd((double*)acc.sum + p, v0);
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      if (i0 + u * blockDim.x >= len) continue;
+      const unsigned long long key = kk[u];
+      if ((int64_t)(key >> 32) >= kp.P || (key >> 32) - (uint64_t)p0 >= (uint64_t)kRangeParts) {  // malformed
+        atomicOr(err, 1u);
+        continue;
       }
-      if (f1) unsafeAtomicAdd(acc.normalized_sum + p, v1);
-      if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, v2);
-      continue;
+      const double v0 = w0[u], v1 = w1[u], v2 = w2[u];
+      if (direct) {
+        const int64_t p = (int64_t)(key >> 32);
+        atomicAdd((unsigned long long*)(acc.privacy_id_count + p), 1ull);
+        if (acc.count) atomicAdd((unsigned long long*)(acc.count + p), (unsigned long long)(uint32_t)key);
+        if (f0) {
+          if (sum_int) atomicAdd((unsigned long long*)acc.sum + p, (unsigned long long)__double_as_longlong(v0));
+          else unsafeAtomicAdd((double*)acc.sum + p, v0);
+        }
+        if (f1) unsafeAtomicAdd(acc.normalized_sum + p, v1);
+        if (f2) unsafeAtomicAdd(acc.normalized_sum_sq + p, v2);
+        continue;
+      }
+      const int lp = (int)((key >> 32) - (uint64_t)p0);
+      atomicAdd(pc + lp, 1u);
+      atomicAdd(cn + lp, (unsigned)key);
+      if (f0) {
+        if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0));
+        else atomicAdd(s0 + lp, v0);
+      }
+      if (f1) atomicAdd(s1 + lp, v1);
+      if (f2) atomicAdd(s2 + lp, v2);
     }
-    const int lp = (int)((key >> 32) - (uint64_t)p0);
-    atomicAdd(pc + lp, 1u);
-    atomicAdd(cn + lp, (unsigned)key);
-    if (f0) {
-      if (sum_int) atomicAdd((unsigned long long*)(s0 + lp), (unsigned long long)__double_as_longlong(v0));
-      else atomicAdd(s0 + lp, v0);
-    }
-    if (f1) atomicAdd(s1 + lp, v1);
-    if (f2) atomicAdd(s2 + lp, v2);
   }
   if (direct) return;
   __syncthreads();
@@ -3486,8 +3542,9 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     stg.f2 = w.stg_f2 ? (double*)(ws + w.stg_f2) : nullptr;
     PDP_HIP_CHECK(hipMemsetAsync(fine_total, 0, (uint64_t)(p.n_fine + 1) * 4, st));
     PDP_PROF_BEGIN("k_split_count", st);
+    unsigned* item_hist = (unsigned*)(ws + w.item_hist);
     hipLaunchKernelGGL(k_split_count, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec,
-                       (const uint4*)items, (const unsigned*)n_items, fine_total);
+                       (const uint4*)items, (const unsigned*)n_items, fine_total, item_hist);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     const int rc = scan_u32(fine_total, p.n_fine, (unsigned*)(ws + w.fine_chunks), st);
@@ -3495,7 +3552,7 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     PDP_HIP_CHECK(hipMemcpyAsync(fine_cur, fine_total, (uint64_t)p.n_fine * 4, hipMemcpyDeviceToDevice, st));
     PDP_PROF_BEGIN("k_split_scatter", st);
     hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
-                       (const uint4*)items, (const unsigned*)n_items, fine_cur);
+                       (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     uint4* fitems = (uint4*)(ws + w.fine_items);
@@ -3555,6 +3612,19 @@ int launch_scatter(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   return PDP_OK;
 }
 
+// compute units of the current device (cached per device)
+int64_t device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
 // tile-local level 1 -> level-2 cursors and bucket starts -> tile-local level 2
 template <int FMT>
 int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
@@ -3588,7 +3658,11 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
                        (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err,
                        (void*)&band, (void*)&band_cnt};
       PDP_PROF_BEGIN("k_sieve_l1", st);
-      PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(th), args1, lds1, st));
+      // persistent: as many workgroups as fit at once (one per CU at 1,024
+      // threads, two at 512), each looping over its tiles
+      const int64_t per_cu = th == kSieveThreads2 ? 2 : 1;
+      const int64_t grid1 = std::min<int64_t>(p.n_tiles, per_cu * device_cus());
+      PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)grid1), dim3(th), args1, lds1, st));
       PDP_PROF_END(st);
       PDP_HIP_CHECK(hipGetLastError());
     }

@@ -15,7 +15,9 @@ while IFS='|' read -r name bargs; do
 import json, sys
 r = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 bp = r.get("bound_plan") or {}
+st = bp.get("stats") or {}
 print(sys.argv[2], "ms/step %.3f" % r["ms_per_step"], "plan", {k: bp.get(k) for k in ("sieve", "band", "merge", "key_format", "sieve_threads") if k in bp},
+      {k: st[k] for k in ("rows_partitioned", "band_rows", "unresolved_ids", "unresolved2_ids") if k in st},
       {k: round(v["ms"], 3) for k, v in r["kernels"].items() if v["ms"] * v.get("launches_per_step", 1) > 0.03}, flush=True)
 s = r.get("secondary")
 if s:
