@@ -3674,6 +3674,9 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
     void* args1[] = {(void*)&kp,         (void*)&pid,  (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
                      (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err};
     PDP_PROF_BEGIN("k_scatter_l1", st);
+    // (one workgroup per tile: a persistent form with the next stage's loads
+    // issued early measured the same at C5, 3.04 vs 3.06 ms -- the 2:1
+    // read/write mix, not load latency, bounds it; profiles/r04/ab/ab3_l1_local.txt)
     PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
