@@ -406,7 +406,7 @@ def run_api_workload(args, workload, world, rank, device):
             "algorithm": info.algorithm, "bucket_bits": info.bucket_bits, "n_buckets": info.n_buckets,
             "lds_bytes": info.lds_bytes, "merge": info.merge, "sieve": info.sieve / 65536.0,
             "band": info.band / 65536.0, "tuning": tune,
-            "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(info.key_format,
+            "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide", 5: "packed64"}.get(info.key_format,
                                                                                      info.key_format)},
         "seed": None,
         "partitions_kept": kept,
@@ -522,7 +522,7 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
     from pipelinedp_amd import _native as N
     rec1 = {N.KEYS_COMPACT: 8, N.KEYS_WIDE: 12}.get(plan.key_format, 8)        # level-1 record
     rec2 = {N.KEYS_WIDE: 12, N.KEYS_PACKED_WIDE: 12}.get(plan.key_format, 8)   # level-2 key + row
-    key2 = rec2 - 4
+    key2 = 8 if plan.key_format == N.KEYS_PACKED64 else rec2 - 4                # what B1 streams
     pair_rec = 8 + 8 * n_fields
     cand = stats["rows_partitioned"]
     fix = stats["fixup_rows"]
@@ -735,7 +735,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         "kernels": table,
         "bound_plan": {"algorithm": plan.algorithm, "bucket_bits": plan.bucket_bits,
                        "n_buckets": plan.n_buckets, "lds_bytes": plan.lds_bytes,
-                       "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide"}.get(
+                       "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide", 5: "packed64"}.get(
                            plan.key_format, plan.key_format),
                        "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0,
                        "sieve_threads": plan.sieve_threads, "stats": stats},

@@ -119,6 +119,12 @@ typedef struct pdp_bound_config {
                               level 2 on: the COMPACT pair.  8 B per row and pass: needs bucket +
                               partition bits <= 31 and super + bucket + partition bits <= 47
                               (AUTO's first choice with the tile-local level 1) */
+#define PDP_KEYS_PACKED64 5 /* level 1 PACKED (8 B), level 2 on one u64 per record (row << (bucket + partition
+                              bits) | bucket-local pid << partition bits | partition; all ones = dead): 8 B
+                              per record and pass with no row array, where the bucket + partition bits
+                              exceed 31 (C4/C5: P = 1e7) but rows < 2^(64 - bucket - partition bits) - 2 and
+                              super + bucket + partition bits <= 47; tile-local level 1 only (AUTO picks it
+                              there before PACKED_WIDE) */
 #define PDP_KEYS_PACKED_WIDE 4 /* level 1 PACKED (8 B), level 2 on WIDE (u64 key + u32 row):
                               partition counts whose bucket + partition bits exceed 31 (C4/C5:
                               P = 1e7) with super + bucket + partition bits <= 47; tile-local

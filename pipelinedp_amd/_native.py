@@ -30,7 +30,7 @@ OP_COUNT, OP_SUM, OP_PRIVACY_ID_COUNT, OP_MEAN, OP_VARIANCE, OP_THRESHOLDED_PID 
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
 ALGO_AUTO, ALGO_GLOBAL_SKETCH, ALGO_BUCKETED, ALGO_PAIR_TABLE = 0, 1, 2, 3
 MERGE_AUTO, MERGE_ATOMIC, MERGE_RANGES = 0, 1, 2
-KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED, KEYS_PACKED_WIDE = 0, 1, 2, 3, 4
+KEYS_AUTO, KEYS_WIDE, KEYS_COMPACT, KEYS_PACKED, KEYS_PACKED_WIDE, KEYS_PACKED64 = 0, 1, 2, 3, 4, 5
 MAX_L0 = 2**31 - 1            # pipelinedp_amd.h PDP_MAX_*
 MAX_LINF = 2**31 - 1
 MAX_CONTRIBUTIONS = 2**31 - 1

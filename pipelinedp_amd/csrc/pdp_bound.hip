@@ -283,6 +283,10 @@ Plan make_plan(const pdp_bound_config* c) {
                          p.super_bits + p.bucket_bits + p.pk_bits <= 64 - 1 - kTileRowBits;
   // PACKED level 1 with WIDE records from level 2 on (tile-local level 1 only)
   const bool packed_wide_ok = p.super_bits + p.bucket_bits + p.pk_bits <= 64 - 1 - kTileRowBits;
+  // ... or with one u64 per record (PACKED64): the row above the bucket-local
+  // pid and partition, all ones reserved for dead records
+  const int row_bits = 64 - p.bucket_bits - p.pk_bits;
+  const bool packed64_ok = packed_wide_ok && (row_bits >= 33 || c->n_rows < ((int64_t)1 << row_bits) - 2);
   p.key_format = 0;
   p.n_stages = (c->n_rows + kL1Rows - 1) / kL1Rows;
   p.l1_local = 0;
@@ -298,12 +302,15 @@ Plan make_plan(const pdp_bound_config* c) {
       // run as one span), else PACKED_WIDE; else COMPACT / PACKED / WIDE
       if (packed_ok && local_fits(PDP_KEYS_PACKED))
         p.key_format = PDP_KEYS_PACKED;
+      else if (!packed_ok && packed64_ok && local_fits(PDP_KEYS_PACKED64))
+        p.key_format = PDP_KEYS_PACKED64;
       else if (!packed_ok && packed_wide_ok && local_fits(PDP_KEYS_PACKED_WIDE))
         p.key_format = PDP_KEYS_PACKED_WIDE;
       else
         p.key_format = compact_ok ? PDP_KEYS_COMPACT : (packed_ok ? PDP_KEYS_PACKED : PDP_KEYS_WIDE);
     } else if ((want == PDP_KEYS_COMPACT && !compact_ok) || (want == PDP_KEYS_PACKED && !packed_ok) ||
-               (want == PDP_KEYS_PACKED_WIDE && !(packed_wide_ok && local_fits(PDP_KEYS_PACKED_WIDE)))) {
+               (want == PDP_KEYS_PACKED_WIDE && !(packed_wide_ok && local_fits(PDP_KEYS_PACKED_WIDE))) ||
+               (want == PDP_KEYS_PACKED64 && !(packed64_ok && local_fits(PDP_KEYS_PACKED64)))) {
       p.algorithm = -1;  // infeasible
     } else {
       p.key_format = want;
@@ -462,9 +469,12 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.super_base = off; off = align256(off + (uint64_t)(p.n_supers + 1) * 4);
     w.super_tm = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
     w.super_off = off; off = align256(off + (uint64_t)p.n_tiles * p.n_supers * 4);
-    const bool packed = (p.key_format == PDP_KEYS_PACKED || p.key_format == PDP_KEYS_PACKED_WIDE) && p.super_bits > 0;
+    const bool packed = (p.key_format == PDP_KEYS_PACKED || p.key_format == PDP_KEYS_PACKED_WIDE ||
+                         p.key_format == PDP_KEYS_PACKED64) && p.super_bits > 0;
     const uint64_t kb1 = p.key_format == PDP_KEYS_COMPACT ? 4 : 8;  // level-1 key
-    const uint64_t kb2 = (p.key_format == PDP_KEYS_WIDE || p.key_format == PDP_KEYS_PACKED_WIDE) ? 8 : 4;  // level-2 key
+    const uint64_t kb2 = (p.key_format == PDP_KEYS_WIDE || p.key_format == PDP_KEYS_PACKED_WIDE ||
+                          p.key_format == PDP_KEYS_PACKED64) ? 8 : 4;  // level-2 key
+    const bool rows2 = p.key_format != PDP_KEYS_PACKED64;  // PACKED64: the row rides in the key
     // level-1 records: stage blocks, or the sieve's per-tile flush blocks
     const uint64_t n1 = p.sieve ? (uint64_t)p.n_tiles * kSieveTileStride
                                 : (p.l1_local ? (uint64_t)p.n_stages * kL1Rows : n);
@@ -496,7 +506,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     }
     if (p.super_bits > 0) {
       w.keys2 = off; off = align256(off + n * kb2);
-      w.rows2 = off; off = align256(off + n * 4);
+      if (rows2) { w.rows2 = off; off = align256(off + n * 4); }
+      else w.rows2 = w.keys2;  // unused
     } else {
       w.keys2 = w.keys1;
       w.rows2 = w.rows1;
@@ -561,7 +572,7 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad algorithm");
   if (c->merge < PDP_MERGE_AUTO || c->merge > PDP_MERGE_RANGES)
     return set_error(PDP_E_INVALID, "bad merge");
-  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED_WIDE)
+  if (c->key_format < PDP_KEYS_AUTO || c->key_format > PDP_KEYS_PACKED64)
     return set_error(PDP_E_INVALID, "bad key_format");
   if (c->sieve_threads != 0 && c->sieve_threads != kSieveThreads2 && c->sieve_threads != kL1Threads)
     return set_error(PDP_E_INVALID, "sieve_threads must be 0, 512 or 1024");
@@ -594,6 +605,7 @@ struct KP {  // kernel parameters
   int sieve_emit;       // bucket kernel (main launch, band on): unresolved ids' candidate rows -> fix_rec
   int slot_bits;        // level-1 blocks per tile = 2^slot_bits (Plan.slot_bits)
   int64_t fix_cap;      // sieve: entries the fix-up row list (fix_rec, Ws.fix_rec) holds
+  int row_shift;        // PACKED64 level-2 records: the row's first bit (pk_bits + bucket_bits)
 };
 
 KP make_kp(const pdp_bound_config* c, const Plan& p) {
@@ -622,6 +634,7 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.sieve_emit = p.band != 0;
   k.slot_bits = p.slot_bits;
   k.fix_cap = 0;  // set from the layout (Ws.fix_cap) where the fix-up runs
+  k.row_shift = p.pk_bits + p.bucket_bits;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -911,10 +924,24 @@ using RecKey = typename std::conditional<COMPACT, uint32_t, unsigned long long>:
 template <int FMT>
 using L1Key = typename std::conditional<FMT == PDP_KEYS_COMPACT, uint32_t, unsigned long long>::type;
 template <int FMT>
-constexpr bool kPackedL1 = FMT == PDP_KEYS_PACKED || FMT == PDP_KEYS_PACKED_WIDE;  // no level-1 row array
+constexpr bool kPackedL1 =
+    FMT == PDP_KEYS_PACKED || FMT == PDP_KEYS_PACKED_WIDE || FMT == PDP_KEYS_PACKED64;  // no level-1 row array
 // level-2 (bucket-order) record key per format
 template <int FMT>
-using L2Key = RecKey<FMT != PDP_KEYS_WIDE && FMT != PDP_KEYS_PACKED_WIDE>;
+using L2Key = RecKey<FMT != PDP_KEYS_WIDE && FMT != PDP_KEYS_PACKED_WIDE && FMT != PDP_KEYS_PACKED64>;
+// level-2 records of the bucket kernel: u32 key + u32 row (COMPACT, and
+// PACKED from level 2 on), u64 key + u32 row (WIDE, PACKED_WIDE), one u64
+// with the row in its high bits (PACKED64; all ones = dead)
+constexpr int kRecCompact = 0, kRecWide = 1, kRecP64 = 2;
+template <int FMT>
+constexpr int kRecOf = FMT == PDP_KEYS_PACKED64 ? kRecP64
+                                                 : ((FMT == PDP_KEYS_WIDE || FMT == PDP_KEYS_PACKED_WIDE) ? kRecWide
+                                                                                                          : kRecCompact);
+inline int rec_of(int key_format) {
+  return key_format == PDP_KEYS_PACKED64 ? kRecP64
+                                         : ((key_format == PDP_KEYS_WIDE || key_format == PDP_KEYS_PACKED_WIDE)
+                                                ? kRecWide : kRecCompact);
+}
 
 // MAXD destinations per stage; the small form (<= 256 destinations, u8 tags)
 // fits four workgroups per CU with compact keys instead of three.  ROWS:
@@ -935,7 +962,8 @@ size_t l1_stage_bytes(int key_format) {
   switch (key_format) {
     case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kL1Items, kL1Threads>);
     case PDP_KEYS_PACKED:
-    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kL1Items, kL1Threads>);
+    case PDP_KEYS_PACKED_WIDE:
+    case PDP_KEYS_PACKED64: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kL1Items, kL1Threads>);
     default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kL1Items, kL1Threads>);
   }
 }
@@ -945,7 +973,8 @@ size_t sieve_stage_bytes_t(int key_format) {
   switch (key_format) {
     case PDP_KEYS_COMPACT: return sizeof(StageLds<L1Key<PDP_KEYS_COMPACT>, kSmallDest, true, kSieveItems, TH>);
     case PDP_KEYS_PACKED:
-    case PDP_KEYS_PACKED_WIDE: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kSieveItems, TH>);
+    case PDP_KEYS_PACKED_WIDE:
+    case PDP_KEYS_PACKED64: return sizeof(StageLds<L1Key<PDP_KEYS_PACKED>, kSmallDest, false, kSieveItems, TH>);
     default: return sizeof(StageLds<L1Key<PDP_KEYS_WIDE>, kSmallDest, true, kSieveItems, TH>);
   }
 }
@@ -1862,11 +1891,13 @@ __device__ __forceinline__ KO unpacked_key(const KP& kp, uint32_t local, uint64_
   }
 }
 
-// tile-local level 2 records per thread: half for 8-byte level-2 keys
-// (WIDE / PACKED_WIDE), so their LDS windows and registers leave room for two
-// workgroups per CU
+// tile-local level 2 records per thread: half for 8-byte level-2 keys with a
+// row array (WIDE / PACKED_WIDE), so their LDS windows and registers leave
+// room for two workgroups per CU; PACKED64 carries no row array
 template <int FMT>
-constexpr int l2_items() { return sizeof(L2Key<FMT>) == 8 ? kL2Items / 2 : kL2Items; }
+constexpr int l2_items() { return sizeof(L2Key<FMT>) == 8 && FMT != PDP_KEYS_PACKED64 ? kL2Items / 2 : kL2Items; }
+template <int FMT>
+constexpr bool kL2RowArray = FMT != PDP_KEYS_PACKED64;  // level 2 writes a row array
 
 template <int FMT, int MAXD>
 __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const uint16_t* __restrict__ soff,
@@ -1884,7 +1915,7 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
   constexpr bool PACKED = kPackedL1<FMT>;  // PACKED / PACKED_WIDE level-1 records
   constexpr bool ROWS1 = !PACKED;
   extern __shared__ unsigned long long stage_raw[];
-  using SL = StageLds<KO, MAXD, true, NI, kL2Threads>;
+  using SL = StageLds<KO, MAXD, kL2RowArray<FMT>, NI, kL2Threads>;
   using D = typename SL::D;
   SL& s = *reinterpret_cast<SL*>(stage_raw);
 #ifdef PDP_PHASE_CLOCK
@@ -2000,8 +2031,13 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
           const uint64_t v = raw[q];
           const uint32_t mid = (uint32_t)((v >> kp.pk_bits) & ((1ULL << (bb + kp.super_bits)) - 1));
           d[h + q] = (int)(mid >> bb);
-          x[h + q] = unpacked_key<KO>(kp, mid & local_mask, v);
           r[h + q] = rr[q] + (uint32_t)((v >> kPackedRowShift) & (kTileRows - 1));
+          if constexpr (FMT == PDP_KEYS_PACKED64)  // (row | local pid | partition), all ones if dead
+            x[h + q] = (KO)((v >> 63) ? ~0ULL
+                                      : (((uint64_t)r[h + q] << kp.row_shift) |
+                                         ((uint64_t)(mid & local_mask) << kp.pk_bits) | (v & kp.pk_mask)));
+          else
+            x[h + q] = unpacked_key<KO>(kp, mid & local_mask, v);
         } else {
           x[h + q] = (KO)raw[q];
           r[h + q] = rr[q];
@@ -2054,11 +2090,12 @@ struct WaveQueue {
 // RM: what a candidate carries beside its key -- kRowNone, kRowLoad (rows[i],
 // a 16-byte load per R records beside the keys) or kRowIndex (the record's
 // position i in `keys`, for candidate lists).
-constexpr int kRowNone = 0, kRowLoad = 1, kRowIndex = 2;
+// kRowFromKey: the row is the record's bits from row_shift up (PACKED64).
+constexpr int kRowNone = 0, kRowLoad = 1, kRowIndex = 2, kRowFromKey = 3;
 template <int KU, int RM, typename K, typename CV, typename P, typename W>
 __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const unsigned* __restrict__ rows,
                                               int64_t begin, int64_t end, WaveQueue q, CV&& conv, P&& pred,
-                                              W&& work) {
+                                              W&& work, int row_shift = 0) {
   constexpr bool ROWS = RM != kRowNone;
   constexpr bool LOADR = RM == kRowLoad;
   constexpr int R = 16 / sizeof(K);
@@ -2106,11 +2143,13 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
       x = conv(keys[begin + t]);
       if (LOADR) r = rows[begin + t];
       if (RM == kRowIndex) r = (uint32_t)(begin + t);
+      if (RM == kRowFromKey) r = (uint32_t)((uint64_t)keys[begin + t] >> row_shift);
     }
     if (t >= R && t < 2 * R - 1 && a1 + (t - R) < end) {
       x = conv(keys[a1 + (t - R)]);
       if (LOADR) r = rows[a1 + (t - R)];
       if (RM == kRowIndex) r = (uint32_t)(a1 + (t - R));
+      if (RM == kRowFromKey) r = (uint32_t)((uint64_t)keys[a1 + (t - R)] >> row_shift);
     }
     push(x, r);
   }
@@ -2142,6 +2181,9 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
       } else if constexpr (RM == kRowLoad) {
         if constexpr (R == 4) return e == 0 ? rx[u].x : (e == 1 ? rx[u].y : (e == 2 ? rx[u].z : rx[u].w));
         else return e == 0 ? rx[u].x : rx[u].y;
+      } else if constexpr (RM == kRowFromKey) {
+        static_assert(R == 2, "row-in-key records are 8 bytes");
+        return (uint32_t)((uint64_t)(e == 0 ? kx[u].x : kx[u].y) >> row_shift);
       } else {
         return 0u;
       }
@@ -2202,19 +2244,20 @@ struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
   } while (0)
 #endif
 
-template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES, bool COMPACT>
-__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const RecKey<COMPACT>* __restrict__ keys,
+template <int VALUE_KIND, bool KEEP_ALL_ROWS, bool RANGES, int REC>
+__global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const RecKey<REC == kRecCompact>* __restrict__ keys,
                                                                  const unsigned* __restrict__ rowidx,
                                                                  const unsigned* __restrict__ offsets,
                                                                  const void* __restrict__ value,
                                                                  pdp_partition_accumulators acc, PairRecords rec,
-                                                                 RecKey<COMPACT>* __restrict__ cand_key,
+                                                                 RecKey<REC == kRecCompact>* __restrict__ cand_key,
                                                                  unsigned* __restrict__ cand_idx,
                                                                  unsigned* __restrict__ unres_bits,
                                                                  unsigned* __restrict__ unres_list,
                                                                  unsigned* __restrict__ sctl, unsigned* __restrict__ err,
                                                                  unsigned long long* __restrict__ fix_rec,
                                                                  const unsigned* __restrict__ unres_prev) {
+  constexpr bool COMPACT = REC == kRecCompact;
   extern __shared__ unsigned long long smem[];
 #ifdef PDP_PHASE_CLOCK
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -2298,7 +2341,17 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const int64_t begin = offsets[b];
   const int64_t end = offsets[b + 1];  // offsets has n_buckets + 1 entries
   const uint64_t bmask = (uint64_t)S - 1;
-  auto conv = [&](RecKey<COMPACT> v) -> uint64_t { return expand_key(kp, hpid, v); };
+  // PACKED64 records (row | local pid | partition; all ones dead) and their
+  // candidate-list form (local pid | partition)
+  auto expand64 = [&](unsigned long long v) -> uint64_t {
+    if (v == ~0ULL) return kEmpty;
+    const uint64_t local = (v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1);
+    return pair_key_from(hpid[local].x, kp.seed, (int64_t)(v & kp.pk_mask), local << kp.pk_bits, kp.rand_shift);
+  };
+  auto conv = [&](RecKey<COMPACT> v) -> uint64_t {
+    if constexpr (REC == kRecP64) return expand64(v);
+    else return expand_key(kp, hpid, v);
+  };
   // B1: bottom-l0 distinct pair keys per privacy id; candidates are keys at or
   // below their sketch's current maximum.  A pair kept in the end entered the
   // sketch at its first row and never left it (the maximum only decreases),
@@ -2312,10 +2365,18 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   const uint64_t lbits = ((uint64_t)1 << (kp.pk_bits + kp.bucket_bits)) - 1;  // local pid | partition
   // (each record's row index rides along, loaded with its key: B2 then needs
   // no dependent gather of it)
-  stream_bucket<COMPACT ? 4 : kUnroll, kRowLoad>(
+  stream_bucket<COMPACT ? 4 : kUnroll, REC == kRecP64 ? kRowFromKey : kRowLoad>(
       keys, rowidx, begin, end, wq,
       // the candidate test rides on the pid-hash read (b1_candidate)
-      [&](RecKey<COMPACT> v) -> uint64_t { return b1_candidate(kp, hpid, v); },
+      [&](RecKey<COMPACT> v) -> uint64_t {
+        if constexpr (REC == kRecP64) {
+          const uint64_t x = expand64(v);
+          if (x == kEmpty) return kEmpty;
+          return (uint32_t)(x >> 32) <= hpid[(v >> kp.pk_bits) & ((1ULL << kp.bucket_bits) - 1)].y ? x : kEmpty;
+        } else {
+          return b1_candidate(kp, hpid, v);
+        }
+      },
       [&](uint64_t x) { return x != kEmpty; },
       [&](uint64_t x, uint32_t i)  {  // i: the record's row
         const int64_t pl = (int64_t)((x >> kp.pk_bits) & bmask);
@@ -2336,7 +2397,8 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
           cand_key[o] = (RecKey<COMPACT>)(x & lbits);
           cand_idx[o] = i;
         }
-      });
+      },
+      kp.row_shift);
   __syncthreads();
   if (kp.sieve_mark) mark(true);  // emits nothing for its unresolved ids (B2 skips them): the fix-up's
   PDP_PHASE(2);
@@ -2729,14 +2791,15 @@ __global__ void __launch_bounds__(kBlock) k_fix_filter(KP kp, const unsigned* __
 // of the per-bucket counts; a slot per row from the bucket's cursor), as the
 // bucket kernel's records: (bucket-local pid << pk_bits | partition), dead
 // bit for a non-public or invalid partition, and the row.
-template <bool COMPACT>
+template <int REC>
 __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __restrict__ pk,
                                                         const uint8_t* __restrict__ allowed,
                                                         const unsigned long long* __restrict__ fix_rec,
                                                         const unsigned* __restrict__ sctl,
                                                         const unsigned* __restrict__ fix_start,
                                                         unsigned* __restrict__ fix_cur,
-                                                        RecKey<COMPACT>* __restrict__ keys, unsigned* __restrict__ rows) {
+                                                        RecKey<REC == kRecCompact>* __restrict__ keys,
+                                                        unsigned* __restrict__ rows) {
   const int64_t total = (int64_t)sctl[1] < kp.fix_cap ? (int64_t)sctl[1] : kp.fix_cap;
   const uint64_t lmask = ((uint64_t)1 << kp.bucket_bits) - 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -2749,11 +2812,13 @@ __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __
     const uint64_t lpk = (u & lmask) << kp.pk_bits;
     const int64_t b = (int64_t)(u >> kp.bucket_bits);
     const unsigned pos = fix_start[b] + atomicAdd(fix_cur + b, 1u);
-    if constexpr (COMPACT)
+    if constexpr (REC == kRecCompact)
       keys[pos] = (uint32_t)(dead ? (0x80000000ull | lpk) : (lpk | (uint64_t)k));
-    else
+    else if constexpr (REC == kRecWide)
       keys[pos] = dead ? ((1ull << 63) | lpk) : (lpk | (uint64_t)k);
-    rows[pos] = r;
+    else  // PACKED64: the row in the key, all ones if dead
+      keys[pos] = dead ? ~0ull : (((uint64_t)r << kp.row_shift) | lpk | (uint64_t)k);
+    if constexpr (REC != kRecP64) rows[pos] = r;
   }
 }
 
@@ -3370,12 +3435,15 @@ int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void
                          const unsigned* offsets, const void* value, const pdp_partition_accumulators& acc,
                          PairRecords rec, char* ws, const Ws& w, const char* name, const Marks& mk) {
   const bool ranges = p.merge == PDP_MERGE_RANGES;
-  // PACKED: COMPACT records from level 2 on; PACKED_WIDE: WIDE ones
-  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
-  const void* kern = compact ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, true>
-                                       : (const void*)k_bucket_bound<VK, KA, false, true>)
-                             : (ranges ? (const void*)k_bucket_bound<VK, KA, true, false>
-                                       : (const void*)k_bucket_bound<VK, KA, false, false>);
+  // PACKED: COMPACT records from level 2 on; PACKED_WIDE: WIDE ones; PACKED64: its own
+  const int kind = rec_of(p.key_format);
+  const void* kern =
+      kind == kRecCompact ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, kRecCompact>
+                                   : (const void*)k_bucket_bound<VK, KA, false, kRecCompact>)
+      : kind == kRecWide  ? (ranges ? (const void*)k_bucket_bound<VK, KA, true, kRecWide>
+                                   : (const void*)k_bucket_bound<VK, KA, false, kRecWide>)
+                         : (ranges ? (const void*)k_bucket_bound<VK, KA, true, kRecP64>
+                                   : (const void*)k_bucket_bound<VK, KA, false, kRecP64>);
   PDP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)p.lds_bytes));
   void* cand_key = ws + w.cand_key;
   unsigned* cand_idx = (unsigned*)(ws + w.cand_idx);
@@ -3430,7 +3498,7 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   int rc = launch_bucket_kernel<VK, KA>(kp, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
                                         (const unsigned*)(ws + w.counts), value, acc, rec, ws, w, "k_bucket_bound", m1);
   if (rc != PDP_OK || !p.sieve) return rc;
-  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
+  const int kind = rec_of(p.key_format);
   const int64_t n_slots = (int64_t)kp.l0 << kp.bucket_bits;
   // one fix-up: rows listed in fix_rec (sctl[1] of them) -> exact test ->
   // bucket order -> a bucket launch over them into record segment `seg`
@@ -3445,12 +3513,16 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     if (r != PDP_OK) return r;
     const unsigned fix_grid = grid_for(kp.n, 2048);
     PDP_PROF_BEGIN("k_fix_scatter", st);
-    if (compact)
-      hipLaunchKernelGGL(k_fix_scatter<true>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+    if (kind == kRecCompact)
+      hipLaunchKernelGGL(k_fix_scatter<kRecCompact>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
                          (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
                          (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    else if (kind == kRecWide)
+      hipLaunchKernelGGL(k_fix_scatter<kRecWide>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
     else
-      hipLaunchKernelGGL(k_fix_scatter<false>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+      hipLaunchKernelGGL(k_fix_scatter<kRecP64>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
                          (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
                          (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
     PDP_PROF_END(st);
@@ -3707,8 +3779,8 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   const bool small = ((int64_t)1 << p.super_bits) <= kSmallDest;
   const void* l2 = small ? (const void*)k_scatter_l2_local<FMT, kSmallDest>
                          : (const void*)k_scatter_l2_local<FMT, kMaxDest>;
-  const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, true, l2_items<FMT>(), kL2Threads>)
-                            : sizeof(StageLds<K2, kMaxDest, true, l2_items<FMT>(), kL2Threads>);
+  const size_t lds2 = small ? sizeof(StageLds<K2, kSmallDest, kL2RowArray<FMT>, l2_items<FMT>(), kL2Threads>)
+                            : sizeof(StageLds<K2, kMaxDest, kL2RowArray<FMT>, l2_items<FMT>(), kL2Threads>);
   PDP_HIP_CHECK(hipFuncSetAttribute(l2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
   const uint16_t* soff_c = soff;
   const unsigned* sbase_c = sbase;
@@ -3733,26 +3805,35 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
 // gets the all-ones partition (>= P when P is not a power of two) and every
 // record of bucket 1 an out-of-range row, as a malformed workspace would
 // carry; the bucket kernel must flag them in the error word, not fault
-template <bool COMPACT>
+template <int REC>
 __global__ void __launch_bounds__(kBlock) k_debug_corrupt(KP kp, const unsigned* __restrict__ starts,
-                                                          RecKey<COMPACT>* __restrict__ keys,
+                                                          RecKey<REC == kRecCompact>* __restrict__ keys,
                                                           unsigned* __restrict__ rows) {
   const int64_t nb = kp.n_buckets < 2 ? kp.n_buckets : 2;
   for (int64_t i = (int64_t)starts[0] + blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)starts[nb];
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (i < (int64_t)starts[1]) keys[i] = keys[i] | (RecKey<COMPACT>)kp.pk_mask;
-    else rows[i] = 0xFFFFFFF0u;
+    if (i < (int64_t)starts[1]) {
+      if (REC != kRecP64 || keys[i] != ~0ull) keys[i] = keys[i] | (RecKey<REC == kRecCompact>)kp.pk_mask;
+    } else if constexpr (REC == kRecP64) {  // row field all ones but one: >= n_rows (the plan keeps rows below)
+      const uint64_t low = (1ull << kp.row_shift) - 1;
+      if (keys[i] != ~0ull) keys[i] = (keys[i] & low) | (((~0ull >> kp.row_shift) - 1) << kp.row_shift);
+    } else {
+      rows[i] = 0xFFFFFFF0u;
+    }
   }
 }
 
 int launch_debug_corrupt(const KP& kp, const Plan& p, hipStream_t st, char* ws, const Ws& w) {
-  const bool compact = p.key_format != PDP_KEYS_WIDE && p.key_format != PDP_KEYS_PACKED_WIDE;
+  const int rec = rec_of(p.key_format);
   const unsigned* starts = (const unsigned*)(ws + w.counts);
-  if (compact)
-    hipLaunchKernelGGL(k_debug_corrupt<true>, dim3(64), dim3(kBlock), 0, st, kp, starts, (uint32_t*)(ws + w.keys2),
-                       (unsigned*)(ws + w.rows2));
+  if (rec == kRecCompact)
+    hipLaunchKernelGGL(k_debug_corrupt<kRecCompact>, dim3(64), dim3(kBlock), 0, st, kp, starts,
+                       (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+  else if (rec == kRecP64)
+    hipLaunchKernelGGL(k_debug_corrupt<kRecP64>, dim3(64), dim3(kBlock), 0, st, kp, starts,
+                       (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
   else
-    hipLaunchKernelGGL(k_debug_corrupt<false>, dim3(64), dim3(kBlock), 0, st, kp, starts,
+    hipLaunchKernelGGL(k_debug_corrupt<kRecWide>, dim3(64), dim3(kBlock), 0, st, kp, starts,
                        (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
@@ -3955,6 +4036,8 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
       rc2 = launch_local<PDP_KEYS_PACKED>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
     else if (p.key_format == PDP_KEYS_PACKED_WIDE)
       rc2 = launch_local<PDP_KEYS_PACKED_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
+    else if (p.key_format == PDP_KEYS_PACKED64)
+      rc2 = launch_local<PDP_KEYS_PACKED64>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
     else
       rc2 = launch_local<PDP_KEYS_WIDE>(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   } else {

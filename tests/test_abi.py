@@ -139,7 +139,7 @@ def test_sieve_plan(lib):
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c4)), ctypes.byref(info)) == 0
     assert info.sieve == 0
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c4, sieve=4096)), ctypes.byref(info)) == 0
-    assert info.sieve == 4096 and info.key_format == N.KEYS_PACKED_WIDE
+    assert info.sieve == 4096 and info.key_format == N.KEYS_PACKED64  # 8-byte level-2 records (row in the key)
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=-1)), ctypes.byref(info)) == 0
     assert info.sieve == 0
     assert lib.pdp_bound_plan(ctypes.byref(_cfg(**c3, sieve=1 << 20)), ctypes.byref(info)) == 0
@@ -191,7 +191,7 @@ def test_workspace_bytes(lib):
     ("max_contributions", -1, -4, b"max_contributions"),
     ("n_rows", 1 << 32, -1, b"n_rows"), ("n_partitions", 0, -1, b"n_partitions"),
     ("n_privacy_ids", 0, -1, b"n_privacy_ids"), ("value_kind", 7, -1, b"value_kind"),
-    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 5, -1, b"key_format"),
+    ("algorithm", 9, -1, b"algorithm"), ("merge", 5, -1, b"merge"), ("key_format", 6, -1, b"key_format"),
 ])
 def test_invalid_configs_are_rejected(lib, field, value, code, msg):
     info = N.BoundPlanInfo()

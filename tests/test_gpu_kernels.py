@@ -234,7 +234,7 @@ def test_two_level_range_merge_matches_oracle(device, P, skew):
     _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
 
 
-@pytest.mark.parametrize("keys", [1, 2, 3, 4], ids=["wide", "compact", "packed", "packed-wide"])
+@pytest.mark.parametrize("keys", [1, 2, 3, 4, 5], ids=["wide", "compact", "packed", "packed-wide", "packed64"])
 @pytest.mark.parametrize("public", [False, True])
 def test_tile_local_partition_matches_oracle(device, keys, public):
     """The tile-local level 1 (stage blocks + per-stage super-bucket offsets,
@@ -303,13 +303,15 @@ def test_tile_local_partition_unaligned_columns(device):
 def test_compact_records_chosen_when_they_fit():
     """C2 (U = 1e6, P = 1e5, L0 = 8, Linf = 2) moves 8-byte records: PACKED
     (one u64 per row) through the tile-local level 1, then COMPACT pairs; at
-    P = 1e7 the level-1 record stays PACKED and level 2 on moves the 12-byte
-    (u64 key + row) WIDE records."""
+    P = 1e7 the level-1 record stays PACKED and level 2 on moves PACKED64
+    records (row, bucket-local pid and partition in one u64) -- 8 bytes, not
+    the 12 of PACKED_WIDE's u64 key + row."""
     from pipelinedp_amd import executor as X
     spec = X.BoundingSpec(l0=8, linf=2, value_kind=O.VALUE_F64, flags=O.ACC_NSUM, min_value=0.0,
                           max_value=10.0, middle=5.0)
     assert X.bound_plan(100_000_000, 1_000_000, 100_000, spec).key_format == 3
-    assert X.bound_plan(100_000_000, 1_000_000, 10_000_000, spec).key_format == 4
+    assert X.bound_plan(100_000_000, 1_000_000, 10_000_000, spec).key_format == 5
+    assert X.bound_plan(100_000_000, 1_000_000, 10_000_000, spec, key_format=4).key_format == 4
 
 
 def test_empty_input(device):

@@ -306,10 +306,11 @@ def test_c4_bucketing_packed_wide_records_match_oracle(device):
     val = rng.random(n) * 10.0
     spec = _spec(4, 2, O.VALUE_F64, O.ACC_NSUM | O.ACC_NSUM2)
     plan = _plan(n, U, P, spec)
-    assert plan.algorithm == 2 and plan.key_format == 4 and plan.n_buckets > 10_000
-    got = _gpu(device, pid, pk, val, U, P, spec, 0x4C4)
+    assert plan.algorithm == 2 and plan.key_format == 5 and plan.n_buckets > 10_000  # PACKED64
     want = _oracle(pid, pk, val, U, P, spec, 0x4C4, plan.rand_shift)
-    _compare(got, want, _scale(pk, val, P, spec))
+    _compare(_gpu(device, pid, pk, val, U, P, spec, 0x4C4), want, _scale(pk, val, P, spec))
+    assert _plan(n, U, P, spec, key_format=4).key_format == 4  # and PACKED_WIDE, asked for
+    _compare(_gpu(device, pid, pk, val, U, P, spec, 0x4C4, key_format=4), want, _scale(pk, val, P, spec))
 
 
 def test_many_buckets_wide_level2_fanout_matches_oracle(device):
@@ -380,7 +381,7 @@ def test_c5_shard_plan_matches_oracle(device):
     val = np.clip(rng.lognormal(1.0, 1.0, n), 0.0, 20.0)
     spec = _spec(4, 2, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 20.0)
     plan = _plan(n, U, P, spec)
-    assert plan.algorithm == N.ALGO_BUCKETED and plan.key_format == N.KEYS_PACKED_WIDE
+    assert plan.algorithm == N.ALGO_BUCKETED and plan.key_format == N.KEYS_PACKED64
     assert plan.merge == N.MERGE_RANGES and plan.n_ranges < -(-P // 2048)  # coarse ranges: two-level merge
     got = _gpu(device, pid, pk, val, U, P, spec, 0x5C5)
     want = _oracle(pid, pk, val, U, P, spec, 0x5C5, plan.rand_shift)

@@ -105,7 +105,8 @@ def test_sieve_key_formats_public_filter_and_offset(device, key_format):
         assert (got["privacy_id_count"][~allowed] == 0).all()
 
 
-def test_sieve_packed_wide(device):
+@pytest.mark.parametrize("key_format", [4, 5], ids=["packed-wide", "packed64"])
+def test_sieve_packed_wide(device, key_format):
     """P = 1e7 (bucket + partition bits > 31): PACKED_WIDE records, 8-byte
     fix-up keys, rand_shift > 32 (the threshold is a multiple of the masked
     hash grain)."""
@@ -117,13 +118,13 @@ def test_sieve_packed_wide(device):
     pid = rng.integers(0, U, n)
     pk = np.minimum(rng.zipf(1.1, n) - 1, P - 1).astype(np.int64)
     val = np.clip(rng.lognormal(1.0, 1.0, n), 0, 20)
-    plan = X.bound_plan(n, U, P, spec, sieve=4096)
-    assert plan.key_format == N.KEYS_PACKED_WIDE and plan.rand_shift > 32 and plan.sieve == 4096
+    plan = X.bound_plan(n, U, P, spec, sieve=4096, key_format=key_format)
+    assert plan.key_format == key_format and plan.rand_shift > 32 and plan.sieve == 4096
     seed = 4242
     want = _want(pid, pk, val, U, P, spec, seed)
     scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
     for sieve in (64, 4096, 32768):
-        _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve), want, scale)
+        _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve, key_format=key_format), want, scale)
 
 
 def test_sieve_c3_shape_slice(device):
@@ -206,8 +207,9 @@ def test_sieve_every_row_a_candidate(device, threads):
     assert ws.stats()["rows_partitioned"] == n
 
 
+@pytest.mark.parametrize("key_format", [0, 5], ids=["auto", "packed64"])
 @pytest.mark.parametrize("sieve", [-1, 4096])
-def test_malformed_records_are_flagged_not_read(device, sieve, monkeypatch):
+def test_malformed_records_are_flagged_not_read(device, sieve, key_format, monkeypatch):
     """PDP_DEBUG_CORRUPT_RECORDS overwrites bucket 0's level-2 records with
     the all-ones partition (>= P) and bucket 1's with an out-of-range row: the
     bucket kernel sets the error word (bound_and_reduce raises) instead of
@@ -223,10 +225,10 @@ def test_malformed_records_are_flagged_not_read(device, sieve, monkeypatch):
     pid, pk, val = _gen(1, n, U, P, spec.value_kind)
     monkeypatch.delenv("PIPELINEDP_AMD_TEST_HOOKS", raising=False)
     with pytest.raises(RuntimeError, match="test hook"):  # rejected outside test mode
-        _run(device, pid, pk, val, U, P, spec, 5, sieve)
+        _run(device, pid, pk, val, U, P, spec, 5, sieve, key_format=key_format)
     monkeypatch.setenv("PIPELINEDP_AMD_TEST_HOOKS", "1")
     with pytest.raises(ValueError, match="outside the dense key range"):
-        _run(device, pid, pk, val, U, P, spec, 5, sieve)
+        _run(device, pid, pk, val, U, P, spec, 5, sieve, key_format=key_format)
     torch.cuda.synchronize()  # the device is still healthy
-    ok = _run(device, pid, pk, val, U, P, base, 5, sieve)
+    ok = _run(device, pid, pk, val, U, P, base, 5, sieve, key_format=key_format)
     assert ok["privacy_id_count"].sum() > 0
