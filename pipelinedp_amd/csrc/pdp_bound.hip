@@ -2220,8 +2220,17 @@ __device__ __forceinline__ void stream_bucket(const K* __restrict__ keys, const 
   }
 }
 
+// blockIdx -> work index with each XCD (blockIdx % 8) owning one contiguous
+// block: XCD x gets q + (x < rem) indices starting at x * q + min(x, rem).
+// A bijection on [0, G) for any G; a speed hint only.
+__device__ __forceinline__ int64_t xcd_major(int64_t id, int64_t G) {
+  const int64_t q = G >> 3, rem = G & 7, x = id & 7, j = id >> 3;
+  return x * q + (x < rem ? x : rem) + j;
+}
+
 struct PairRecords {  // PDP_MERGE_RANGES output of the bucket kernel
-  unsigned* runs;                // [n_buckets][n_ranges + 1] run starts within the bucket block
+  unsigned* runs;                // [n_ranges + 1][run_stride] run starts within the bucket block (range-major)
+  int64_t run_stride;            // buckets_out: one column per output bucket
   unsigned long long* key;       // (partition << 32) | count
   double* f0;                    // sum (int64 bits with PDP_SUM_INT)
   double* f1;                    // normalized sum
@@ -2265,7 +2274,10 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
 #endif
   const int64_t S = (int64_t)1 << kp.bucket_bits;
   const int l0 = kp.l0;
-  const int64_t b = blockIdx.x;
+  // XCD-aware bucket order: workgroups are dispatched round-robin over the 8
+  // XCDs (blockIdx % 8), so XCD x takes one contiguous block of buckets and
+  // its writes to the range-major run table (and the records) share L2 lines
+  const int64_t b = xcd_major(blockIdx.x, gridDim.x);
   // threshold sieve: a privacy id of this bucket with fewer than l0
   // candidate pairs (its sketch not full; `sketch` = false: every id) may
   // have kept pairs among rows this launch did not see; mark it in the
@@ -2297,8 +2309,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   // their privacy ids unresolved
   if ((!kp.sieve_mark || unres_prev != nullptr) && offsets[b] == offsets[b + 1]) {  // block-uniform
     if (RANGES) {
-      unsigned* const run0 = rec.runs + b * (kp.n_ranges + 1);
-      for (int t = threadIdx.x; t <= kp.n_ranges; t += blockDim.x) run0[t] = 0;
+      for (int t = threadIdx.x; t <= kp.n_ranges; t += blockDim.x) rec.runs[t * rec.run_stride + b] = 0;
     }
     if (kp.sieve_mark) mark(false);
     return;
@@ -2325,7 +2336,7 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   // high half of its sketch maximum (b1_candidate)}
   uint2* hpid = (uint2*)((unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap);
   for (int64_t t = threadIdx.x; t < S; t += blockDim.x)
-    hpid[t] = make_uint2(pid_hash(kp.seed, ((int64_t)blockIdx.x << kp.bucket_bits) | t), 0xFFFFFFFFu);
+    hpid[t] = make_uint2(pid_hash(kp.seed, (b << kp.bucket_bits) | t), 0xFFFFFFFFu);
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
     sk[t] = kEmpty;
     cnt[t] = 0;
@@ -2495,7 +2506,6 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   }
   PDP_PHASE(4);
   const void* const b3_value = (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) ? nullptr : value;
-  unsigned* run = nullptr;
   if (RANGES) {
     // B3a: kept pairs per partition range -> this bucket's run starts
     for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
@@ -2507,12 +2517,11 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
     const unsigned h = threadIdx.x < kp.n_ranges ? rh[threadIdx.x] : 0u;  // n_ranges <= blockDim
     unsigned total;
     const unsigned ex = block_excl_scan(h, wsum, &total);
-    run = rec.runs + b * (kp.n_ranges + 1);
     if (threadIdx.x < kp.n_ranges) {
-      run[threadIdx.x] = ex;
+      rec.runs[threadIdx.x * rec.run_stride + b] = ex;
       rcur[threadIdx.x] = ex;
     }
-    if (threadIdx.x == 0) run[kp.n_ranges] = total;
+    if (threadIdx.x == 0) rec.runs[kp.n_ranges * rec.run_stride + b] = total;
     __syncthreads();
   }
   // B3: merge every kept pair into its partition (RANGES: emit a pair record)
@@ -2841,12 +2850,12 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
   __shared__ unsigned wsum[kRangeThreads / 64 + 1];
   __shared__ unsigned s_base;
   const int r = blockIdx.x;
-  const int64_t stride = kp.n_ranges + 1;
+  const int64_t stride = kp.n_buckets;  // range-major: row r is contiguous over buckets
   const int64_t n_buckets = last_ids != nullptr && *last_ids == 0u ? kp.n_buckets - last_buckets : kp.n_buckets;
   auto len_of = [&](int64_t b) -> unsigned {
     if (b >= n_buckets) return 0u;
-    const unsigned* run = runs + b * stride + r;
-    return run[1] - run[0];
+    const unsigned* run = runs + r * stride + b;
+    return run[stride] - run[0];
   };
   unsigned total = 0;
   for (int64_t c = 0; c < n_buckets; c += blockDim.x) {
@@ -2930,9 +2939,9 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecor
     unsigned len = 0;
     if (threadIdx.x < nb) {
       const int64_t b = bb + threadIdx.x;
-      const unsigned* run = rec.runs + b * (kp.n_ranges + 1) + r;
+      const unsigned* run = rec.runs + r * rec.run_stride + b;
       const unsigned s = run[0];
-      len = run[1] - s;
+      len = run[rec.run_stride] - s;
       start[threadIdx.x] = (unsigned long long)(b * n_slots + s);
     }
     unsigned total;
@@ -3029,9 +3038,9 @@ __device__ __forceinline__ void item_rounds(const KP& kp, const PairRecords& rec
     unsigned len = 0;
     if (threadIdx.x < nb) {
       const int64_t b = bb + threadIdx.x;
-      const unsigned* run = rec.runs + b * (kp.n_ranges + 1) + r;
+      const unsigned* run = rec.runs + r * rec.run_stride + b;
       const unsigned s0 = run[0];
-      len = run[1] - s0;
+      len = run[rec.run_stride] - s0;
       start[threadIdx.x] = (unsigned long long)(b * n_slots + s0);
     }
     unsigned total;
@@ -3464,10 +3473,11 @@ int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void
   return PDP_OK;
 }
 
-PairRecords pair_records(char* ws, const Ws& w) {
+PairRecords pair_records(char* ws, const Ws& w, const Plan& p) {
   PairRecords rec{};
   if (w.runs) {
     rec.runs = (unsigned*)(ws + w.runs);
+    rec.run_stride = p.buckets_out;
     rec.key = (unsigned long long*)(ws + w.rec_key);
     rec.f0 = w.rec_f0 ? (double*)(ws + w.rec_f0) : nullptr;
     rec.f1 = w.rec_f1 ? (double*)(ws + w.rec_f1) : nullptr;
@@ -3490,7 +3500,7 @@ template <int VK, bool KA>
 int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
                    const uint8_t* allowed, const void* value, const pdp_partition_accumulators& acc, char* ws,
                    const Ws& w) {
-  const PairRecords rec = pair_records(ws, w);
+  const PairRecords rec = pair_records(ws, w, p);
   unsigned long long* fix_rec = (unsigned long long*)(ws + w.fix_rec);  // level-1 blocks are dead
   Marks m1{w.unres_bits ? (unsigned*)(ws + w.unres_bits) : nullptr,
            w.unres_list ? (unsigned*)(ws + w.unres_list) : nullptr, w.sctl ? (unsigned*)(ws + w.sctl) : nullptr,
@@ -3531,7 +3541,7 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     kf.sieve_mark = mark;
     kf.sieve_emit = 0;
     PairRecords fr = rec;
-    fr.runs += seg * p.n_buckets * (p.n_ranges + 1);
+    fr.runs += seg * p.n_buckets;  // column offset (range-major table)
     fr.key += seg * p.n_buckets * n_slots;
     if (fr.f0) fr.f0 += seg * p.n_buckets * n_slots;
     if (fr.f1) fr.f1 += seg * p.n_buckets * n_slots;
@@ -3581,7 +3591,7 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
                  const pdp_partition_accumulators& acc) {
   KP kp = kp0;
   kp.n_buckets = p.buckets_out;
-  const PairRecords rec = pair_records(ws, w);
+  const PairRecords rec = pair_records(ws, w, p);
   unsigned* err = (unsigned*)(ws + w.err);
   {
     PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_range_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
