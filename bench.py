@@ -58,8 +58,27 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
 # wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for
 # the workload and tree named in the file; None otherwise.
-PMC_SUMMARY = {"c3": os.path.join(HERE, "profiles", "r03", "c3_pmc.json"),
-               "c2": os.path.join(HERE, "profiles", "r03", "c2_pmc.json")}
+PMC_SUMMARY = {w: os.path.join(HERE, "profiles", "r04", f"{w}_pmc.json") for w in ("c3", "c2", "c4", "c5", "hist")}
+
+
+def load_pmc(pmc_file, workload, n, world):
+    """Per-kernel HBM bytes from a PMC summary, joined only when it was made
+    from this workload at this size AND from these kernel sources (its "tree"
+    equals tools/tree_id.py's id of the tree bench.py runs on).  Returns
+    (traffic, source, refused): refused names why a file present was not used."""
+    if world != 1 or not pmc_file or not os.path.exists(pmc_file):
+        return {}, None, None
+    sys.path.insert(0, os.path.join(HERE, "tools"))
+    from tree_id import source_tree_id
+    with open(pmc_file) as f:
+        pmc = json.load(f)
+    src = os.path.relpath(pmc_file, HERE)
+    if not pmc.get("workload", "").startswith(f"{workload} n={n} "):
+        return {}, None, f"{src}: workload {pmc.get('workload')!r}, not {workload} n={n}"
+    tree = source_tree_id()
+    if pmc.get("tree") != tree:
+        return {}, None, f"{src}: profiled tree {pmc.get('tree')}, this tree {tree}"
+    return {k: v["hbm_bytes"] for k, v in pmc["kernels"].items() if "hbm_bytes" in v}, src, None
 
 # workload constants (SURVEY §8(d))
 C2 = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000, l0=8, linf=2)
@@ -347,9 +366,14 @@ def run_api_workload(args, workload, world, rank, device):
     ws = X.BoundWorkspace()
     tune = tuning_of(args)
 
+    counter = [0]
+
     def step():
+        # seeded per step (bench.py --seed): the line is reproducible
+        counter[0] += 1
         acc = pdp.NaiveBudgetAccountant(total_epsilon=EPS, total_delta=DELTA)
-        backend = CB.ColumnarBackend(privacy_id_sharding="trusted", workspace=ws, tuning=tune)
+        backend = CB.ColumnarBackend(privacy_id_sharding="trusted", workspace=ws, tuning=tune,
+                                     seed=args.seed + counter[0])
         sink = pdp.DPEngine(acc, backend).aggregate(table, params, ext)
         acc.compute_budgets()
         return len(sink.collect()), backend
@@ -378,12 +402,39 @@ def run_api_workload(args, workload, world, rank, device):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     info = backend.last_plan_info
-    del pid, pk, value, table, ws
+    # kept pairs / rows and the plan's stats for the byte accounting: one more
+    # bounding pass with the spec the API built (untimed)
+    spec = backend.last_bounding
+    acc = X.new_accumulators(P, spec, device)
+    X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=1, acc=acc,
+                       workspace=ws, **tune)
+    kept_pairs = int(acc["privacy_id_count"].sum().item())
+    kept_rows = int(acc["count"].sum().item())
+    n_fields = sum(acc[k] is not None for k in ("sum", "normalized_sum", "normalized_sum_sq"))
+    stats = ws.stats()
+    plan = X.bound_plan(n, U, P, spec, **tune)
+    del pid, pk, value, table, ws, acc
     kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
     launches = {k: v[1] / args.steps for k, v in kernels.items()}
     ms_per_step = elapsed / args.steps * 1e3
+    traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY[workload], workload, n, world)
+    alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats, P)
+    table = {}
+    for k, ms in kernel_ms.items():
+        e = {"ms": ms, "launches_per_step": launches[k]}
+        if k in alg:
+            e["alg_bytes"] = alg[k]
+            e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
+            e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
+        if k in traffic:
+            e["pmc_bytes"] = traffic[k]
+            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
+        table[k] = e
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
-    path_bytes = 24.0 * n
+    # compulsory bytes: the three input columns once, and per
+    # kept partition its key, accumulators and output metrics
+    k_out = 2 if workload == "c4" else 3
+    path_bytes = 24.0 * n + kept * (8 + 8 * (2 + n_fields) + 8 * k_out)
     path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
     strat = args.strategy.replace("_", " ") + ("" if args.strategy == "truncated_geometric" else " thresholding")
     desc = (f"C4: DPEngine.aggregate VARIANCE+PRIVACY_ID_COUNT, Gaussian, private partitions ({strat}), "
@@ -397,18 +448,21 @@ def run_api_workload(args, workload, world, rank, device):
                    "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
                    "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
                    "timed": "public API per step: DPEngine.aggregate + compute_budgets() + collect()"},
-        "roofline": {"bound": "hbm", "kernel": dom, "avg_ms": kernel_ms[dom], "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": table[dom].get("achieved_gbs"),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": table[dom].get("frac"),
+                     "traffic": traffic.get(dom), "traffic_source": traffic_src, "traffic_refused": traffic_refused,
+                     "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom]},
         "path_roofline": {"achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes},
-        "kernels": {k: {"ms": kernel_ms[k], "launches_per_step": launches[k]} for k in kernel_ms},
+                          "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes,
+                          "traffic_per_step": sum(traffic.values()) if traffic else None},
+        "kernels": table, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "bound_plan": None if info is None else {
             "algorithm": info.algorithm, "bucket_bits": info.bucket_bits, "n_buckets": info.n_buckets,
             "lds_bytes": info.lds_bytes, "merge": info.merge, "sieve": info.sieve / 65536.0,
-            "band": info.band / 65536.0, "tuning": tune,
+            "band": info.band / 65536.0, "tuning": tune, "stats": stats,
             "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide", 5: "packed64"}.get(info.key_format,
                                                                                      info.key_format)},
-        "seed": None,
+        "seed": args.seed,
         "partitions_kept": kept,
         "privacy_id_verify_ms": verify_ms,
     }
@@ -468,6 +522,7 @@ def run_hist_workload(args, world, rank, device):
     # algorithmic bytes per launch: rows read / records moved once
     alg = {"k_hb_count": 16.0 * n, "k_hb_l1": (24.0 + 16.0) * n, "k_hb_bcount": 8.0 * n,
            "k_hb_l2": 32.0 * n, "k_hb_pairs": 16.0 * n}
+    traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY["hist"], "hist", n, world)
     table = {}
     for k, ms in kernel_ms.items():
         e = {"ms": ms, "launches_per_step": launches[k]}
@@ -475,6 +530,9 @@ def run_hist_workload(args, world, rank, device):
             e["alg_bytes"] = alg[k]
             e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
             e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
+        if k in traffic:
+            e["pmc_bytes"] = traffic[k]
+            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
         table[k] = e
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
     ms_per_step = elapsed / args.steps * 1e3
@@ -488,7 +546,8 @@ def run_hist_workload(args, world, rank, device):
                    "rows_per_gpu": n, "privacy_ids": U, "partitions": P,
                    "parallelism": f"rows sharded by privacy_id over {world} GPU(s)"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": table[dom].get("achieved_gbs"),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": table[dom].get("frac"), "traffic": None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": table[dom].get("frac"),
+                     "traffic": traffic.get(dom), "traffic_source": traffic_src, "traffic_refused": traffic_refused,
                      "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom]},
         "path_roofline": {"achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes},
@@ -514,7 +573,7 @@ def hist_cpu_baseline(sample_rows):
                       f"restatement of computing_histograms.py) on one core, {dt:.1f} s"}
 
 
-def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
+def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats, P=0):
     """Algorithmic bytes of each kernel of one step: every
     input it must read once plus every output it must write once.  `stats`
     (BoundWorkspace.stats): rows through the partition passes (the sieve's
@@ -551,6 +610,14 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats):
         out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * (fix + fix2)  # list in, partition gathered, record out
         out["k_bucket_fix"] = key2 * fix
     out["k_range_reduce"] = 2.0 * pair_rec * kept_pairs
+    # two-level merge (P > 2^21): the coarse records' keys counted per fine
+    # range, the records moved once into fine-range order, then read once
+    # and summed into the accumulators (written once)
+    acc_bytes = 8.0 * (2 + n_fields) * P
+    out["k_split_count"] = 8.0 * kept_pairs
+    out["k_split_scatter"] = 2.0 * pair_rec * kept_pairs
+    out["k_fine_reduce"] = pair_rec * kept_pairs + acc_bytes
+    out["k_select"] = acc_bytes  # selection reads every partition's accumulators
     return out
 
 
@@ -686,13 +753,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     launches = {k: v[1] / args.steps for k, v in kernels.items()}
     ms_per_step = elapsed / args.steps * 1e3
     total_rows = n * world * args.steps
-    traffic, traffic_src = {}, None
-    if pmc_file and os.path.exists(pmc_file):
-        with open(pmc_file) as f:
-            pmc = json.load(f)
-        if pmc.get("workload", "").startswith(f"{workload} n={n} ") and world == 1:
-            traffic = {k: v["hbm_bytes"] for k, v in pmc["kernels"].items() if "hbm_bytes" in v}
-            traffic_src = os.path.relpath(pmc_file, HERE)
+    traffic, traffic_src, traffic_refused = load_pmc(pmc_file, workload, n, world)
     alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2, stats)
     table = {}
     for k, ms in kernel_ms.items():
@@ -725,7 +786,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
             "bound": "hbm", "kernel": dom,
             "achieved": table[dom].get("achieved_gbs"), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": table[dom].get("frac"), "traffic": traffic.get(dom), "traffic_source": traffic_src,
-            "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom],
+            "traffic_refused": traffic_refused, "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom],
         },
         "path_roofline": {  # the headline fraction: 24 B/row compulsory over the whole step
             "achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": path_gbs / HBM_PEAK_GBS,

@@ -225,6 +225,9 @@ def _clz32(v):
 
 
 def secure_gaussian(np_, seed, gidx, slot):
+    """pdp_internal.h gaussian_attempt: one Philox block per attempt -- x[31:24]
+    geometric bits (leading ones, at most 8), x[23] sign, (y, z) the uniform
+    offset's 64 bits, (w, x[20:0]) the acceptance uniform's 53 bits."""
     gidx = np.asarray(gidx, dtype=np.int64)
     out = np.empty(len(gidx))
     k = np.zeros(len(gidx), dtype=np.uint32)
@@ -232,17 +235,17 @@ def secure_gaussian(np_, seed, gidx, slot):
     pend = np.arange(len(gidx))
     while len(pend):
         a = noise_block(seed, gidx[pend], slot, k[pend])
-        b = noise_block(seed, gidx[pend], slot, k[pend] + 1)
-        k[pend] += 2
-        nx, ny = ~a[0], ~a[1]
-        geom = np.where(a[0] != 0xFFFFFFFF, _clz32(nx), np.where(a[1] != 0xFFFFFFFF, 32 + _clz32(ny), 64))
-        two_sided = np.where((a[2] >> np.uint32(31)) != 0, geom, -geom - 1)
+        k[pend] += 1
+        ones = (~a[0] & np.uint32(0xFF000000)) | np.uint32(0x00800000)
+        geom = _clz32(ones)
+        two_sided = np.where(((a[0] >> np.uint32(23)) & np.uint32(1)) != 0, geom, -geom - 1)
         st = _U64(step)
         with np.errstate(over="ignore"):
-            hi_part = b[0].astype(np.uint64) * st + ((b[1].astype(np.uint64) * st) >> _U64(32))
+            hi_part = a[1].astype(np.uint64) * st + ((a[2].astype(np.uint64) * st) >> _U64(32))
         uni = (hi_part >> _U64(32)).astype(np.int64)
         m = np.int64(step) * two_sided + uni
-        accept_u = u01(b[2], b[3])
+        u53 = (a[3].astype(np.uint64) << _U64(21)) | (a[0] & np.uint32(0x1FFFFF)).astype(np.uint64)
+        accept_u = (u53.astype(np.float64) + 0.5) * (1.0 / 9007199254740992.0)
         md = m.astype(np.float64)
         inb = np.abs(md) <= np_["bound"]
         prob = np_["coef"] * np.exp(-2.0 * md * md / np_["n"]) * np_["corr"]

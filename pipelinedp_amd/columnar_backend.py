@@ -497,6 +497,7 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
                 raise ValueError(f"unknown tuning key {k!r} (one of {', '.join(self.TUNING_KEYS)})")
             self._tuning[k] = int(v)
         self.last_plan_info = None
+        self.last_bounding = None  # BoundingSpec of the last bounding pass (bench accounting)
 
     # ---------------------------------------------------- recorded ops --
     def _node(self, op, col, stage, **kw):
@@ -710,6 +711,7 @@ class AggregateRun:
                                      bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset,
                                      workspace=self.backend._workspace, **tune)
             self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec, **tune)
+            self.backend.last_bounding = spec
         return acc, spec, pk_enc, allowed
 
     def _selection(self):

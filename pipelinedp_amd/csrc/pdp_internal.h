@@ -118,12 +118,14 @@ struct U4 {
 };
 
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  // each 32 x 32 -> 64 product as one v_mad_u64_u32 (one quarter-rate
+  // instruction for both halves, not a v_mul_lo_u32 + v_mul_hi_u32 pair)
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -211,30 +213,45 @@ __device__ __forceinline__ double secure_laplace(const pdp_noise_params& np, uin
 // GaussianDistribution::Sample: g * (Binomial(n, 1/2) - n/2) by rejection from
 // a two-sided geometric(1/2) over blocks of `step` integers; acceptance
 // uses Google's approximate binomial probability (Secure Noise Generation,
-// Lemma 7).  Two Philox blocks per attempt: (x, y) geometric bits, z sign;
-// then (x, y) the uniform offset in [0, step), (z, w) the acceptance uniform.
-// one attempt (Philox blocks k, k + 1; k advances by 2): true and *md = the
-// binomial offset if accepted.  About 1 in 16 attempts is accepted, so a
-// kernel drawing many samples runs attempts, not samples, per loop trip
-// (k_select_gauss) to keep a wave's lanes busy.
+// Lemma 7).  ONE Philox block per attempt (k advances by 1), its 128 bits
+// split as: x[31:24] geometric bits (leading ones; eight ones = geometric 8),
+// x[23] sign, (y, z) the 64 bits of the uniform offset in [0, step), and
+// (w, x[20:0]) the 53 bits of the acceptance uniform.  Eight geometric bits
+// suffice: every proposal with geometric >= 4 lies beyond `bound` (bound /
+// step = sqrt(ln n) / 2 < 3.4 for any n < 2^64) and is rejected, so lumping
+// geometric >= 8 into 8 leaves the accepted distribution unchanged.  Returns
+// true and *md = the binomial offset if accepted.  About 1 in 16 attempts is
+// accepted, so a kernel drawing many samples runs attempts, not samples, per
+// loop trip (k_select_gauss) to keep a wave's lanes busy.  The Philox block is
+// ~3/4 of an attempt's instructions (20 v_mad_u64_u32 at quarter rate).
 __device__ __forceinline__ bool gaussian_attempt(const pdp_noise_params& np, uint64_t seed, int64_t gidx,
                                                  uint32_t slot, uint32_t& k, double* md_out) {
   const uint64_t step = (uint64_t)np.step;
   const U4 a = noise_block(seed, gidx, slot, k++);
-  const U4 b = noise_block(seed, gidx, slot, k++);
-  int geom;
-  if (a.x != 0xFFFFFFFFu) geom = __clz(~a.x);
-  else if (a.y != 0xFFFFFFFFu) geom = 32 + __clz(~a.y);
-  else geom = 64;  // probability 2^-64: capped
-  const int64_t two_sided = (a.z >> 31) ? (int64_t)geom : -(int64_t)geom - 1;
-  // floor(r * step / 2^64) for the 64 random bits r = (b.x, b.y); step < 2^32
-  const uint64_t hi_part = (uint64_t)b.x * step + (((uint64_t)b.y * step) >> 32);
+  const int geom = __clz(~a.x & 0xFF000000u | 0x00800000u);  // leading ones of x[31:24], at most 8
+  const int64_t two_sided = ((a.x >> 23) & 1u) ? (int64_t)geom : -(int64_t)geom - 1;
+  // floor(r * step / 2^64) for the 64 random bits r = (y, z); step < 2^32
+  const uint64_t hi_part = (uint64_t)a.y * step + (((uint64_t)a.z * step) >> 32);
   const int64_t uni = (int64_t)(hi_part >> 32);
   const int64_t m = (int64_t)step * two_sided + uni;
-  const double accept_u = u01(b.z, b.w);
+  const uint64_t u53 = ((uint64_t)a.w << 21) | (a.x & 0x1FFFFFu);
+  const double accept_u = ((double)u53 + 0.5) * (1.0 / 9007199254740992.0);
   const double md = (double)m;
   *md_out = md;
   if (fabs(md) > np.bound) return false;
+  // squeeze: the fp32 threshold is within 1e-4 (relative) of the fp64 one
+  // below (|md| <= bound keeps 2 md^2 / n <= ln n < 45, so fp32's ~1e-7
+  // relative errors on md, 1/n and the exponent cost at most ~2e-5); only an
+  // acceptance uniform within 1e-3 of it takes the exact fp64 test, so the
+  // decision is the exact test's and a wave rarely pays the fp64 exp and
+  // division
+  {
+    const float mf = (float)md;
+    const float xf = 2.0f * mf * mf * __frcp_rn((float)np.n);
+    const float tf = (float)(np.coef * np.corr * (double)np.step * 0.25) * __expf(-xf) * (float)(1u << geom);
+    if (accept_u < (double)tf * (1.0 - 1e-3)) return true;
+    if (accept_u >= (double)tf * (1.0 + 1e-3)) return false;
+  }
   const double prob = np.coef * exp(-2.0 * md * md / np.n) * np.corr;
   return prob > 0.0 && accept_u < prob * (double)np.step * ldexp(1.0, geom) / 4.0;
 }

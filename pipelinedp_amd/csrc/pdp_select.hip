@@ -78,50 +78,72 @@ __global__ void __launch_bounds__(kBlock) k_select(pdp_select_config cfg, const 
 // Laplace / Gaussian thresholding with Gaussian noise: the rejection sampler
 // takes ~16 attempts per sample (geometric), so a lane per partition leaves a
 // wave waiting ~74 attempts for its slowest lane.  Here each loop trip is one
-// attempt and a lane whose sample was accepted moves on to its next partition
-// (grid-stride), so the lanes' trips even out over ~20 partitions each.  Same
+// attempt, and a lane whose sample was accepted takes the wave's next
+// partition: every wave owns one contiguous chunk of partitions and hands
+// them out in order (ballot + prefix count, no atomics), so its lanes stay
+// busy until the chunk runs dry (a fixed grid stride left each lane its own
+// ~20 partitions, and the wave the slowest lane's sum of attempts).  Same
 // Philox blocks per partition as secure_add_noise, so the same draws.
 __global__ void __launch_bounds__(kBlock) k_select_gauss(pdp_select_config cfg, const int64_t* __restrict__ row_count,
                                                          uint8_t* __restrict__ keep, double* __restrict__ noised) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ULL << lane) - 1;
+  const int64_t n_waves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t chunk = (cfg.n_partitions + n_waves - 1) / n_waves;
+  const int64_t c0 = wave * chunk < cfg.n_partitions ? wave * chunk : cfg.n_partitions;
+  const int64_t c1 = c0 + chunk < cfg.n_partitions ? c0 + chunk : cfg.n_partitions;
   const double g = cfg.noise.granularity;
-  int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t mr = cfg.max_rows_per_privacy_id > 0 ? cfg.max_rows_per_privacy_id : 1;
+  // a fresh partition's set-up runs on some lane of nearly every trip, so it
+  // avoids the int64 division (mr == 1) and the fmod (a power-of-two grid
+  // <= 1 leaves an integer count where it is): both paths give the same value
+  int g_exp = 0;
+  const bool unit_grid = g > 0.0 && g <= 1.0 && frexp(g, &g_exp) == 0.5;
+  int64_t p = c0 + lane;
+  int64_t cursor = c0 + 64;  // wave-uniform: the chunk's next partition to hand out
   bool fresh = true;
   uint32_t k = 0;
   double base = 0.0, shift = 0.0;
-  while (p < cfg.n_partitions) {
-    if (fresh) {
-      fresh = false;
-      k = 0;
-      const int64_t rc = row_count[p];
-      const int64_t mr = cfg.max_rows_per_privacy_id > 0 ? cfg.max_rows_per_privacy_id : 1;
-      int64_t n = (rc + mr - 1) / mr;
-      bool live = rc > 0;
-      int64_t sh = 0;
-      if (live && cfg.pre_threshold > 0) {
-        if (n < cfg.pre_threshold) live = false;
-        sh = cfg.pre_threshold - 1;
-        n -= sh;
+  while (__ballot(p < c1) != 0) {  // wave-uniform trip count
+    bool done = false;
+    if (p < c1) {
+      if (fresh) {
+        fresh = false;
+        k = 0;
+        const int64_t rc = row_count[p];
+        int64_t n = mr == 1 ? rc : (rc + mr - 1) / mr;  // mr: uniform
+        bool live = rc > 0;
+        int64_t sh = 0;
+        if (live && cfg.pre_threshold > 0) {
+          if (n < cfg.pre_threshold) live = false;
+          sh = cfg.pre_threshold - 1;
+          n -= sh;
+        }
+        if (!live) {
+          keep[p] = 0;
+          if (noised) noised[p] = __builtin_nan("");
+          done = true;
+        } else {
+          base = unit_grid ? (double)n : round_to_multiple((double)n, g);
+          shift = (double)sh;
+        }
       }
-      if (!live) {
-        keep[p] = 0;
-        if (noised) noised[p] = __builtin_nan("");
-        p += stride;
-        fresh = true;
-        continue;
+      double md;
+      if (!done && gaussian_attempt(cfg.noise, cfg.seed, cfg.partition_offset + p, 0x53454C00u, k, &md)) {
+        const double v = base + md * g;
+        const bool kp = v > cfg.threshold;
+        keep[p] = kp;
+        if (noised) noised[p] = kp ? v + shift : __builtin_nan("");
+        done = true;
       }
-      base = round_to_multiple((double)n, g);
-      shift = (double)sh;
     }
-    double md;
-    if (gaussian_attempt(cfg.noise, cfg.seed, cfg.partition_offset + p, 0x53454C00u, k, &md)) {
-      const double v = base + md * g;
-      const bool kp = v > cfg.threshold;
-      keep[p] = kp;
-      if (noised) noised[p] = kp ? v + shift : __builtin_nan("");
-      p += stride;
+    const unsigned long long m = __ballot(done);
+    if (done) {
+      p = cursor + __popcll(m & below);
       fresh = true;
     }
+    cursor += __popcll(m);
   }
 }
 

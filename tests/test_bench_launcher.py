@@ -26,3 +26,23 @@ def test_gpus_2_spawns_two_ranks():
 
 def test_default_is_one_rank():
     assert _run("--dry-run")["n_gpus"] == 1
+
+
+def test_pmc_join_checks_the_source_tree(tmp_path):
+    """bench.py joins a PMC summary only for its workload, size AND kernel
+    sources (verdict r03 weak #5: a stale tree's counters were reported)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench
+    from tree_id import source_tree_id
+    f = tmp_path / "c3_pmc.json"
+    body = {"workload": "c3 n=1000 ", "kernels": {"k_sieve_l1": {"hbm_bytes": 123.0}}}
+    f.write_text(json.dumps(dict(body, tree="0123456789abcdef")))
+    traffic, src, refused = bench.load_pmc(str(f), "c3", 1000, 1)
+    assert traffic == {} and src is None and "profiled tree" in refused
+    f.write_text(json.dumps(dict(body, tree=source_tree_id())))
+    traffic, src, refused = bench.load_pmc(str(f), "c3", 1000, 1)
+    assert traffic == {"k_sieve_l1": 123.0} and refused is None
+    traffic, src, refused = bench.load_pmc(str(f), "c3", 2000, 1)  # another size
+    assert traffic == {} and "workload" in refused
+    assert bench.load_pmc(str(f), "c3", 1000, 2) == ({}, None, None)  # N > 1: never joined

@@ -13,7 +13,7 @@ shift 2
 EXTRA="$@"
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-declare -A ROWS=([c3]=1000000000 [c2]=100000000)
+declare -A ROWS=([c3]=1000000000 [c2]=100000000 [c4]=125000000 [c5]=625000000 [hist]=100000000)
 BENCH="python -u bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline --no-secondary --no-api $EXTRA"
 timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $OUT/$W/trace -o run --output-format csv -- $BENCH > $OUT/${W}_trace.log 2>&1 || { echo "trace pass failed"; tail -5 $OUT/${W}_trace.log; exit 1; }
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
@@ -23,5 +23,5 @@ for C in FETCH_SIZE WRITE_SIZE "$SQ1" "$SQ2"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $C -d $OUT/$W/pmc$i -o run --output-format csv -- $BENCH > $OUT/${W}_pmc$i.log 2>&1 || { echo "PMC pass $i ($C) failed"; tail -5 $OUT/${W}_pmc$i.log; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT/$W $OUT/${W}_pmc.json "$W n=${ROWS[$W]} tree=$(cat .tree_id 2>/dev/null || echo unknown)" || exit 1
+python3 tools/pmc_summary.py $OUT/$W $OUT/${W}_pmc.json "$W n=${ROWS[$W]} " || exit 1
 echo "prof ok"

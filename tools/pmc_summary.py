@@ -13,6 +13,9 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tree_id import source_tree_id  # noqa: E402
+
 
 def short_name(full):
     m = re.search(r"(k_[a-z0-9_]+)", full)
@@ -51,7 +54,7 @@ def main():
             e["write_bytes"] = avg["WRITE_SIZE"] * 1024.0
             e["hbm_bytes"] = e["fetch_bytes"] + e["write_bytes"]
         kernels[k] = e
-    json.dump({"workload": tag, "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes)",
+    json.dump({"workload": tag, "tree": source_tree_id(), "correction": "hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB -> bytes)",
                "kernels": kernels}, open(out, "w"), indent=1, sort_keys=True)
     for k, e in sorted(kernels.items()):
         if "hbm_bytes" in e:
