@@ -110,6 +110,8 @@ def parse():
                     help="threshold sieve t * 2^16 (0 auto, -1 off; pdp_bound_config.sieve)")
     ap.add_argument("--sieve-threads", type=int, default=0,
                     help="the sieve's level-1 workgroup: 0 auto, 512 or 1024 (pdp_bound_config.sieve_threads)")
+    ap.add_argument("--bucket-threads", type=int, default=0,
+                    help="the bucket kernel's workgroup: 0 auto, 512 or 1024 (pdp_bound_config.bucket_threads)")
     ap.add_argument("--merge", type=int, default=0, help="PDP_MERGE_* (0 auto, 1 atomic, 2 ranges)")
     ap.add_argument("--seed", type=int, default=20261017,
                     help="sampling seed base: step i uses seed + i, so a run is reproducible (c2 / c3)")
@@ -317,7 +319,7 @@ def verify_sharding(ids, world, rank, U):
 def tuning_of(args):
     """The bench's data-movement knobs (identical results) as ColumnarBackend tuning."""
     t = dict(key_format=args.key_format, sieve=args.sieve, sieve_band=args.sieve_band,
-             sieve_threads=args.sieve_threads, merge=args.merge)
+             sieve_threads=args.sieve_threads, bucket_threads=args.bucket_threads, merge=args.merge)
     return {k: v for k, v in t.items() if v}
 
 
@@ -460,6 +462,7 @@ def run_api_workload(args, workload, world, rank, device):
             "algorithm": info.algorithm, "bucket_bits": info.bucket_bits, "n_buckets": info.n_buckets,
             "lds_bytes": info.lds_bytes, "merge": info.merge, "sieve": info.sieve / 65536.0,
             "band": info.band / 65536.0, "tuning": tune, "stats": stats,
+            "bucket_threads": info.bucket_threads,
             "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide", 5: "packed64"}.get(info.key_format,
                                                                                      info.key_format)},
         "seed": args.seed,
@@ -799,7 +802,8 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                        "key_format": {1: "wide", 2: "compact", 3: "packed", 4: "packed_wide", 5: "packed64"}.get(
                            plan.key_format, plan.key_format),
                        "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0,
-                       "sieve_threads": plan.sieve_threads, "stats": stats},
+                       "sieve_threads": plan.sieve_threads, "bucket_threads": plan.bucket_threads,
+                       "stats": stats},
         "seed": args.seed,
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 11
+#define PDP_ABI_VERSION 12
 
 /* error codes */
 #define PDP_OK 0
@@ -89,6 +89,9 @@ typedef struct pdp_bound_config {
                                 for t <= 1/4), > 0 = on, < 0 = off (identical results) */
   int32_t sieve_threads;     /* the sieve's level-1 workgroup (identical results): 0 = auto (1024),
                                 1024, or 512 (two per CU, when its LDS fits) */
+  int32_t bucket_threads;    /* the bucket kernel's workgroup (identical results): 0 = auto (1024),
+                                1024, or 512 (buckets of half as many privacy ids, whose LDS lets two
+                                workgroups share a CU; needs <= 512 partition ranges) */
 } pdp_bound_config;
 
 /* bounds up to int32; above 256 (l0, linf) the pair-table algorithm runs, and
@@ -151,6 +154,7 @@ typedef struct pdp_bound_plan_info {
   int32_t sieve;       /* resolved threshold sieve, t = sieve / 2^16 (0 = off) */
   int32_t band;        /* resolved side band, t2 = band / 2^16 (0 = off) */
   int32_t sieve_threads; /* resolved sieve level-1 workgroup size (0 without the sieve) */
+  int32_t bucket_threads; /* resolved bucket-kernel workgroup size (BUCKETED) */
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 11
+ABI_VERSION = 12
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
@@ -97,6 +97,7 @@ class BoundConfig(ctypes.Structure):
         ("sieve", ctypes.c_int32),
         ("sieve_band", ctypes.c_int32),
         ("sieve_threads", ctypes.c_int32),
+        ("bucket_threads", ctypes.c_int32),
     ]
 
 
@@ -116,6 +117,7 @@ class BoundPlanInfo(ctypes.Structure):
         ("sieve", ctypes.c_int32),
         ("band", ctypes.c_int32),
         ("sieve_threads", ctypes.c_int32),
+        ("bucket_threads", ctypes.c_int32),
     ]
 
 

@@ -475,12 +475,12 @@ class ColumnarBackend(pipeline_backend.PipelineBackend):
         device workspace; by default each backend keeps its own across runs).
       tuning: data-movement knobs of the bounding kernels, all of which keep
         the results identical (pdp_bound_config: algorithm, merge,
-        key_format, sieve, sieve_band, sieve_threads); default {} = the
+        key_format, sieve, sieve_band, sieve_threads, bucket_threads); default {} = the
         library's plan.  The environment variable PIPELINEDP_AMD_TUNING
         ("sieve=16384,merge=1") supplies defaults for it.
     """
 
-    TUNING_KEYS = ("algorithm", "merge", "key_format", "sieve", "sieve_band", "sieve_threads")
+    TUNING_KEYS = ("algorithm", "merge", "key_format", "sieve", "sieve_band", "sieve_threads", "bucket_threads")
 
     def __init__(self, device=None, seed: Optional[int] = None, privacy_id_sharding: str = "verify",
                  workspace=None, tuning: Optional[dict] = None):

@@ -65,6 +65,10 @@ constexpr int kL2Runs = kL2GroupTiles * kStagesPerTile;  // level-1 runs per lev
 constexpr int kUnroll = 8;
 constexpr int kBucketThreads = 1024;
 constexpr int64_t kLdsBudget = 124 * 1024;  // per-pid state; + range scratch + wave queues <= 160 KiB
+// 512-thread bucket workgroups: per-pid state <= 56 KiB, so that with the
+// range scratch (<= 4 KiB at 512 ranges), 8 wave queues (12 KiB) and the pid
+// hashes two workgroups fit one CU's 160 KiB
+constexpr int64_t kLdsBudget2 = 56 * 1024;
 constexpr int kMinRandomBits = 24;
 constexpr int64_t kMaxBuckets = 36 * 1024;  // u32 histogram in 144 KiB of LDS
 constexpr int kMaxSupers = 128;   // destinations of a level-1 scatter
@@ -202,6 +206,7 @@ struct Plan {
   int64_t buckets_out;  // buckets of pair records: n_buckets, x2 with the sieve (fix-up after), x3 with the band
   int l2_mult;          // tile groups per level-2 workgroup (1 without the sieve)
   int sieve_threads;    // k_sieve_l1 workgroup: 1,024 or 512 threads (SieveShape)
+  int bucket_threads;   // k_bucket_bound workgroup: 1,024 or 512 threads (half-size buckets)
   int slot_bits;        // level-1 blocks per tile = 2^slot_bits (kStagesPerTile, or SieveShape::kSlots)
   int hist_u16;         // tile-local level 1 counts buckets in u16 halves (counts_tm / counts_tm2)
 };
@@ -216,7 +221,14 @@ Plan make_plan(const pdp_bound_config* c) {
   Plan p{};
   p.pk_bits = bits_for(c->n_partitions);
   const int64_t per_pid = per_pid_lds(c);
-  const int64_t max_pids = kLdsBudget / per_pid;
+  // the bucket kernel's workgroup: 512 threads (on request) only where the
+  // per-partition-range scan fits one thread per range
+  const int64_t n_ranges_est = (c->n_partitions + kRangeParts - 1) >> kRangeBits;
+  p.bucket_threads = c->bucket_threads == kBucketThreads / 2 &&
+                             (n_ranges_est <= kBucketThreads / 2 || n_ranges_est > kMaxRanges)
+                         ? kBucketThreads / 2
+                         : kBucketThreads;
+  const int64_t max_pids = (p.bucket_threads == kBucketThreads ? kLdsBudget : kLdsBudget2) / per_pid;
   int s = -1, s2 = 0;
   if (max_pids >= 16) {
     s = 0;
@@ -272,7 +284,7 @@ Plan make_plan(const pdp_bound_config* c) {
   }
   if (p.merge == PDP_MERGE_RANGES) {
     // per-bucket range histogram + cursors + block-scan scratch after the sketches
-    p.lds_bytes += (2 * (int64_t)p.n_ranges + kBucketThreads / 64 + 1) * 4;
+    p.lds_bytes += (2 * (int64_t)p.n_ranges + p.bucket_threads / 64 + 1) * 4;
   }
   // row records of the partition passes: u32 (sub-bucket, local pid,
   // partition) with bit 31 = dead when those fields fit (COMPACT); else the
@@ -383,7 +395,7 @@ Plan make_plan(const pdp_bound_config* c) {
     p.l2_mult = m < 1 ? 1 : (m > cap ? cap : m);
   }
   if (p.algorithm == PDP_ALGO_BUCKETED) {  // candidate queues (key + row) per wave + pid hashes
-    p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (kBucketThreads / 64) * kQueueCap * 12;
+    p.lds_bytes = ((p.lds_bytes + 7) & ~(int64_t)7) + (p.bucket_threads / 64) * kQueueCap * 12;
     p.lds_bytes += ((int64_t)8 << p.bucket_bits);  // {pid hash, sketch-maximum high half} per pid
   }
   if (p.merge == PDP_MERGE_RANGES) {
@@ -576,6 +588,8 @@ int validate(const pdp_bound_config* c) {
     return set_error(PDP_E_INVALID, "bad key_format");
   if (c->sieve_threads != 0 && c->sieve_threads != kSieveThreads2 && c->sieve_threads != kL1Threads)
     return set_error(PDP_E_INVALID, "sieve_threads must be 0, 512 or 1024");
+  if (c->bucket_threads != 0 && c->bucket_threads != kBucketThreads / 2 && c->bucket_threads != kBucketThreads)
+    return set_error(PDP_E_INVALID, "bucket_threads must be 0, 512 or 1024");
   if ((c->flags & PDP_DEBUG_CORRUPT_RECORDS) && !test_hooks_enabled())
     return set_error(PDP_E_INVALID, "PDP_DEBUG_CORRUPT_RECORDS is a test hook: set PIPELINEDP_AMD_TEST_HOOKS=1");
   if (pairs_mode(c)) return pairs_validate(c);
@@ -2325,16 +2339,17 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   unsigned* rh = cnt + n_slots;          // RANGES: [n_ranges] kept pairs per partition range
   unsigned* rcur = rh + kp.n_ranges;     //         [n_ranges] write cursors
   unsigned* wsum = rcur + kp.n_ranges;   //         block-scan scratch
-  unsigned* tail = RANGES ? wsum + kBucketThreads / 64 + 1 : rh;
+  const int n_waves = (int)(blockDim.x >> 6);  // 16 or 8 (Plan.bucket_threads)
+  unsigned* tail = RANGES ? wsum + n_waves + 1 : rh;
   // derived from smem by offset (not through an integer round trip) so the
   // compiler keeps the LDS address space and emits ds_* rather than flat_*
   unsigned long long* qbase = smem + (((const char*)tail - (const char*)smem) + 7) / 8;
   const int wave = threadIdx.x >> 6;
   const WaveQueue wq{qbase + wave * kQueueCap,
-                     (unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + wave * kQueueCap};
+                     (unsigned*)(qbase + n_waves * kQueueCap) + wave * kQueueCap};
   // per privacy id of the bucket, after the queues: {pid_hash (expand_key),
   // high half of its sketch maximum (b1_candidate)}
-  uint2* hpid = (uint2*)((unsigned*)(qbase + (kBucketThreads / 64) * kQueueCap) + (kBucketThreads / 64) * kQueueCap);
+  uint2* hpid = (uint2*)((unsigned*)(qbase + n_waves * kQueueCap) + n_waves * kQueueCap);
   for (int64_t t = threadIdx.x; t < S; t += blockDim.x)
     hpid[t] = make_uint2(pid_hash(kp.seed, (b << kp.bucket_bits) | t), 0xFFFFFFFFu);
   for (int64_t t = threadIdx.x; t < n_slots; t += blockDim.x) {
@@ -3467,7 +3482,8 @@ int launch_bucket_kernel(const KP& kp, const Plan& p, hipStream_t st, const void
                   (void*)&cand_idx, (void*)&unres_bits, (void*)&unres_list, (void*)&sctl,
                   (void*)&err,      (void*)&fix_rec,    (void*)&prev};
   PDP_PROF_BEGIN(name, st);
-  PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3(kBucketThreads), args, (size_t)p.lds_bytes, st));
+  PDP_HIP_CHECK(hipLaunchKernel(kern, dim3((unsigned)p.n_buckets), dim3((unsigned)p.bucket_threads), args,
+                                (size_t)p.lds_bytes, st));
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   return PDP_OK;
@@ -3984,6 +4000,7 @@ int pdp_bound_plan(const pdp_bound_config* cfg, pdp_bound_plan_info* info) {
   info->sieve = p.sieve;
   info->band = p.band;
   info->sieve_threads = p.sieve ? p.sieve_threads : 0;
+  info->bucket_threads = p.bucket_threads;
   return PDP_OK;
 }
 

@@ -201,7 +201,7 @@ def _acc_struct(acc) -> N.PartitionAccumulators:
 def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, seed: int,
                  row_offset: int = 0, algorithm: int = N.ALGO_AUTO,
                  merge: int = N.MERGE_AUTO, key_format: int = N.KEYS_AUTO, sieve: int = 0,
-                 sieve_band: int = 0, sieve_threads: int = 0) -> N.BoundConfig:
+                 sieve_band: int = 0, sieve_threads: int = 0, bucket_threads: int = 0) -> N.BoundConfig:
     c = N.BoundConfig()
     c.n_rows = int(n_rows)
     c.n_privacy_ids = int(n_privacy_ids)
@@ -225,16 +225,17 @@ def bound_config(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec, se
     c.sieve = int(sieve)
     c.sieve_band = int(sieve_band)
     c.sieve_threads = int(sieve_threads)
+    c.bucket_threads = int(bucket_threads)
     return c
 
 
 def bound_plan(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec,
                algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
                key_format: int = N.KEYS_AUTO, sieve: int = 0, sieve_band: int = 0,
-               sieve_threads: int = 0) -> N.BoundPlanInfo:
+               sieve_threads: int = 0, bucket_threads: int = 0) -> N.BoundPlanInfo:
     """Execution plan the library resolves for this shard (no device work)."""
     cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge, key_format, sieve,
-                       sieve_band, sieve_threads)
+                       sieve_band, sieve_threads, bucket_threads)
     info = N.BoundPlanInfo()
     N.check(N.lib().pdp_bound_plan(ctypes.byref(cfg), ctypes.byref(info)), "pdp_bound_plan")
     return info
@@ -274,7 +275,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                      check_keys: bool = True, timer: Optional["StageTimer"] = None,
                      algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
                      key_format: int = N.KEYS_AUTO, sieve: int = 0, sieve_band: int = 0,
-                     sieve_threads: int = 0):
+                     sieve_threads: int = 0, bucket_threads: int = 0):
     """Bounds contributions of one shard and ADDS its per-partition accumulators.
 
     pid, pk: int64 device tensors of length n (dense keys; pid may be None
@@ -308,7 +309,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")
     cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
-                       key_format, sieve, sieve_band, sieve_threads)
+                       key_format, sieve, sieve_band, sieve_threads, bucket_threads)
     nbytes = ctypes.c_uint64(0)
     N.check(lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)),
             "pdp_bound_workspace_bytes")

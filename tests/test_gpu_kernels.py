@@ -31,13 +31,13 @@ def _gen(seed, n, U, P, value_kind, skew=False):
     return pid, pk, val
 
 
-def _rand_shift(n, U, P, spec, algorithm=0):
+def _rand_shift(n, U, P, spec, algorithm=0, bucket_threads=0):
     from pipelinedp_amd import executor as X
-    return X.bound_plan(n, U, P, spec, algorithm).rand_shift
+    return X.bound_plan(n, U, P, spec, algorithm, bucket_threads=bucket_threads).rand_shift
 
 
 def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0, merge=0,
-             key_format=0):
+             key_format=0, bucket_threads=0):
     import torch
     from pipelinedp_amd import executor as X
     tp = torch.as_tensor(pid).to(device)
@@ -46,18 +46,18 @@ def _run_gpu(device, pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0,
     ta = None if allowed is None else torch.as_tensor(allowed.astype(np.uint8)).to(device)
     acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
                              allowed=ta, row_offset=row_offset, algorithm=algorithm, merge=merge,
-                             key_format=key_format)
+                             key_format=key_format, bucket_threads=bucket_threads)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
 
-def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0):
+def _oracle(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, algorithm=0, bucket_threads=0):
     return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0,
                               linf=spec.linf, value_kind=spec.value_kind, flags=spec.flags,
                               min_value=spec.min_value, max_value=spec.max_value,
                               middle=spec.middle, min_sum=spec.min_sum, max_sum=spec.max_sum,
                               seed=seed, row_offset=row_offset, allowed=allowed,
-                              rand_shift=_rand_shift(len(pid), U, P, spec, algorithm))
+                              rand_shift=_rand_shift(len(pid), U, P, spec, algorithm, bucket_threads))
 
 
 def _abs_scale(pid, pk, val, P, lo, hi, mid):
@@ -231,6 +231,31 @@ def test_two_level_range_merge_matches_oracle(device, P, skew):
     assert info.merge == 2 and info.n_ranges <= 256 and (P + 2047) // 2048 > 1024
     got = _run_gpu(device, pid, pk, val, U, P, spec, 33)
     want = _oracle(pid, pk, val, U, P, spec, 33)
+    _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
+
+
+@pytest.mark.parametrize("P,keys", [(5_000, 3), (5_000, 5), (10_000_000, 0), (1_500_000, 0)])
+def test_half_size_buckets_match_oracle(device, P, keys):
+    """bucket_threads = 512: buckets of half as many privacy ids (two
+    workgroups per CU), single-level and two-level range merges, a heavy id."""
+    from pipelinedp_amd import executor as X
+    rng = np.random.default_rng(P + keys)
+    n, U = 1_200_000, 200_000
+    pid = rng.integers(0, U, n)
+    pid[:30_000] = 4_321
+    pk = np.minimum(rng.zipf(1.3, n) - 1, P - 1).astype(np.int64)
+    val = rng.normal(4.0, 3.0, n)
+    spec = X.BoundingSpec(l0=3, linf=2, value_kind=O.VALUE_F64,
+                          flags=O.ACC_SUM | O.ACC_NSUM | O.ACC_NSUM2, min_value=0.0, max_value=9.0, middle=4.5)
+    full = X.bound_plan(n, U, P, spec, 2, 2, keys)
+    half = X.bound_plan(n, U, P, spec, 2, 2, keys, bucket_threads=512)
+    assert full.bucket_threads == 1024
+    if 512 < half.n_ranges <= 1024:  # one thread per range: no half-size buckets
+        assert half.bucket_threads == 1024
+        return
+    assert half.bucket_threads == 512 and half.bucket_bits == full.bucket_bits - 1 and half.lds_bytes <= 80 * 1024
+    got = _run_gpu(device, pid, pk, val, U, P, spec, 91, algorithm=2, merge=2, key_format=keys, bucket_threads=512)
+    want = _oracle(pid, pk, val, U, P, spec, 91, algorithm=2, bucket_threads=512)
     _compare(got, want, _abs_scale(pid, pk, val, P, 0.0, 9.0, 4.5))
 
 

@@ -41,7 +41,7 @@ def _spec(case):
 
 
 def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format=0, row_offset=0, band=0,
-         workspace=None, threads=0):
+         workspace=None, threads=0, bucket_threads=0):
     import torch
     from pipelinedp_amd import executor as X
     tv = None if val is None else torch.as_tensor(val).to(device)
@@ -49,17 +49,17 @@ def _run(device, pid, pk, val, U, P, spec, seed, sieve, allowed=None, key_format
     acc = X.bound_and_reduce(torch.as_tensor(pid).to(device), torch.as_tensor(pk).to(device), tv,
                              n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, allowed=ta,
                              key_format=key_format, sieve=sieve, row_offset=row_offset, sieve_band=band,
-                             workspace=workspace, sieve_threads=threads)
+                             workspace=workspace, sieve_threads=threads, bucket_threads=bucket_threads)
     torch.cuda.synchronize()
     return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
 
 
-def _want(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0):
+def _want(pid, pk, val, U, P, spec, seed, allowed=None, row_offset=0, bucket_threads=0):
     return O.bound_and_reduce(pid, pk, val, n_privacy_ids=U, n_partitions=P, l0=spec.l0, linf=spec.linf,
                               value_kind=spec.value_kind, flags=spec.flags, min_value=spec.min_value,
                               max_value=spec.max_value, middle=spec.middle, min_sum=spec.min_sum,
                               max_sum=spec.max_sum, seed=seed, allowed=allowed, row_offset=row_offset,
-                              rand_shift=_rand_shift(len(pid), U, P, spec))
+                              rand_shift=_rand_shift(len(pid), U, P, spec, bucket_threads=bucket_threads))
 
 
 @pytest.mark.parametrize("case", CASES, ids=[f"l0={c[0]}-linf={c[1]}-f={c[3]}" for c in CASES])
@@ -232,3 +232,18 @@ def test_malformed_records_are_flagged_not_read(device, sieve, key_format, monke
     torch.cuda.synchronize()  # the device is still healthy
     ok = _run(device, pid, pk, val, U, P, base, 5, sieve, key_format=key_format)
     assert ok["privacy_id_count"].sum() > 0
+
+
+@pytest.mark.parametrize("sieve", [6000, 10096])
+def test_sieve_with_half_size_buckets(device, sieve):
+    """bucket_threads = 512 under the sieve and its band: the candidate
+    records, the fix-up launches and the range merge over twice the buckets."""
+    from pipelinedp_amd import executor as X
+    spec = _spec(CASES[0])
+    U, P, n = 400_000, 100_003, 4_000_000
+    pid, pk, val = _gen(5, n, U, P, spec.value_kind, skew=True)
+    plan = X.bound_plan(n, U, P, spec, sieve=sieve, bucket_threads=512)
+    assert plan.sieve == sieve and plan.bucket_threads == 512
+    got = _run(device, pid, pk, val, U, P, spec, 19, sieve, bucket_threads=512)
+    want = _want(pid, pk, val, U, P, spec, 19, bucket_threads=512)
+    _compare(got, want, _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle))
