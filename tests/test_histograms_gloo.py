@@ -101,3 +101,47 @@ def test_partition_counter_overflow_across_ranks_raises():
     results = ctx.Manager().dict()
     mp.spawn(_overflow_worker, args=(_free_port(), results), nprocs=2, join=True)
     assert dict(results) == {0: "ValueError", 1: "ValueError"}
+
+
+def _weights_worker(rank, port, results):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        # L0/L1 weight sums that land exactly on x.5 only when the ranks' parts
+        # are added before rounding: key 7 -> 1.25 + 1.25, key 9 -> 0.5 + 2.0,
+        # key 11 only on rank 1 (3/8 + 1/8 in one part)
+        wsmall = torch.zeros(2000, dtype=torch.float64)
+        wsmall[3] = 0.75 if rank == 0 else 1.75
+        keys = [7, 9] if rank == 0 else [9, 7, 11]
+        ws = [1.25, 0.5] if rank == 0 else [2.0, 1.25, 0.5]
+        wtab = torch.zeros((8, 2), dtype=torch.int64)
+        for i, (k, w) in enumerate(zip(keys, ws)):
+            wtab[2 * i, 0] = k
+            wtab[2 * i, 1] = torch.tensor([w], dtype=torch.float64).view(torch.int64)[0]
+        uk, uw = parallel.exchange_preaggregated_weights(wsmall, wtab, None)
+        results[rank] = (dict(zip(uk.tolist(), uw.tolist())), wsmall[3].item(), int(wtab.abs().sum()))
+    except Exception as e:  # pragma: no cover - reported by the parent
+        results[rank] = repr(e)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_preaggregated_weights_summed_before_rounding():
+    """2-rank pre-aggregated weights equal the 1-rank sums at a .5
+    tie (dyadic weights: every addition order gives the same fp64 sum, so the
+    2-rank and 1-rank bins round alike; non-dyadic ties such as 1/3 + 1/6 can
+    differ by an ulp with the summation order -- as the reference's own Python
+    sum order does -- and stay parity-unpinned)."""
+    ctx = mp.get_context("spawn")
+    results = ctx.Manager().dict()
+    mp.spawn(_weights_worker, args=(_free_port(), results), nprocs=2, join=True)
+    assert all(isinstance(results[r], tuple) for r in (0, 1)), dict(results)
+    merged = {}
+    for r in (0, 1):
+        for k, w in results[r][0].items():
+            assert k not in merged  # each key summed on exactly one (its owner) rank
+            merged[k] = w
+    assert merged == {7: 2.5, 9: 2.5, 11: 0.5}
+    assert [round(merged[k]) for k in (7, 9)] == [2, 2]  # half to even, as one rank's 2.5
+    assert results[0][1] == 2.5 and results[1][1] == 0.0  # small weights: rank 0 holds the sum
+    assert results[0][2] == 0 and results[1][2] == 0       # the tables are zeroed
