@@ -774,7 +774,9 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     launches = {k: v[1] / args.steps for k, v in kernels.items()}
     ms_per_step = elapsed / args.steps * 1e3
     total_rows = n * world * args.steps
-    traffic, traffic_src, traffic_refused = load_pmc(pmc_file, workload, n, world)
+    # a variant's counters are not the base workload's: --small-ids names its own
+    traffic, traffic_src, traffic_refused = load_pmc(
+        pmc_file, f"{workload}-small{args.small_ids:g}" if args.small_ids else workload, n, world)
     alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2, stats)
     table = {}
     for k, ms in kernel_ms.items():
@@ -904,6 +906,7 @@ def main():
         "bound_plan": r["bound_plan"],
         "seed": r.get("seed"),
         "partitions_kept": r["partitions_kept"],
+        "kept_pairs": r.get("kept_pairs"), "kept_rows": r.get("kept_rows"),
         "privacy_id_verify": r.get("privacy_id_verify_ms"),
         "step_ms_spread": r.get("step_ms_spread"),
         "api": r["api"],
