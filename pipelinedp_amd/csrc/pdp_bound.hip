@@ -3562,7 +3562,12 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     if (fr.f0) fr.f0 += seg * p.n_buckets * n_slots;
     if (fr.f1) fr.f1 += seg * p.n_buckets * n_slots;
     if (fr.f2) fr.f2 += seg * p.n_buckets * n_slots;
-    return launch_bucket_kernel<VK, KA>(kf, p, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
+    // fix-up buckets hold only unresolved ids' rows and most are empty: the
+    // same buckets and LDS on 512 threads (half the waves to launch per
+    // bucket; the kernel sizes its queues from blockDim)
+    Plan pf = p;
+    if (p.merge != PDP_MERGE_RANGES || p.n_ranges <= kBucketThreads / 2) pf.bucket_threads = kBucketThreads / 2;
+    return launch_bucket_kernel<VK, KA>(kf, pf, st, ws + w.keys2, (const unsigned*)(ws + w.rows2),
                                         (const unsigned*)fix_cnt, value, acc, fr, ws, w, name, mk);
   };
   auto rescan = [&](const unsigned* bits, const unsigned* list, unsigned* sctl) {
