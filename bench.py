@@ -48,6 +48,14 @@ import time
 
 import numpy as np
 
+# The caching allocator's expandable segments (set before torch is imported;
+# a caller's own PYTORCH_HIP_ALLOC_CONF wins): on the same box and binary,
+# k_sieve_l1 streams the 16 GB of C3 key columns in 3.43-3.45 ms with them and
+# 3.72-3.74 ms without, three processes each, interleaved
+# (profiles/r04/ab/ab10_alloc_conf.txt) -- how the input columns and the
+# workspace are mapped, not the kernels, made round 3's "box to box" spread.
+os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
     sys.path.insert(0, HERE)
