@@ -109,6 +109,7 @@ def parse():
     ap.add_argument("--workload", choices=("c3", "c2", "c4", "c5", "hist"), default="c3")
     ap.add_argument("--rows", type=int, default=0, help="override: rows in total (c3) / per GPU (c2)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-secondary", action="store_true", help="skip the C2 secondary run at N = 1")
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
     ap.add_argument("--key-format", type=int, default=0, help="PDP_KEYS_* (0 auto)")
@@ -859,11 +860,20 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
+    if args.cpu_baseline_only:  # the child below: CPU baselines as one JSON line, no GPU
+        cpu = (cpu_baselines(args.workload, args.cpu_sample_rows) if args.workload in ("c3", "c2")
+               else (hist_cpu_baseline(4 * args.cpu_sample_rows), None))
+        print(json.dumps(cpu), flush=True)
+        return
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2"):
-        cpu = cpu_baselines(args.workload, args.cpu_sample_rows)  # before any GPU state exists
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "hist":
-        cpu = (hist_cpu_baseline(4 * args.cpu_sample_rows), None)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2", "hist"):
+        # in a child process, before any GPU state exists: run in this process,
+        # the baseline's host allocations slowed the timed k_sieve_l1 by
+        # 0.35 ms (3.48 -> 3.83 ms at C3, profiles/r04/ab/ab11_cpu_baseline_process.txt)
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--workload",
+                              args.workload, "--cpu-sample-rows", str(args.cpu_sample_rows)],
+                             capture_output=True, text=True, check=True)
+        cpu = json.loads([l for l in out.stdout.splitlines() if l.startswith("[")][-1])
     import torch
     import torch.distributed as dist
     # PDP_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
