@@ -865,15 +865,6 @@ def main():
                else (hist_cpu_baseline(4 * args.cpu_sample_rows), None))
         print(json.dumps(cpu), flush=True)
         return
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2", "hist"):
-        # in a child process, before any GPU state exists: run in this process,
-        # the baseline's host allocations slowed the timed k_sieve_l1 by
-        # 0.35 ms (3.48 -> 3.83 ms at C3, profiles/r04/ab/ab11_cpu_baseline_process.txt)
-        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--workload",
-                              args.workload, "--cpu-sample-rows", str(args.cpu_sample_rows)],
-                             capture_output=True, text=True, check=True)
-        cpu = json.loads([l for l in out.stdout.splitlines() if l.startswith("[")][-1])
     import torch
     import torch.distributed as dist
     # PDP_BENCH_BACKEND=gloo rehearses the multi-rank path with every rank on
@@ -928,14 +919,26 @@ def main():
         "privacy_id_verify": r.get("privacy_id_verify_ms"),
         "step_ms_spread": r.get("step_ms_spread"),
         "api": r["api"],
-        "cpu_baseline": cpu[0] if cpu else None,
-        "cpu_baseline_strong": cpu[1] if cpu else None,
+        "cpu_baseline": None,
+        "cpu_baseline_strong": None,
     }
     if world == 1 and args.workload == "c3" and not args.no_secondary and not args.rows:
         torch.cuda.empty_cache()
         s = run_workload(args, "c2", 1, 0, device, PMC_SUMMARY["c2"])
         result["secondary"] = {k: s[k] for k in ("value", "ms_per_step", "config", "roofline",
                                                  "path_roofline", "kernels", "bound_plan", "api")}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2", "hist"):
+        # after the GPU measurements, in a child process: run before them (in
+        # this process or a child) the baseline's ~30 s of 16-core host work
+        # left the timed k_sieve_l1 0.35 ms slower (3.48 -> 3.83 ms at C3,
+        # profiles/r04/ab/ab11_cpu_baseline_process.txt)
+        out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--workload",
+                              args.workload, "--cpu-sample-rows", str(args.cpu_sample_rows)],
+                             capture_output=True, text=True, check=True)
+        cpu = json.loads([l for l in out.stdout.splitlines() if l.startswith("[")][-1])
+    if cpu:
+        result["cpu_baseline"], result["cpu_baseline_strong"] = cpu[0], cpu[1]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
