@@ -48,13 +48,6 @@ import time
 
 import numpy as np
 
-# The caching allocator's expandable segments (set before torch is imported;
-# a caller's own PYTORCH_HIP_ALLOC_CONF wins): on the same box and binary,
-# k_sieve_l1 streams the 16 GB of C3 key columns in 3.43-3.45 ms with them and
-# 3.72-3.74 ms without, three processes each, interleaved
-# (profiles/r04/ab/ab10_alloc_conf.txt) -- how the input columns and the
-# workspace are mapped, not the kernels, made round 3's "box to box" spread.
-os.environ.setdefault("PYTORCH_HIP_ALLOC_CONF", "expandable_segments:True")
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 if HERE not in sys.path:
@@ -860,7 +853,7 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    if args.cpu_baseline_only:  # the child below: CPU baselines as one JSON line, no GPU
+    if args.cpu_baseline_only:  # the child started below: CPU baselines as one JSON line, no GPU
         cpu = (cpu_baselines(args.workload, args.cpu_sample_rows) if args.workload in ("c3", "c2")
                else (hist_cpu_baseline(4 * args.cpu_sample_rows), None))
         print(json.dumps(cpu), flush=True)
@@ -929,10 +922,8 @@ def main():
                                                  "path_roofline", "kernels", "bound_plan", "api")}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("c3", "c2", "hist"):
-        # after the GPU measurements, in a child process: run before them (in
-        # this process or a child) the baseline's ~30 s of 16-core host work
-        # left the timed k_sieve_l1 0.35 ms slower (3.48 -> 3.83 ms at C3,
-        # profiles/r04/ab/ab11_cpu_baseline_process.txt)
+        # after the GPU measurements, in a child process (no GPU state there):
+        # its ~30 s of host work can neither precede nor overlap the timed steps
         out = subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-baseline-only", "--workload",
                               args.workload, "--cpu-sample-rows", str(args.cpu_sample_rows)],
                              capture_output=True, text=True, check=True)
