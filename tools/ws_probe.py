@@ -35,9 +35,23 @@ def l1_ms(pid, pk, ws):
     return k["k_sieve_l1"][0] / k["k_sieve_l1"][1]
 
 
+class AlignedWorkspace(X.BoundWorkspace):
+    """the workspace as a view starting on a 1 GiB virtual-address boundary"""
+
+    def get(self, nbytes, device):
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.raw = torch.empty(int(nbytes) + (1 << 30), dtype=torch.uint8, device=device)
+            off = (-self.raw.data_ptr()) % (1 << 30)
+            self.buf = self.raw[off:off + int(nbytes)]
+        return self.buf
+
+
+print(f"pid at {pid.data_ptr() % (1 << 30):#x} mod 1 GiB, pk at {pk.data_ptr() % (1 << 30):#x}", flush=True)
 for r in range(4):
-    ws = X.BoundWorkspace()
-    print(f"fresh workspace {r}: k_sieve_l1 {l1_ms(pid, pk, ws):.3f} ms", flush=True)
+    ws = X.BoundWorkspace() if r < 2 else AlignedWorkspace()
+    t = l1_ms(pid, pk, ws)
+    print(f"fresh workspace {r} ({type(ws).__name__}) at {ws.buf.data_ptr() % (1 << 30):#x} mod 1 GiB "
+          f"({ws.buf.data_ptr() % (1 << 21):#x} mod 2 MiB): k_sieve_l1 {t:.3f} ms", flush=True)
     del ws
     torch.cuda.empty_cache()
 ws = X.BoundWorkspace()
