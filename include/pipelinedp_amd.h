@@ -486,7 +486,7 @@ int pdp_dataset_histograms_weight_bins(const uint64_t* keys, const double* weigh
  * rank holds an id it does not own, no id can be on two ranks, so the
  * library skips the exchange of distinct ids (contribution_bounders.py:62-111
  * bounds per privacy id over the whole dataset).  ids: device int64[n];
- * *mismatches: device uint32, overwritten (saturates at 2^32 - 1). */
+ * *mismatches: device uint32, overwritten (a saturating count: 2^32 - 1 at most, never wraps to 0). */
 int pdp_owner_mismatches(const int64_t* ids, int64_t n, int32_t world, int32_t rank, uint32_t* mismatches,
                          void* stream);
 

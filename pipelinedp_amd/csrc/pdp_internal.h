@@ -228,7 +228,7 @@ __device__ __forceinline__ bool gaussian_attempt(const pdp_noise_params& np, uin
                                                  uint32_t slot, uint32_t& k, double* md_out) {
   const uint64_t step = (uint64_t)np.step;
   const U4 a = noise_block(seed, gidx, slot, k++);
-  const int geom = __clz(~a.x & 0xFF000000u | 0x00800000u);  // leading ones of x[31:24], at most 8
+  const int geom = __clz((~a.x & 0xFF000000u) | 0x00800000u);  // leading ones of x[31:24], at most 8
   const int64_t two_sided = ((a.x >> 23) & 1u) ? (int64_t)geom : -(int64_t)geom - 1;
   // floor(r * step / 2^64) for the 64 random bits r = (y, z); step < 2^32
   const uint64_t hi_part = (uint64_t)a.y * step + (((uint64_t)a.z * step) >> 32);

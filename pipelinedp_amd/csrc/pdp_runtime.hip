@@ -72,7 +72,7 @@ __device__ __forceinline__ int owner_of(int64_t z, int world) {
   return (int)(r < 0 ? r + world : r);
 }
 
-// grid-stride, 16-byte loads where aligned; one atomic per wave with a mismatch
+// grid-stride, 16-byte loads where aligned; one saturating atomic per wave with a mismatch
 __global__ void __launch_bounds__(kBlock) k_owner_mismatches(const int64_t* __restrict__ ids, int64_t n, int world,
                                                              int rank, unsigned* out) {
   unsigned bad = 0;
@@ -86,7 +86,14 @@ __global__ void __launch_bounds__(kBlock) k_owner_mismatches(const int64_t* __re
   for (int64_t i = 2 * n2 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
     bad += owner_of(ids[i], world) != rank;
   for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
-  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(out, bad);
+  if ((threadIdx.x & 63) == 0 && bad) {  // saturating add: a count that wrapped to 0 would read as "owned"
+    unsigned old = __hip_atomic_load(out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), assumed;
+    do {
+      assumed = old;
+      const unsigned sum = assumed + bad < assumed ? 0xFFFFFFFFu : assumed + bad;
+      old = atomicCAS(out, assumed, sum);
+    } while (old != assumed);
+  }
 }
 }  // namespace
 

@@ -247,3 +247,26 @@ def test_sieve_with_half_size_buckets(device, sieve):
     got = _run(device, pid, pk, val, U, P, spec, 19, sieve, bucket_threads=512)
     want = _want(pid, pk, val, U, P, spec, 19, bucket_threads=512)
     _compare(got, want, _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle))
+
+
+@pytest.mark.parametrize("threads", [512, 1024])
+def test_persistent_level1_loops_over_tiles(device, threads, monkeypatch):
+    """The persistent level 1 with few workgroups (test hook
+    PIPELINEDP_AMD_L1_GRID): each workgroup runs several whole tiles, so the
+    next tile's chunks are prefetched across the tile boundary and the LDS
+    state (bucket counts, band queues, flush slots) is reset between tiles;
+    with the band on and off, equal to the oracle."""
+    from pipelinedp_amd import executor as X
+    spec = _spec(CASES[0])
+    U, P = 200_000, 3001
+    n = 40 * 65536 + 777  # 40 whole tiles and a ragged one
+    pid, pk, val = _gen(41, n, U, P, spec.value_kind, skew=True)
+    seed = 6060
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    monkeypatch.setenv("PIPELINEDP_AMD_TEST_HOOKS", "1")
+    for grid in ("3", "7"):  # 13-14 and 5-6 tiles per workgroup
+        monkeypatch.setenv("PIPELINEDP_AMD_L1_GRID", grid)
+        for band in (0, -1):
+            got = _run(device, pid, pk, val, U, P, spec, seed, 4096, band=band, threads=threads)
+            _compare(got, want, scale)
