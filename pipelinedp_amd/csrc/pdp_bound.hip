@@ -150,9 +150,17 @@ constexpr int64_t kSieveLds2 = 80 * 1024 - 256;  // two 512-thread workgroups pe
 // a tile's flush blocks lie back to back from tile * kSieveTileStride, its
 // band list at tile * kBandTileStride
 // (strides padded by 4 KiB measured 6 % slower at C3, profiles/r05/ab/ab1_l1_placement.txt)
+// non-temporal loads (ld_nt) of the columns level 1 streams and of the band
+// lists k_band_scan streams (C3 0.277 -> 0.255 ms); measured neutral or worse
+// and not used: k_scatter_l1_local's key loads (C4 +0.03 ms), level 2's run
+// loads and the bucket kernel's record stream (profiles/r05/ab/ab5_nt_loads.txt)
 #ifndef PDP_L1_NT
 #define PDP_L1_NT 1
 #endif
+#ifndef PDP_NT_BS
+#define PDP_NT_BS 1
+#endif
+
 constexpr int64_t kSieveTileStride = kTileRows;
 constexpr int64_t kBandTileStride = kTileRows;
 constexpr int kSieveMaxT16 = 1 << 15;                          // t <= 1/2
@@ -1720,15 +1728,8 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       for (int q = 0; q < Q; q += 2) {
         const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH);
         if constexpr (FULL) {
-#if PDP_L1_NT & 1
-          typedef long long ll2v __attribute__((ext_vector_type(2)));
-          const ll2v av = __builtin_nontemporal_load(reinterpret_cast<const ll2v*>(pid + i));
-          const ll2v cv = __builtin_nontemporal_load(reinterpret_cast<const ll2v*>(pk + i));
-          const longlong2 a = make_longlong2(av.x, av.y), c = make_longlong2(cv.x, cv.y);
-#else
-          const longlong2 a = *reinterpret_cast<const longlong2*>(pid + i);
-          const longlong2 c = *reinterpret_cast<const longlong2*>(pk + i);
-#endif
+          const longlong2 a = ld_maybe_nt<PDP_L1_NT>(reinterpret_cast<const longlong2*>(pid + i));
+          const longlong2 c = ld_maybe_nt<PDP_L1_NT>(reinterpret_cast<const longlong2*>(pk + i));
           u[q] = a.x;
           u[q + 1] = a.y;
           k[q] = c.x;
@@ -2807,7 +2808,7 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
 #pragma unroll
         for (int v = 0; v < KU; ++v) {
           const int64_t j = j0 + v * 64 + lane;
-          e[v] = j < cnt ? bt[j] : ~0ULL;
+          e[v] = j < cnt ? ld_maybe_nt<PDP_NT_BS>(bt + j) : ~0ULL;
         }
 #pragma unroll
         for (int v = 0; v < KU; ++v) {
@@ -3870,6 +3871,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
       PDP_HIP_CHECK(hipGetLastError());
     }
   }
+  if (test_hooks_enabled() && std::getenv("PIPELINEDP_AMD_STOP_AFTER_L1") != nullptr && p.sieve) return PDP_OK;
   if (!p.sieve) {
     const size_t lds1 = (l1_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
     const void* l1 = u16 ? (const void*)k_scatter_l1_local<FMT, true> : (const void*)k_scatter_l1_local<FMT, false>;
@@ -4176,6 +4178,9 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     rc2 = launch_offsets(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   }
   if (rc2 != PDP_OK) return rc2;
+  // test hook (tools/l1_probe.py): level 1 alone, timed by the profiler;
+  // nothing downstream reads what it wrote
+  if (test_hooks_enabled() && std::getenv("PIPELINEDP_AMD_STOP_AFTER_L1") != nullptr) return PDP_OK;
   // PDP_MERGE_ATOMIC: the bucket kernel adds into the accumulators, so it
   // runs in pdp_reduce_partitions; PDP_MERGE_RANGES: all sampling runs here
   if (p.merge != PDP_MERGE_RANGES) return PDP_OK;

@@ -37,6 +37,41 @@ inline unsigned grid_for(int64_t n, int64_t cap = 1 << 16) {
 
 inline uint64_t align256(uint64_t x) { return (x + 255) & ~(uint64_t)255; }
 
+// Non-temporal ("streaming") loads of data a kernel reads exactly once: the
+// lines are not kept in L2, which then holds the kernel's partially written
+// output lines until they are whole (k_sieve_l1: C2 level 1 0.385 -> 0.349
+// ms, profiles/r05/ab/ab4_fix_list_nt_loads.txt)
+__device__ __forceinline__ longlong2 ld_nt(const longlong2* p) {
+  typedef long long v2 __attribute__((ext_vector_type(2)));
+  const v2 v = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
+  return make_longlong2(v.x, v.y);
+}
+__device__ __forceinline__ ulonglong2 ld_nt(const ulonglong2* p) {
+  typedef unsigned long long v2 __attribute__((ext_vector_type(2)));
+  const v2 v = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
+  return make_ulonglong2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  typedef unsigned v4 __attribute__((ext_vector_type(4)));
+  const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld_nt(const uint2* p) {
+  typedef unsigned v2 __attribute__((ext_vector_type(2)));
+  const v2 v = __builtin_nontemporal_load(reinterpret_cast<const v2*>(p));
+  return make_uint2(v.x, v.y);
+}
+template <typename T>
+__device__ __forceinline__ T ld_nt(const T* p) {
+  return __builtin_nontemporal_load(p);
+}
+// a load that is non-temporal when NT is set (a compile-time choice per site)
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_maybe_nt(const T* p) {
+  if constexpr (NT) return ld_nt(p);
+  else return *p;
+}
+
 inline int bits_for(int64_t n) {  // smallest b >= 1 with 2^b >= n
   int b = 1;
   while (b < 63 && ((int64_t)1 << b) < n) ++b;
