@@ -62,10 +62,38 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PMC_SUMMARY = {w: os.path.join(HERE, "profiles", "r04", f"{w}_pmc.json") for w in ("c3", "c2", "c4", "c5", "hist")}
 
 
-def load_pmc(pmc_file, workload, n, world):
+# kernels whose work depends on the step's data (the sieve's fix-up: how many
+# privacy ids stay unresolved, how many rows the band and the fix-up list hold)
+# -> the bound_plan.stats fields that measure it.  Their PMC bytes are joined
+# only when the profiled run's stats equal this run's on those fields and the
+# profiled launches moved about the same bytes each.
+DATA_DEPENDENT = {
+    "k_band_scan": ("unresolved_ids", "band_rows"),
+    "k_fix_filter": ("fixup_rows", "fixup2_rows"),
+    "k_fix_scatter": ("fixup_rows", "fixup2_rows"),
+    "k_fix_buckets": ("unresolved_ids", "unresolved2_ids"),
+    "k_bucket_fix": ("unresolved_ids", "fixup_rows"),
+    "k_sieve_rescan": ("unresolved_ids", "unresolved2_ids", "fixup2_rows"),
+    "k_bucket_fix2": ("unresolved2_ids", "fixup2_rows"),
+}
+
+
+def join_pmc_entry(kernel, e, pmc_stats, stats):
+    """Whether a PMC summary entry may stand for this run's launches of `kernel`."""
+    keys = DATA_DEPENDENT.get(kernel)
+    if keys is None:
+        return True
+    if not pmc_stats or not stats or any(pmc_stats.get(k) != stats.get(k) for k in keys):
+        return False
+    lo, hi = e.get("launch_hbm_bytes_min"), e.get("launch_hbm_bytes_max")
+    return lo is not None and hi is not None and hi <= 1.25 * lo + 1e6
+
+
+def load_pmc(pmc_file, workload, n, world, stats=None):
     """Per-kernel HBM bytes from a PMC summary, joined only when it was made
     from this workload at this size AND from these kernel sources (its "tree"
-    equals tools/tree_id.py's id of the tree bench.py runs on).  Returns
+    equals tools/tree_id.py's id of the tree bench.py runs on); a
+    data-dependent kernel's entry only when join_pmc_entry allows it.  Returns
     (traffic, source, refused): refused names why a file present was not used."""
     if world != 1 or not pmc_file or not os.path.exists(pmc_file):
         return {}, None, None
@@ -79,7 +107,22 @@ def load_pmc(pmc_file, workload, n, world):
     tree = source_tree_id()
     if pmc.get("tree") != tree:
         return {}, None, f"{src}: profiled tree {pmc.get('tree')}, this tree {tree}"
-    return {k: v["hbm_bytes"] for k, v in pmc["kernels"].items() if "hbm_bytes" in v}, src, None
+    return ({k: v["hbm_bytes"] for k, v in pmc["kernels"].items()
+             if "hbm_bytes" in v and join_pmc_entry(k, v, pmc.get("stats"), stats)}, src, None)
+
+
+def pmc_entry(e, k, traffic, ms):
+    """Adds a kernel's PMC bytes to its table entry -- unless they imply a rate
+    above the HBM peak, which no launch can move (a figure from launches that
+    did other work than these); returns whether they were added."""
+    if k not in traffic:
+        return False
+    gbs = traffic[k] / (ms * 1e-3) / 1e9
+    if gbs > HBM_PEAK_GBS:
+        return False
+    e["pmc_bytes"] = traffic[k]
+    e["pmc_gbs"] = gbs
+    return True
 
 # workload constants (SURVEY §8(d))
 C2 = dict(rows=100_000_000, privacy_ids=1_000_000, partitions=100_000, l0=8, linf=2)
@@ -167,11 +210,14 @@ def build_plan(l0, linf):
 
 
 def cpu_baselines(workload, sample_rows):
-    """Rank 0, N = 1, before any GPU work.  `port`: the row-wise restatement
-    of LocalBackend DPEngine.aggregate (the reference's single-threaded CPU
-    path, oracle/local_backend_port.py) on a bounded sample of the workload;
-    `strong`: the vectorised NumPy oracle on up to 16 host processes
-    (oracle/strong_baseline.py)."""
+    """Rank 0, N = 1, after the GPU work in a child process.  `port`: the
+    row-wise restatement of LocalBackend DPEngine.aggregate (the reference's
+    single-threaded CPU path, oracle/local_backend_port.py) on a bounded
+    sample of the workload; `strong`: the vectorised NumPy oracle on every
+    CPU this process may use (os.cpu_count() bounded by the affinity mask and
+    the cgroup quota, oracle/strong_baseline.py); `c1`: the
+    port at BASELINE config 1 itself (1e6 movie_view rows, COUNT + SUM,
+    BASELINE.md §3.1)."""
     from oracle import local_backend_port as port
     from oracle import strong_baseline as strong
     w = C3 if workload == "c3" else C2
@@ -196,15 +242,24 @@ def cpu_baselines(workload, sample_rows):
                       f"np.random.choice, np.clip per pair; no namedtuples or DPEngine generators, so it "
                       f"runs ~2x the reference's own measured rate, BASELINE.md §2); {dt:.1f} s, "
                       f"{len(out)} partitions kept; the full workload is a linear extrapolation"}
-    workers = max(1, min(16, os.cpu_count() or 1))
+    workers, cpu_note = strong.usable_cpus()
     per = 2_000_000
     rate, sdt, kept = strong.run(workers, per, per // 100, w["partitions"], w.get("zipf", 0.0) or 1.0001,
                                  w["l0"], w["linf"], EPS, DELTA)
     strong_res = {"value": rate, "unit": "rows/s", "cores": workers, "kind": "port", "cpu_model": model,
                   "sample": f"{workers} x {per} rows (privacy-id shards, Zipf pk), vectorised NumPy oracle "
                             f"(oracle/columnar.py) one process per shard + merge/select/noise; "
-                            f"{sdt:.2f} s, {kept} partitions kept"}
-    return base, strong_res
+                            f"{sdt:.2f} s, {kept} partitions kept; {cpu_note}"}
+    c1_rows = port.movie_view_rows(1_000_000, seed=0)
+    t0 = time.perf_counter()
+    c1_out = port.aggregate_count_sum(c1_rows, l0=2, linf=1, min_value=1.0, max_value=5.0, eps=EPS, delta=DELTA)
+    c1_dt = time.perf_counter() - t0
+    c1 = {"value": len(c1_rows) / c1_dt, "unit": "rows/s", "cores": 1, "kind": "port", "cpu_model": model,
+          "sample": f"BASELINE config 1 itself: 1e6 synthetic movie_view rows (user_id over 1e5, movie_id "
+                    f"min(Zipf(1.3), 17770), rating 1-5), COUNT+SUM, L0=2, Linf=1, clip [1, 5], Laplace, "
+                    f"truncated-geometric selection; oracle/local_backend_port.py aggregate_count_sum on one "
+                    f"core, {c1_dt:.1f} s, {len(c1_out)} partitions kept"}
+    return base, strong_res, c1
 
 
 def gen_c3(n, U, P, rank, world, device, seed, small_ids=0.0):
@@ -439,7 +494,7 @@ def run_api_workload(args, workload, world, rank, device):
     kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
     launches = {k: v[1] / args.steps for k, v in kernels.items()}
     ms_per_step = elapsed / args.steps * 1e3
-    traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY[workload], workload, n, world)
+    traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY[workload], workload, n, world, stats)
     alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats, P)
     table = {}
     for k, ms in kernel_ms.items():
@@ -448,9 +503,8 @@ def run_api_workload(args, workload, world, rank, device):
             e["alg_bytes"] = alg[k]
             e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
             e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
-        if k in traffic:
-            e["pmc_bytes"] = traffic[k]
-            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
+        if not pmc_entry(e, k, traffic, ms):
+            traffic.pop(k, None)  # out of traffic_per_step too
         table[k] = e
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
     # compulsory bytes: the three input columns once, and per
@@ -539,12 +593,18 @@ def run_hist_workload(args, world, rank, device):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    pairs = int(torch.unique(pid * P + pk).numel())  # distinct (privacy id, partition) pairs, untimed
     del pid, pk, val, ws
     kernel_ms = {k: v[0] / v[1] for k, v in kernels.items()}
     launches = {k: v[1] / args.steps for k, v in kernels.items()}
     # algorithmic bytes per launch: rows read / records moved once
     alg = {"k_hb_count": 16.0 * n, "k_hb_l1": (24.0 + 16.0) * n, "k_hb_bcount": 8.0 * n,
-           "k_hb_l2": 32.0 * n, "k_hb_pairs": 16.0 * n}
+           "k_hb_l2": 32.0 * n, "k_hb_pairs": 16.0 * n,
+           # the per-bucket pair pass: 16-byte records in, a 16-byte (partition,
+           # rows, sum) record out per distinct pair; the range pass and the
+           # float histograms read those once; per-id / per-partition stats
+           "k_hb_pid_pairs": 16.0 * n + 16.0 * pairs, "k_hb_prange": 16.0 * pairs,
+           "k_h_float": 16.0 * pairs, "k_h_ids": 16.0 * (U + P)}
     traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY["hist"], "hist", n, world)
     table = {}
     for k, ms in kernel_ms.items():
@@ -553,9 +613,8 @@ def run_hist_workload(args, world, rank, device):
             e["alg_bytes"] = alg[k]
             e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
             e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
-        if k in traffic:
-            e["pmc_bytes"] = traffic[k]
-            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
+        if not pmc_entry(e, k, traffic, ms):
+            traffic.pop(k, None)  # out of traffic_per_step too
         table[k] = e
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
     ms_per_step = elapsed / args.steps * 1e3
@@ -574,7 +633,7 @@ def run_hist_workload(args, world, rank, device):
                      "bytes_per_launch": alg.get(dom), "avg_ms": kernel_ms[dom]},
         "path_roofline": {"achieved": path_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": path_gbs / HBM_PEAK_GBS, "bytes_per_step": path_bytes},
-        "kernels": table, "bound_plan": None, "partitions_kept": None, "api": None,
+        "kernels": table, "bound_plan": None, "partitions_kept": None, "api": None, "pairs": pairs,
     }
 
 
@@ -765,6 +824,12 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         step(args.warmup + 2 * args.steps + i)
         torch.cuda.synchronize()
         samples.append((time.perf_counter() - ts) * 1e3)
+    # the plan the timed steps ran: the auto plan, unless the library's plan
+    # feedback (executor.py) turned the sieve off for these columns
+    feedback = X.plan_feedback_state(pid, pk, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
+                                     row_offset=rank * n)
+    if feedback and feedback["unsieved"] and not args.sieve:
+        plan = X.bound_plan(n, U, P_pad, bounding, **dict(tune, sieve=-1))
     api = api_timing(args, workload, pid, pk, value, U, P, ws) if (world == 1 and args.api) else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -778,7 +843,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     total_rows = n * world * args.steps
     # a variant's counters are not the base workload's: --small-ids names its own
     traffic, traffic_src, traffic_refused = load_pmc(
-        pmc_file, f"{workload}-small{args.small_ids:g}" if args.small_ids else workload, n, world)
+        pmc_file, f"{workload}-small{args.small_ids:g}" if args.small_ids else workload, n, world, stats)
     alg = kernel_alg_bytes(plan, n, kept_pairs, kept_rows, 2, stats)
     table = {}
     for k, ms in kernel_ms.items():
@@ -787,9 +852,8 @@ def run_workload(args, workload, world, rank, device, pmc_file):
             e["alg_bytes"] = alg[k]
             e["achieved_gbs"] = alg[k] / (ms * 1e-3) / 1e9
             e["frac"] = e["achieved_gbs"] / HBM_PEAK_GBS
-        if k in traffic:
-            e["pmc_bytes"] = traffic[k]
-            e["pmc_gbs"] = traffic[k] / (ms * 1e-3) / 1e9
+        if not pmc_entry(e, k, traffic, ms):
+            traffic.pop(k, None)  # out of traffic_per_step too
         table[k] = e
     dom = max(kernel_ms, key=lambda k: kernel_ms[k] * launches[k])
     path_bytes = 24.0 * n + kept * (8 + 8 * 3 + 8 * 3)  # SURVEY §8(d) compulsory bytes
@@ -827,7 +891,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                            plan.key_format, plan.key_format),
                        "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0,
                        "sieve_threads": plan.sieve_threads, "bucket_threads": plan.bucket_threads,
-                       "stats": stats},
+                       "stats": stats, "plan_feedback": feedback},
         "seed": args.seed,
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,
@@ -855,7 +919,7 @@ def main():
         return
     if args.cpu_baseline_only:  # the child started below: CPU baselines as one JSON line, no GPU
         cpu = (cpu_baselines(args.workload, args.cpu_sample_rows) if args.workload in ("c3", "c2")
-               else (hist_cpu_baseline(4 * args.cpu_sample_rows), None))
+               else (hist_cpu_baseline(4 * args.cpu_sample_rows), None, None))
         print(json.dumps(cpu), flush=True)
         return
     import torch
@@ -914,6 +978,7 @@ def main():
         "api": r["api"],
         "cpu_baseline": None,
         "cpu_baseline_strong": None,
+        "cpu_baseline_c1": None,
     }
     if world == 1 and args.workload == "c3" and not args.no_secondary and not args.rows:
         torch.cuda.empty_cache()
@@ -930,6 +995,7 @@ def main():
         cpu = json.loads([l for l in out.stdout.splitlines() if l.startswith("[")][-1])
     if cpu:
         result["cpu_baseline"], result["cpu_baseline_strong"] = cpu[0], cpu[1]
+        result["cpu_baseline_c1"] = cpu[2] if len(cpu) > 2 else None
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

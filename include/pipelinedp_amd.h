@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 12
+#define PDP_ABI_VERSION 13
 
 /* error codes */
 #define PDP_OK 0
@@ -352,6 +352,17 @@ typedef struct pdp_bound_stats {
 
 int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,
                          pdp_bound_stats* out, void* stream);
+
+/* The sieve's fix-up counters of the last pdp_bound_contributions, copied
+ * to out[0..3] = {unresolved ids, fix-up rows, ids the side band left
+ * unresolved, their re-read rows} by copies enqueued on `stream` (nothing
+ * synchronises; `out` should be pinned host memory, valid until the stream
+ * has passed the copies).  Entries a plan has no counter for (no sieve, no
+ * band) are set to 0 before returning.  The library's own plan choice uses
+ * it: a table whose fix-up needed the whole-column re-read for many ids runs
+ * unsieved on the next call (pipelinedp_amd/executor.py, plan feedback). */
+int pdp_bound_stats_async(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,
+                          uint32_t* out, void* stream);
 
 /* Dataset histograms: compute_dataset_histograms
  * (pipeline_dp/dataset_histograms/computing_histograms.py:456-513) over one

@@ -40,6 +40,30 @@ def _worker(args):
     return dt, acc["privacy_id_count"], acc["count"], acc["normalized_sum"]
 
 
+def usable_cpus():
+    """(workers, note): the CPUs this process may run on -- os.cpu_count(),
+    bounded by its affinity mask and by a cgroup CPU quota (cpu.max) when one
+    is set (a GPU box grants each GPU a share of a larger host's cores)."""
+    total = os.cpu_count() or 1
+    n, why = total, []
+    try:
+        aff = len(os.sched_getaffinity(0))
+        if aff < n:
+            n, why = aff, why + [f"affinity {aff}"]
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(quota) // int(period))
+            if q < n:
+                n, why = q, why + [f"cgroup quota {q}"]
+    except (OSError, ValueError):
+        pass
+    return n, f"os.cpu_count() = {total}" + (f", usable {n} ({', '.join(why)})" if why else "")
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -80,4 +104,4 @@ def run(workers, rows_per_worker, privacy_ids_per_worker, partitions, zipf_a, l0
 
 
 if __name__ == "__main__":
-    print(run(min(16, os.cpu_count() or 1), 1_000_000, 10_000, 1_000_000, 1.1, 2, 1, 1.0, 1e-6))
+    print(run(usable_cpus()[0], 1_000_000, 10_000, 1_000_000, 1.1, 2, 1, 1.0, 1e-6))

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 12
+ABI_VERSION = 13
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "pdp_bound_error_flags",
     "pdp_owner_mismatches",
     "pdp_bound_stats_read",
+    "pdp_bound_stats_async",
     "pdp_profiler_enable",
     "pdp_profiler_report",
 )
@@ -250,6 +251,7 @@ def signatures():
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
         "pdp_owner_mismatches": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),
         "pdp_bound_stats_read": (ctypes.c_int, [P(BoundConfig), vp, u64, P(BoundStats), vp]),
+        "pdp_bound_stats_async": (ctypes.c_int, [P(BoundConfig), vp, u64, vp, vp]),
         "pdp_profiler_enable": (ctypes.c_int, [ctypes.c_int]),
         "pdp_profiler_report": (ctypes.c_int, [i32, ctypes.c_char_p, P(ctypes.c_double), P(i64), P(i32)]),
     }

@@ -4237,6 +4237,23 @@ int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uin
   return PDP_OK;
 }
 
+int pdp_bound_stats_async(const pdp_bound_config* cfg, const void* workspace, uint64_t workspace_bytes,
+                          uint32_t* out, void* stream) {
+  if (out == nullptr) return set_error(PDP_E_INVALID, "out is NULL");
+  Plan p;
+  Ws w;
+  const int rc = check_ws(cfg, workspace, workspace_bytes, &p, &w);
+  if (rc != PDP_OK) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const char* ws = (const char*)workspace;
+  const bool bucketed = !pairs_mode(cfg) && p.algorithm == PDP_ALGO_BUCKETED && cfg->n_rows > 0;
+  if (!(bucketed && p.sieve)) out[0] = out[1] = 0;
+  if (!(bucketed && p.band)) out[2] = out[3] = 0;
+  if (bucketed && p.sieve) PDP_HIP_CHECK(hipMemcpyAsync(out, ws + w.sctl, 8, hipMemcpyDeviceToHost, st));
+  if (bucketed && p.band) PDP_HIP_CHECK(hipMemcpyAsync(out + 2, ws + w.sctl2, 8, hipMemcpyDeviceToHost, st));
+  return PDP_OK;
+}
+
 int pdp_reduce_partitions(const pdp_bound_config* cfg, const void* value, void* workspace,
                           uint64_t workspace_bytes, const pdp_partition_accumulators* acc, void* stream) {
   Plan p;

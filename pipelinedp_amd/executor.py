@@ -236,6 +236,11 @@ def bound_plan(n_rows, n_privacy_ids, n_partitions, bounding: BoundingSpec,
     """Execution plan the library resolves for this shard (no device work)."""
     cfg = bound_config(n_rows, n_privacy_ids, n_partitions, bounding, 0, 0, algorithm, merge, key_format, sieve,
                        sieve_band, sieve_threads, bucket_threads)
+    return bound_plan_info(cfg)
+
+
+def bound_plan_info(cfg) -> N.BoundPlanInfo:
+    """pdp_bound_plan of a built pdp_bound_config."""
     info = N.BoundPlanInfo()
     N.check(N.lib().pdp_bound_plan(ctypes.byref(cfg), ctypes.byref(info)), "pdp_bound_plan")
     return info
@@ -267,6 +272,67 @@ class BoundWorkspace:
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
             self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         return self.buf
+
+
+# Plan feedback ("light users").  The threshold sieve leaves
+# privacy ids with fewer than l0 distinct pairs below its threshold for a
+# fix-up; an id short of l0 pairs below the side band's 2t as well needs its
+# rows re-read from the whole privacy-id column, and past RESCAN_BLOOM_MAX such
+# ids that re-read tests every row against an L2-resident bitmap (C3 with 30 %
+# of the ids holding 1-3 rows: 16.4 ms sieved against 12.9 ms unsieved,
+# DESIGN.md §3 "Light users").  Whether a table is like that shows in the
+# fix-up's counters, which pdp_bound_stats_async copies to pinned host memory
+# at the end of every sieved call without synchronising; the next call on the
+# same resident columns reads them (once their copy has completed) and, when
+# the re-read was of the slow kind, runs the auto plan without the sieve.  The
+# choice changes only speed: every plan computes the same result.  Every
+# FEEDBACK_REPROBE-th unsieved call tries the sieve again, so a table whose
+# contents changed in place is re-measured.
+RESCAN_BLOOM_MAX = 8192  # pdp_bound.hip kBloomMaxIds: above it the re-read tests a bitmap per row
+FEEDBACK_REPROBE = 64
+_feedback = {}
+
+
+class _PlanFeedback:
+    def __init__(self):
+        torch = _torch()
+        self.host = torch.zeros(4, dtype=torch.int32, pin_memory=True)  # uint32 counters
+        self.event = None    # recorded after the copies into `host`
+        self.band = False    # the measured plan had the side band
+        self.unsieved = False
+        self.calls = 0
+
+
+def _feedback_key(pid, pk, n, U, P, bounding, row_offset):
+    return (_ptr(pid) or 0, _ptr(pk), n, int(U), int(P), int(bounding.l0), int(bounding.linf),
+            int(bounding.flags), int(row_offset), pk.device.index)
+
+
+def _feedback_sieve(key) -> int:
+    """The sieve argument the auto plan takes for these columns: 0 (auto) or
+    -1 (off) after a measured call whose re-read covered many ids."""
+    fb = _feedback.get(key)
+    if fb is None:
+        return 0
+    if fb.event is not None and fb.event.query():
+        c = fb.host.tolist()
+        slow = (c[2] if fb.band else c[0]) > RESCAN_BLOOM_MAX
+        fb.unsieved = fb.unsieved or slow
+        fb.event = None
+    if not fb.unsieved:
+        return 0
+    fb.calls += 1
+    if fb.calls % FEEDBACK_REPROBE == 0:
+        fb.unsieved = False  # measure the sieved plan again
+        return 0
+    return -1
+
+
+def plan_feedback_state(pid, pk, *, n_privacy_ids, n_partitions, bounding, row_offset=0):
+    """Tests / diagnostics: None, or {"unsieved": bool, "pending": bool}."""
+    fb = _feedback.get(_feedback_key(pid, pk, int(pk.shape[0]), n_privacy_ids, n_partitions, bounding,
+                                     row_offset))
+    return None if fb is None else {"unsieved": fb.unsieved, "pending": fb.event is not None}
 
 
 def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
@@ -308,6 +374,10 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     if bounding.linf < 0 or bounding.linf > N.MAX_LINF:
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")
+    feedback = (sieve == 0 and algorithm == N.ALGO_AUTO and n > 0)
+    fkey = _feedback_key(pid, pk, n, n_privacy_ids, n_partitions, bounding, row_offset) if feedback else None
+    if feedback:
+        sieve = _feedback_sieve(fkey)
     cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
                        key_format, sieve, sieve_band, sieve_threads, bucket_threads)
     nbytes = ctypes.c_uint64(0)
@@ -336,6 +406,21 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     N.check(lib.pdp_reduce_partitions(ctypes.byref(cfg), _ptr(value), _ptr(ws), ws.numel(),
                                       ctypes.byref(_acc_struct(acc)), st),
             "pdp_reduce_partitions")
+    if feedback and sieve == 0:
+        info = bound_plan_info(cfg)
+        if info.sieve:  # a sieved call: its fix-up counters for the next one
+            fb = _feedback.get(fkey)
+            if fb is None:
+                if len(_feedback) > 256:
+                    _feedback.clear()
+                fb = _feedback[fkey] = _PlanFeedback()
+            if fb.event is None:
+                N.check(lib.pdp_bound_stats_async(ctypes.byref(cfg), _ptr(ws), ws.numel(),
+                                                  ctypes.c_void_p(fb.host.data_ptr()), st),
+                        "pdp_bound_stats_async")
+                fb.band = bool(info.band)
+                fb.event = torch.cuda.Event()
+                fb.event.record(stream if stream is not None else torch.cuda.current_stream(device))
     _mark(timer, "end_bound")
     return acc
 

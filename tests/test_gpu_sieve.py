@@ -270,3 +270,51 @@ def test_persistent_level1_loops_over_tiles(device, threads, monkeypatch):
         for band in (0, -1):
             got = _run(device, pid, pk, val, U, P, spec, seed, 4096, band=band, threads=threads)
             _compare(got, want, scale)
+
+
+def test_plan_feedback_runs_light_user_tables_unsieved(device):
+    """Light users: half the privacy ids hold 1-3 rows, so the
+    sieve leaves more than RESCAN_BLOOM_MAX ids for the whole-column re-read.
+    The first auto call runs sieved and leaves its fix-up counters behind
+    (pdp_bound_stats_async); the next call on the same columns runs the
+    unsieved plan.  Both equal the oracle; another table keeps the sieve."""
+    import torch
+    from pipelinedp_amd import executor as X
+    spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    rng = np.random.default_rng(77)
+    heavy, light = 60_000, 60_000
+    U, P = heavy + light, 50_000
+    big = rng.integers(0, heavy, 100 * heavy)
+    small = np.repeat(np.arange(heavy, U), rng.integers(1, 4, light))
+    pid = rng.permutation(np.concatenate([big, small]))
+    n = len(pid)
+    pk = rng.integers(0, P, n)
+    val = rng.random(n) * 10.0
+    assert X.bound_plan(n, U, P, spec).sieve > 0  # the auto plan sieves this shape
+    seed = 4321
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    tp, tk, tv = (torch.as_tensor(a).to(device) for a in (pid, pk, val))
+    ws = X.BoundWorkspace()
+
+    def call():
+        acc = X.bound_and_reduce(tp, tk, tv, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed,
+                                 workspace=ws)
+        torch.cuda.synchronize()
+        return {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+
+    _compare(call(), want, scale)
+    st1 = ws.stats()
+    assert st1["sieve"] > 0 and st1["unresolved_ids"] > X.RESCAN_BLOOM_MAX, st1
+    _compare(call(), want, scale)
+    assert ws.stats()["sieve"] == 0  # measured slow: unsieved now
+    assert X.plan_feedback_state(tp, tk, n_privacy_ids=U, n_partitions=P, bounding=spec)["unsieved"]
+    # a table of heavy users only keeps the sieved plan
+    pid2 = rng.integers(0, heavy, 100 * heavy)
+    pk2 = rng.integers(0, P, len(pid2))
+    val2 = rng.random(len(pid2)) * 10.0
+    t2 = [torch.as_tensor(a).to(device) for a in (pid2, pk2, val2)]
+    for _ in range(2):
+        X.bound_and_reduce(*t2, n_privacy_ids=heavy, n_partitions=P, bounding=spec, seed=seed, workspace=ws)
+        torch.cuda.synchronize()
+        assert ws.stats()["sieve"] > 0

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One-screen summary of a bench.py JSON line (usage: bench_summary.py LOG)."""
+"""One-screen summary of bench.py JSON lines (usage: bench_summary.py LOG [LOG ...])."""
 import json
 import sys
 
@@ -12,11 +12,12 @@ def show(tag, r):
     print("   " + "  ".join(f"{k}={v['ms']:.3f}" for k, v in ks.items() if v["ms"] * v["launches_per_step"] > 0.02))
 
 
-line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
-r = json.loads(line)
-show("main", r)
-if r.get("secondary"):
-    show("secondary", r["secondary"])
-for k in ("cpu_baseline", "cpu_baseline_strong"):
-    if r.get(k):
-        print(f"{k}: {r[k]['value']:.4g} rows/s on {r[k]['cores']} core(s)")
+for path in sys.argv[1:]:
+    line = [l for l in open(path) if l.startswith("{")][-1]
+    r = json.loads(line)
+    show(path, r)
+    if r.get("secondary"):
+        show("secondary", r["secondary"])
+    for k in ("cpu_baseline", "cpu_baseline_strong", "cpu_baseline_c1"):
+        if r.get(k):
+            print(f"{k}: {r[k]['value']:.4g} rows/s on {r[k]['cores']} core(s)  ({r[k]['sample'][-90:]})")

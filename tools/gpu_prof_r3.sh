@@ -23,5 +23,5 @@ for C in FETCH_SIZE WRITE_SIZE "$SQ1" "$SQ2"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $C -d $OUT/$W/pmc$i -o run --output-format csv -- $BENCH > $OUT/${W}_pmc$i.log 2>&1 || { echo "PMC pass $i ($C) failed"; tail -5 $OUT/${W}_pmc$i.log; exit 1; }
 done
-python3 tools/pmc_summary.py $OUT/$W $OUT/${W}_pmc.json "$W n=${ROWS[$W]} " || exit 1
+python3 tools/pmc_summary.py $OUT/$W $OUT/${W}_pmc.json "$W n=${ROWS[$W]} " $OUT/${W}_pmc1.log || exit 1
 echo "prof ok"
