@@ -169,6 +169,10 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the "
                          "n_gpus it sees (tests/test_bench_launcher.py)")
+    ap.add_argument("--share-of", type=int, default=0,
+                    help="c3 at N = 1: one rank's share of an N-GPU run -- rows / N, privacy ids / N, and "
+                         "selection + noise over the rank's P / N partitions after the (omitted) "
+                         "reduce-scatter, as every rank of the N-GPU run does (VERDICT r04 #4)")
     ap.add_argument("--no-api", dest="api", action="store_false",
                     help="skip the public-API timing (DPEngine.aggregate on ColumnarBackend)")
     return ap.parse_args()
@@ -747,10 +751,11 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     from pipelinedp_amd import _native as N
     from pipelinedp_amd import executor as X
     from pipelinedp_amd import parallel
+    share = args.share_of if (workload == "c3" and world == 1 and args.share_of > 1) else 1
     if workload == "c3":
-        total = args.rows or C3["rows"]
+        total = (args.rows or C3["rows"]) // share
         n = total // world
-        U = (args.privacy_ids or C3["privacy_ids"]) // world
+        U = (args.privacy_ids or C3["privacy_ids"]) // share // world
         P = C3["partitions"]
         bounding, selection, ops = build_plan(C3["l0"], C3["linf"])
         pid, pk, value = gen_c3(n, U, P, rank, world, device, 2000, args.small_ids)
@@ -781,6 +786,8 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
                            check_keys=False, **tune)
         mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
+        if share > 1:  # one rank's share: its slice of the partitions (rank 0's)
+            mine = {k: (None if t is None else t[:P_pad // share]) for k, t in mine.items()}
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
                                           seed_noise=seed_base ^ (i * 104729 + 2),
@@ -871,7 +878,9 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                          + (f", {args.small_ids:g} of the privacy ids with 1-3 rows"
                             if workload == "c3" and args.small_ids else "")),
             "rows_per_gpu": n, "privacy_ids_per_gpu": U, "partitions": P,
-            "parallelism": f"rows sharded by privacy_id over {world} GPU(s)",
+            "parallelism": (f"rows sharded by privacy_id over {world} GPU(s)" if share == 1 else
+                            f"ONE RANK'S SHARE of a {share}-GPU run on one GPU: rows and privacy ids / {share}, "
+                            f"selection + noise over P / {share} partitions, the reduce-scatter not included"),
         },
         "roofline": {  # dominant kernel, its OWN algorithmic bytes
             "bound": "hbm", "kernel": dom,
@@ -980,7 +989,7 @@ def main():
         "cpu_baseline_strong": None,
         "cpu_baseline_c1": None,
     }
-    if world == 1 and args.workload == "c3" and not args.no_secondary and not args.rows:
+    if world == 1 and args.workload == "c3" and not args.no_secondary and not args.rows and not args.share_of:
         torch.cuda.empty_cache()
         s = run_workload(args, "c2", 1, 0, device, PMC_SUMMARY["c2"])
         result["secondary"] = {k: s[k] for k in ("value", "ms_per_step", "config", "roofline",

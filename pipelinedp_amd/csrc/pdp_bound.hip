@@ -464,6 +464,10 @@ struct Ws {
   uint64_t total;
 };
 
+// row stride of the per-tile bucket counts (KP.cstride): whole 16-byte rows,
+// so k_gscan_sums reads four buckets per lane
+inline int64_t counts_stride(int64_t n_buckets) { return (n_buckets + 3) & ~(int64_t)3; }
+
 Ws layout(const pdp_bound_config* c, const Plan& p) {
   Ws w{};
   uint64_t off = 0;
@@ -481,7 +485,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.nsum2 = off; off = align256(off + slots * 8);
     }
   } else {
-    const uint64_t n_counts = (uint64_t)p.n_buckets * (uint64_t)p.n_tiles;
+    const uint64_t n_counts = (uint64_t)counts_stride(p.n_buckets) * (uint64_t)p.n_tiles;
     const uint64_t n_chunks = ((uint64_t)p.n_buckets + kScanChunk - 1) / kScanChunk;
     const uint64_t n = (uint64_t)c->n_rows;
     w.counts_tm = off; off = align256(off + n_counts * 4);
@@ -626,6 +630,7 @@ struct KP {  // kernel parameters
   int keys_vec;  // privacy_id / partition_key columns are 16-byte aligned
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
+  int64_t cstride;  // row stride of counts_tm / counts_tm2: n_buckets rounded up to 4 (16-byte rows)
   ClipParams clip;
   int64_t n_slots1;     // level-1 blocks read by level 2 (Plan.n_slots1)
   int l2_group_mult;    // tile groups per level-2 workgroup
@@ -669,6 +674,7 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
   k.row_offset = c->row_offset;
+  k.cstride = counts_stride(p.n_buckets);
   k.clip = ClipParams{c->min_value, c->max_value, c->middle, c->min_sum, c->max_sum, c->flags};
   return k;
 }
@@ -796,7 +802,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(KP kp, const int64_t
     }
   }
   __syncthreads();
-  unsigned* row = counts_tm + (int64_t)blockIdx.x * kp.n_buckets;  // tile-major: coalesced
+  unsigned* row = counts_tm + (int64_t)blockIdx.x * kp.cstride;  // tile-major: coalesced
   for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) row[b] = hist[b];
   // this tile's rows per super-bucket (the level-1 scatter's destinations)
   const int64_t nsub = (int64_t)1 << kp.super_bits;
@@ -827,49 +833,71 @@ __device__ __forceinline__ unsigned tile_count(const unsigned* __restrict__ coun
 
 __device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ counts_tm,
                                                   const unsigned* __restrict__ counts_tm2, int64_t n_tiles,
-                                                  int64_t n_buckets, int64_t b, int64_t t0) {
+                                                  int64_t n_buckets, int64_t cstride, int64_t b, int64_t t0) {
   unsigned v = 0;
 #pragma unroll
   for (int j = 0; j < kScanTiles; ++j) {
     const int64_t t = t0 + j;
-    if (t < n_tiles && b < n_buckets) v += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
+    if (t < n_tiles && b < n_buckets) v += tile_count(counts_tm, counts_tm2, t * cstride + b);
   }
   return v;
 }
 
+__device__ __forceinline__ uint4 add4(uint4 a, uint4 b) { return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
 // csum[chunk][b] = rows of bucket b in the chunk's tiles; gsum (nullable):
-// gsum[g][b] = rows of bucket b in the kL2GroupTiles tiles of group g
+// gsum[g][b] = rows of bucket b in the kL2GroupTiles tiles of group g.
+// Four buckets per lane (16-byte loads of the count rows, whose stride
+// cstride is a multiple of 4), a wave's kScanTiles loads in flight together:
+// the rows are read as 1 KiB pieces instead of 256-byte ones (C3: 298 MB of
+// counts)
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* __restrict__ counts_tm,
                                                                  const unsigned* __restrict__ counts_tm2,
-                                                                 int64_t n_tiles, int64_t n_buckets,
+                                                                 int64_t n_tiles, int64_t n_buckets, int64_t cstride,
                                                                  unsigned* __restrict__ csum,
                                                                  unsigned* __restrict__ gsum) {
-  __shared__ unsigned part[kScanWaves][64];
+  static_assert(kScanTiles % kL2GroupTiles == 0, "group sums end inside a wave's tiles");
+  __shared__ uint4 part[kScanWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t b0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  if (gsum == nullptr) {
-    part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
-  } else {
-    unsigned v = 0, gv = 0;
+  const bool in = b0 < n_buckets;  // then b0 + 3 < cstride: the load stays in the row
+  uint4 x[kScanTiles];
 #pragma unroll
-    for (int j = 0; j < kScanTiles; ++j) {
-      const int64_t t = t0 + j;
-      if (t < n_tiles && b < n_buckets) gv += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
-      if ((j + 1) % kL2GroupTiles == 0) {
-        if (t0 + j + 1 - kL2GroupTiles < n_tiles && b < n_buckets)
-          gsum[((t0 + j + 1) / kL2GroupTiles - 1) * n_buckets + b] = gv;
-        v += gv;
-        gv = 0;
-      }
+  for (int j = 0; j < kScanTiles; ++j) {
+    const int64_t t = t0 + j;
+    x[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (in && t < n_tiles) {
+      x[j] = *reinterpret_cast<const uint4*>(counts_tm + t * cstride + b0);
+      if (counts_tm2 != nullptr) x[j] = add4(x[j], *reinterpret_cast<const uint4*>(counts_tm2 + t * cstride + b0));
     }
-    part[w][lane] = v;
   }
+  uint4 v = make_uint4(0u, 0u, 0u, 0u), gv = v;
+#pragma unroll
+  for (int j = 0; j < kScanTiles; ++j) {
+    gv = add4(gv, x[j]);
+    if ((j + 1) % kL2GroupTiles == 0) {
+      if (gsum != nullptr && in && t0 + j + 1 - kL2GroupTiles < n_tiles) {
+        unsigned* g = gsum + ((t0 + j + 1) / kL2GroupTiles - 1) * n_buckets + b0;
+        g[0] = gv.x;
+        if (b0 + 1 < n_buckets) g[1] = gv.y;
+        if (b0 + 2 < n_buckets) g[2] = gv.z;
+        if (b0 + 3 < n_buckets) g[3] = gv.w;
+      }
+      v = add4(v, gv);
+      gv = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  part[w][lane] = v;
   __syncthreads();
-  if (w == 0 && b < n_buckets) {
-    unsigned v = 0;
-    for (int k = 0; k < kScanWaves; ++k) v += part[k][lane];
-    csum[(int64_t)blockIdx.y * n_buckets + b] = v;
+  if (w == 0 && in) {
+    uint4 s = make_uint4(0u, 0u, 0u, 0u);
+    for (int k = 0; k < kScanWaves; ++k) s = add4(s, part[k][lane]);
+    unsigned* c = csum + (int64_t)blockIdx.y * n_buckets + b0;
+    c[0] = s.x;
+    if (b0 + 1 < n_buckets) c[1] = s.y;
+    if (b0 + 2 < n_buckets) c[2] = s.z;
+    if (b0 + 3 < n_buckets) c[3] = s.w;
   }
 }
 
@@ -911,13 +939,14 @@ __global__ void __launch_bounds__(kBlock) k_gscan_groups(const unsigned* __restr
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigned* __restrict__ counts_tm,
                                                                     const unsigned* __restrict__ counts_tm2,
                                                                     int64_t n_tiles, int64_t n_buckets,
+                                                                    int64_t cstride,
                                                                     const unsigned* __restrict__ cpre,
                                                                     unsigned* __restrict__ gcur) {
   __shared__ unsigned part[kScanWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t b = (int64_t)blockIdx.x * 64 + lane;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, b, t0);
+  part[w][lane] = tile_slab_sum(counts_tm, counts_tm2, n_tiles, n_buckets, cstride, b, t0);
   __syncthreads();
   if (b >= n_buckets || t0 >= n_tiles) return;
   unsigned run = cpre[(int64_t)blockIdx.y * n_buckets + b];
@@ -926,7 +955,7 @@ __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_cursors(const unsigne
     const int64_t t = t0 + j;
     if (t >= n_tiles) break;
     if (t % kL2GroupTiles == 0) gcur[(t / kL2GroupTiles) * n_buckets + b] = run;
-    run += tile_count(counts_tm, counts_tm2, t * n_buckets + b);
+    run += tile_count(counts_tm, counts_tm2, t * cstride + b);
   }
 }
 
@@ -1508,18 +1537,18 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
     __syncthreads();
     if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
     if (split && c0 - t0 == (kStagesPerTile / 2 - 1) * kL1Rows) {  // first half tile done
-      flush(counts_tm + t * kp.n_buckets);
+      flush(counts_tm + t * kp.cstride);
       __syncthreads();
     }
   }
   __syncthreads();
   // tile-major rows: coalesced.  Counts of a half tile never reach 2^16
   if (split) {
-    flush(counts_tm2 + t * kp.n_buckets);
+    flush(counts_tm2 + t * kp.cstride);
   } else {
-    flush(counts_tm + t * kp.n_buckets);
+    flush(counts_tm + t * kp.cstride);
     if constexpr (U16)
-      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.n_buckets + b] = 0;
+      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.cstride + b] = 0;
   }
 }
 
@@ -1708,11 +1737,11 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     }
     __syncthreads();
     if (split) {
-      flush_counts(counts_tm2 + t * kp.n_buckets);
+      flush_counts(counts_tm2 + t * kp.cstride);
     } else {
-      flush_counts(counts_tm + t * kp.n_buckets);
+      flush_counts(counts_tm + t * kp.cstride);
       if constexpr (U16)
-        for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.n_buckets + b] = 0;
+        for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.cstride + b] = 0;
     }
     __syncthreads();
   };
@@ -1858,7 +1887,7 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       else __syncthreads();  // every thread has read `fill` before the next chunk's appends
       if constexpr (!kEarly) prefetch();
       if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
-        flush_counts(counts_tm + t * kp.n_buckets);
+        flush_counts(counts_tm + t * kp.cstride);
         __syncthreads();
       }
     };
@@ -2795,7 +2824,9 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
       wave_lds_fence();
     }
   };
-  constexpr int KU = 4;  // entries per lane and trip, loaded together
+  // entries per lane and trip, loaded together (8: at an N = 8 rank's share a
+  // block sees ~2 tiles, so its trips are latency rounds, not a stream)
+  constexpr int KU = 8;
   const int64_t w0 = (int64_t)(threadIdx.x >> 6) * 64 * KU;
   auto run = [&](auto bloom_tag) {
     constexpr bool BLOOM = decltype(bloom_tag)::value;
@@ -2896,6 +2927,10 @@ __global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __
 // launch left unresolved stay unresolved -- none of their pairs lies below t2
 // -- so they are copied to the second bitmap and list (what k_bucket_bound's
 // mark(false) does for an empty bucket).  blist[0] is zeroed by the caller.
+// Grid (buckets / kBlock, kFixRunRows): blockIdx.y = 0 lists and marks,
+// every y writes its share of the run-table rows (consecutive threads:
+// consecutive columns of one row)
+constexpr int kFixRunRows = 16;
 __global__ void __launch_bounds__(kBlock) k_fix_buckets(KP kp, const unsigned* __restrict__ fix_start,
                                                         unsigned* __restrict__ runs, int64_t run_stride,
                                                         unsigned* __restrict__ blist,
@@ -2905,12 +2940,14 @@ __global__ void __launch_bounds__(kBlock) k_fix_buckets(KP kp, const unsigned* _
                                                         unsigned* __restrict__ sctl2) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= kp.n_buckets) return;
-  if (fix_start[b + 1] > fix_start[b]) {
+  const bool empty = fix_start[b + 1] == fix_start[b];
+  if (runs != nullptr && empty)
+    for (int r = blockIdx.y; r <= kp.n_ranges; r += gridDim.y) runs[(int64_t)r * run_stride + b] = 0;
+  if (blockIdx.y != 0) return;
+  if (!empty) {
     blist[1 + atomicAdd(blist, 1u)] = (unsigned)b;
     return;
   }
-  if (runs != nullptr)  // consecutive threads: consecutive columns of each row
-    for (int r = 0; r <= kp.n_ranges; ++r) runs[(int64_t)r * run_stride + b] = 0;
   if (prev == nullptr) return;
   const int64_t id0 = b << kp.bucket_bits;  // bucket_bits >= 6: whole u64 words
   for (int64_t w = 0; w < ((int64_t)1 << kp.bucket_bits) / 64; ++w) {
@@ -3654,7 +3691,8 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     // empty ones' runs and marks) and run on 512 threads (the kernel sizes its
     // queues from blockDim)
     PDP_PROF_BEGIN("k_fix_buckets", st);
-    hipLaunchKernelGGL(k_fix_buckets, dim3(grid_for(p.n_buckets)), dim3(kBlock), 0, st, kf, (const unsigned*)fix_cnt,
+    hipLaunchKernelGGL(k_fix_buckets, dim3(grid_for(p.n_buckets), kFixRunRows), dim3(kBlock), 0, st, kf,
+                       (const unsigned*)fix_cnt,
                        p.merge == PDP_MERGE_RANGES ? fr.runs : nullptr, fr.run_stride, blist,
                        mark ? mk.prev : nullptr, mk.bits, mk.list, mk.sctl);
     PDP_PROF_END(st);
@@ -3886,13 +3924,13 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
-  const int64_t n_bblk = (p.n_buckets + 63) / 64;
+  const int64_t n_bblk4 = (p.n_buckets + 255) / 256;  // k_gscan_sums: four buckets per lane
   const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
   unsigned* csum = (unsigned*)(ws + w.csum);
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
-  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, csum, gcur);
+  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk4, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
+                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, kp.cstride, csum, gcur);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -3995,12 +4033,13 @@ int launch_offsets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   PDP_HIP_CHECK(hipGetLastError());
   // rows per bucket (and, with two levels, the level-2 cursors at tile-group starts)
   const int64_t n_bblk = (p.n_buckets + 63) / 64;
+  const int64_t n_bblk4 = (p.n_buckets + 255) / 256;
   const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
   unsigned* csum = (unsigned*)(ws + w.csum);
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
-  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, csum, (unsigned*)nullptr);
+  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk4, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
+                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, kp.cstride, csum, (unsigned*)nullptr);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -4011,7 +4050,8 @@ int launch_offsets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   if (p.super_bits > 0) {
     PDP_PROF_BEGIN("k_gscan_cursors", st);
     hipLaunchKernelGGL(k_gscan_cursors, dim3((unsigned)n_bblk, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
-                       counts_tm, (const unsigned*)nullptr, p.n_tiles, p.n_buckets, (const unsigned*)csum, gcur);
+                       counts_tm, (const unsigned*)nullptr, p.n_tiles, p.n_buckets, kp.cstride, (const unsigned*)csum,
+                       gcur);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }

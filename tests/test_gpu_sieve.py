@@ -282,7 +282,7 @@ def test_plan_feedback_runs_light_user_tables_unsieved(device):
     from pipelinedp_amd import executor as X
     spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
     rng = np.random.default_rng(77)
-    heavy, light = 60_000, 60_000
+    heavy, light = 80_000, 80_000  # > 64 buckets of 2,048 ids: two partition levels, the sieve's precondition
     U, P = heavy + light, 50_000
     big = rng.integers(0, heavy, 100 * heavy)
     small = np.repeat(np.arange(heavy, U), rng.integers(1, 4, light))
@@ -310,11 +310,11 @@ def test_plan_feedback_runs_light_user_tables_unsieved(device):
     assert ws.stats()["sieve"] == 0  # measured slow: unsieved now
     assert X.plan_feedback_state(tp, tk, n_privacy_ids=U, n_partitions=P, bounding=spec)["unsieved"]
     # a table of heavy users only keeps the sieved plan
-    pid2 = rng.integers(0, heavy, 100 * heavy)
+    pid2 = rng.integers(0, U, 100 * U)
     pk2 = rng.integers(0, P, len(pid2))
     val2 = rng.random(len(pid2)) * 10.0
     t2 = [torch.as_tensor(a).to(device) for a in (pid2, pk2, val2)]
     for _ in range(2):
-        X.bound_and_reduce(*t2, n_privacy_ids=heavy, n_partitions=P, bounding=spec, seed=seed, workspace=ws)
+        X.bound_and_reduce(*t2, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, workspace=ws)
         torch.cuda.synchronize()
         assert ws.stats()["sieve"] > 0
