@@ -454,6 +454,7 @@ struct Ws {
   // their rescan's per-bucket counts / cursors
   uint64_t band, band_cnt, unres2_bits, unres2_list, sctl2, fix_cnt2, fix_cur2;
   uint64_t fix_blist;  // fix-up bucket launches: {count, buckets holding fix-up rows...}
+  uint64_t tile_over;  // tile-local level 1: per tile, the bucket holding all 65,536 of its rows (else ~0)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
   uint64_t rr_items, rr_count;  // range-reduce work items (uint4) and their count
@@ -464,9 +465,10 @@ struct Ws {
   uint64_t total;
 };
 
-// row stride of the per-tile bucket counts (KP.cstride): whole 16-byte rows,
-// so k_gscan_sums reads four buckets per lane
-inline int64_t counts_stride(int64_t n_buckets) { return (n_buckets + 3) & ~(int64_t)3; }
+// row stride of the per-tile bucket counts in buckets (KP.cstride): whole
+// 16-byte rows of u16 pairs (tile-local level 1) or u32 counts, so
+// k_gscan_sums reads eight or four buckets per lane
+inline int64_t counts_stride(int64_t n_buckets) { return (n_buckets + 7) & ~(int64_t)7; }
 
 Ws layout(const pdp_bound_config* c, const Plan& p) {
   Ws w{};
@@ -491,6 +493,7 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
     w.counts_tm = off; off = align256(off + n_counts * 4);
     const bool u16 = p.hist_u16 != 0;
     if (p.l1_local && u16) { w.counts_tm2 = off; off = align256(off + n_counts * 4); }
+    w.tile_over = off; off = align256(off + (uint64_t)p.n_tiles * 4);
     w.counts = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);  // bucket starts
     w.chunk_sums = off; off = align256(off + (n_chunks + 1) * 4);
     const uint64_t n_sc = ((uint64_t)p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
@@ -630,7 +633,7 @@ struct KP {  // kernel parameters
   int keys_vec;  // privacy_id / partition_key columns are 16-byte aligned
   uint64_t pk_mask, seed, row_seed;
   int64_t row_offset;
-  int64_t cstride;  // row stride of counts_tm / counts_tm2: n_buckets rounded up to 4 (16-byte rows)
+  int64_t cstride;  // row stride of counts_tm / counts_tm2 in buckets: n_buckets rounded up to 8
   ClipParams clip;
   int64_t n_slots1;     // level-1 blocks read by level 2 (Plan.n_slots1)
   int l2_group_mult;    // tile groups per level-2 workgroup
@@ -843,61 +846,79 @@ __device__ __forceinline__ unsigned tile_slab_sum(const unsigned* __restrict__ c
   return v;
 }
 
-__device__ __forceinline__ uint4 add4(uint4 a, uint4 b) { return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-
 // csum[chunk][b] = rows of bucket b in the chunk's tiles; gsum (nullable):
 // gsum[g][b] = rows of bucket b in the kL2GroupTiles tiles of group g.
-// Four buckets per lane (16-byte loads of the count rows, whose stride
-// cstride is a multiple of 4), a wave's kScanTiles loads in flight together:
-// the rows are read as 1 KiB pieces instead of 256-byte ones (C3: 298 MB of
-// counts)
+// PACKED16: the count rows are u16 pairs (tile-local level 1,
+// flush_counts16: cstride / 2 words per row, tile_over adds 65,536 back),
+// eight buckets per lane; else u32 rows of cstride, four per lane.  16-byte
+// loads, a wave's kScanTiles rows in flight together (C3: 149 MB of counts)
+template <bool PACKED16>
 __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* __restrict__ counts_tm,
                                                                  const unsigned* __restrict__ counts_tm2,
+                                                                 const unsigned* __restrict__ tile_over,
                                                                  int64_t n_tiles, int64_t n_buckets, int64_t cstride,
                                                                  unsigned* __restrict__ csum,
                                                                  unsigned* __restrict__ gsum) {
   static_assert(kScanTiles % kL2GroupTiles == 0, "group sums end inside a wave's tiles");
-  __shared__ uint4 part[kScanWaves][64];
+  constexpr int V = PACKED16 ? 8 : 4;  // buckets per lane
+  __shared__ unsigned part[kScanWaves][V][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t b0 = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const int64_t b0 = ((int64_t)blockIdx.x * 64 + lane) * V;
   const int64_t t0 = (int64_t)blockIdx.y * kScanChunkTiles + (int64_t)w * kScanTiles;
-  const bool in = b0 < n_buckets;  // then b0 + 3 < cstride: the load stays in the row
+  const int64_t row = PACKED16 ? cstride / 2 : cstride;  // u32 words per row
+  const int64_t col = PACKED16 ? b0 / 2 : b0;
+  const bool in = b0 < n_buckets;  // then the 16-byte load stays inside the row
   uint4 x[kScanTiles];
 #pragma unroll
   for (int j = 0; j < kScanTiles; ++j) {
     const int64_t t = t0 + j;
     x[j] = make_uint4(0u, 0u, 0u, 0u);
     if (in && t < n_tiles) {
-      x[j] = *reinterpret_cast<const uint4*>(counts_tm + t * cstride + b0);
-      if (counts_tm2 != nullptr) x[j] = add4(x[j], *reinterpret_cast<const uint4*>(counts_tm2 + t * cstride + b0));
+      x[j] = *reinterpret_cast<const uint4*>(counts_tm + t * row + col);
+      if (counts_tm2 != nullptr) {
+        const uint4 y = *reinterpret_cast<const uint4*>(counts_tm2 + t * row + col);
+        x[j] = make_uint4(x[j].x + y.x, x[j].y + y.y, x[j].z + y.z, x[j].w + y.w);  // halves < 2^15: no carry
+      }
     }
   }
-  uint4 v = make_uint4(0u, 0u, 0u, 0u), gv = v;
+  unsigned v[V], gv[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) v[k] = gv[k] = 0u;
 #pragma unroll
   for (int j = 0; j < kScanTiles; ++j) {
-    gv = add4(gv, x[j]);
+    const unsigned e[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+#pragma unroll
+    for (int k = 0; k < V; ++k) gv[k] += PACKED16 ? ((e[k / 2] >> (16 * (k & 1))) & 0xFFFFu) : e[k];
+    if (PACKED16 && tile_over != nullptr && in && t0 + j < n_tiles) {
+      const unsigned o = tile_over[t0 + j];  // the bucket with all 65,536 rows, or ~0
+#pragma unroll
+      for (int k = 0; k < V; ++k) gv[k] += (o == (unsigned)(b0 + k)) ? 65536u : 0u;
+    }
     if ((j + 1) % kL2GroupTiles == 0) {
       if (gsum != nullptr && in && t0 + j + 1 - kL2GroupTiles < n_tiles) {
         unsigned* g = gsum + ((t0 + j + 1) / kL2GroupTiles - 1) * n_buckets + b0;
-        g[0] = gv.x;
-        if (b0 + 1 < n_buckets) g[1] = gv.y;
-        if (b0 + 2 < n_buckets) g[2] = gv.z;
-        if (b0 + 3 < n_buckets) g[3] = gv.w;
+#pragma unroll
+        for (int k = 0; k < V; ++k)
+          if (b0 + k < n_buckets) g[k] = gv[k];
       }
-      v = add4(v, gv);
-      gv = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        v[k] += gv[k];
+        gv[k] = 0u;
+      }
     }
   }
-  part[w][lane] = v;
+#pragma unroll
+  for (int k = 0; k < V; ++k) part[w][k][lane] = v[k];
   __syncthreads();
   if (w == 0 && in) {
-    uint4 s = make_uint4(0u, 0u, 0u, 0u);
-    for (int k = 0; k < kScanWaves; ++k) s = add4(s, part[k][lane]);
     unsigned* c = csum + (int64_t)blockIdx.y * n_buckets + b0;
-    c[0] = s.x;
-    if (b0 + 1 < n_buckets) c[1] = s.y;
-    if (b0 + 2 < n_buckets) c[2] = s.z;
-    if (b0 + 3 < n_buckets) c[3] = s.w;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      unsigned sum = 0;
+      for (int q = 0; q < kScanWaves; ++q) sum += part[q][k][lane];
+      if (b0 + k < n_buckets) c[k] = sum;
+    }
   }
 }
 
@@ -1422,6 +1443,32 @@ __device__ __forceinline__ void copy_block(K* __restrict__ dst, const K* src, un
   for (unsigned k = nv * V + threadIdx.x; k < total; k += blockDim.x) dst[k] = src[k];
 }
 
+// The tile-local level 1's bucket counts leave LDS as u16 pairs per u32
+// word (rows of kp.cstride / 2 words; bucket 2w in the low half): half the
+// bytes of u32 counts for level 1 to write and k_gscan_sums to read.  The
+// LDS counts are u32 per bucket, or (U16) already u16 pairs of a half tile
+// (< 2^15 each).  A u32 count of 65,536 -- every row of the tile in one
+// bucket -- is stored as 0 with the bucket in tile_over[t], which the scan
+// adds back (tile_over is all ones otherwise; the caller sets it so).
+template <bool U16>
+__device__ __forceinline__ void flush_counts16(unsigned* __restrict__ bh, int64_t n_buckets,
+                                               unsigned* __restrict__ dst, unsigned* __restrict__ over, int th) {
+  const int64_t n_pairs = (n_buckets + 1) / 2;
+  for (int64_t w = threadIdx.x; w < n_pairs; w += th) {
+    if constexpr (U16) {
+      dst[w] = bh[w];
+      bh[w] = 0;
+    } else {
+      const unsigned v0 = bh[2 * w], v1 = 2 * w + 1 < n_buckets ? bh[2 * w + 1] : 0u;
+      bh[2 * w] = 0;
+      if (2 * w + 1 < n_buckets) bh[2 * w + 1] = 0;
+      dst[w] = (v0 & 0xFFFFu) | (v1 << 16);
+      if (v0 > 0xFFFFu) *over = (unsigned)(2 * w);
+      if (v1 > 0xFFFFu) *over = (unsigned)(2 * w + 1);
+    }
+  }
+}
+
 template <int FMT, bool U16>
 __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const int64_t* __restrict__ pid,
                                                                    const int64_t* __restrict__ pk,
@@ -1430,7 +1477,8 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
                                                                    unsigned* __restrict__ counts_tm2,
                                                                    uint16_t* __restrict__ soff,
                                                                    L1Key<FMT>* __restrict__ keys1,
-                                                                   unsigned* __restrict__ rows1, unsigned* err) {
+                                                                   unsigned* __restrict__ rows1, unsigned* err,
+                                                                   unsigned* __restrict__ tile_over) {
   using K = L1Key<FMT>;
   constexpr bool ROWS = !kPackedL1<FMT>;
   extern __shared__ unsigned long long stage_raw[];
@@ -1442,19 +1490,10 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
   const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
   for (int64_t b = threadIdx.x; b < n_words; b += blockDim.x) bh[b] = 0;
   __syncthreads();
-  auto flush = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
-    for (int64_t wd = threadIdx.x; wd < n_words; wd += blockDim.x) {
-      const unsigned v = bh[wd];
-      bh[wd] = 0;
-      if constexpr (U16) {
-        dst[2 * wd] = v & 0xFFFFu;
-        if (2 * wd + 1 < kp.n_buckets) dst[2 * wd + 1] = v >> 16;
-      } else {
-        dst[wd] = v;
-      }
-    }
-  };
   const int64_t t = blockIdx.x;
+  auto flush = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
+    flush_counts16<U16>(bh, kp.n_buckets, dst, tile_over + t, blockDim.x);
+  };
   const int nd = (int)kp.n_supers;
   const int64_t t0 = t * kTileRows;
   const int64_t t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
@@ -1537,18 +1576,18 @@ __global__ void __launch_bounds__(kL1Threads)  k_scatter_l1_local(KP kp, const i
     __syncthreads();
     if (c0 + kL1Rows < t1) load(c0 + kL1Rows, u, k);
     if (split && c0 - t0 == (kStagesPerTile / 2 - 1) * kL1Rows) {  // first half tile done
-      flush(counts_tm + t * kp.cstride);
+      flush(counts_tm + t * (kp.cstride / 2));
       __syncthreads();
     }
   }
   __syncthreads();
   // tile-major rows: coalesced.  Counts of a half tile never reach 2^16
   if (split) {
-    flush(counts_tm2 + t * kp.cstride);
+    flush(counts_tm2 + t * (kp.cstride / 2));
   } else {
-    flush(counts_tm + t * kp.cstride);
+    flush(counts_tm + t * (kp.cstride / 2));
     if constexpr (U16)
-      for (int64_t b = threadIdx.x; b < kp.n_buckets; b += blockDim.x) counts_tm2[t * kp.cstride + b] = 0;
+      for (int64_t w = threadIdx.x; w < kp.cstride / 2; w += blockDim.x) counts_tm2[t * (kp.cstride / 2) + w] = 0;
   }
 }
 
@@ -1587,7 +1626,8 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
                                                          L1Key<FMT>* __restrict__ keys1,
                                                          unsigned* __restrict__ rows1, unsigned* err,
                                                          unsigned long long* __restrict__ band,
-                                                         unsigned* __restrict__ band_cnt) {
+                                                         unsigned* __restrict__ band_cnt,
+                                                         unsigned* __restrict__ tile_over) {
   using K = L1Key<FMT>;
   using SS = SieveShape<TH>;
   constexpr bool ROWS = !kPackedL1<FMT>;
@@ -1610,23 +1650,14 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     bfill = 0;
   }
   __syncthreads();
-  auto flush_counts = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
-    for (int64_t wd = threadIdx.x; wd < n_words; wd += TH) {
-      const unsigned v = bh[wd];
-      bh[wd] = 0;
-      if constexpr (U16) {
-        dst[2 * wd] = v & 0xFFFFu;
-        if (2 * wd + 1 < kp.n_buckets) dst[2 * wd + 1] = v >> 16;
-      } else {
-        dst[wd] = v;
-      }
-    }
-  };
   // persistent: workgroup g takes tiles g, g + G, ... (G = gridDim.x, about
   // one per CU), so a tile's last chunks prefetch the next tile's first ones
   // and no tile starts with its loads' latency exposed
   const int nd = (int)kp.n_supers;
   int64_t t = 0, t0 = 0, t1 = 0, next_t0 = -1;  // the tile; the next one's first row (-1: none)
+  auto flush_counts = [&](unsigned* __restrict__ dst) {  // after a barrier; leaves bh zeroed
+    flush_counts16<U16>(bh, kp.n_buckets, dst, tile_over + t, TH);
+  };
   const int mid_bits = kp.bucket_bits + kp.super_bits;
   const uint32_t t32 = kp.sieve_t32;
   const int lane = threadIdx.x & 63;
@@ -1737,11 +1768,11 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     }
     __syncthreads();
     if (split) {
-      flush_counts(counts_tm2 + t * kp.cstride);
+      flush_counts(counts_tm2 + t * (kp.cstride / 2));
     } else {
-      flush_counts(counts_tm + t * kp.cstride);
+      flush_counts(counts_tm + t * (kp.cstride / 2));
       if constexpr (U16)
-        for (int64_t b = threadIdx.x; b < kp.n_buckets; b += TH) counts_tm2[t * kp.cstride + b] = 0;
+        for (int64_t w = threadIdx.x; w < kp.cstride / 2; w += TH) counts_tm2[t * (kp.cstride / 2) + w] = 0;
     }
     __syncthreads();
   };
@@ -1887,7 +1918,7 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
       else __syncthreads();  // every thread has read `fill` before the next chunk's appends
       if constexpr (!kEarly) prefetch();
       if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
-        flush_counts(counts_tm + t * kp.cstride);
+        flush_counts(counts_tm + t * (kp.cstride / 2));
         __syncthreads();
       }
     };
@@ -2068,7 +2099,7 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
     KO x[NI];
     unsigned r[NI];
     int d[NI];
-    constexpr int H = NI / 2;
+    constexpr int H = NI / 2;  // (all NI in one round spills 21-33 VGPRs: level 2 +37 %, profiles/r05/ab/ab9)
 #pragma unroll
     for (int h = 0; h < NI; h += H) {
       KI raw[H];
@@ -3872,6 +3903,8 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
+  unsigned* tile_over = (unsigned*)(ws + w.tile_over);  // all ones unless a tile's rows are all one bucket's
+  PDP_HIP_CHECK(hipMemsetAsync(tile_over, 0xFF, (uint64_t)p.n_tiles * 4, st));
   unsigned* sbase = p.sieve ? (unsigned*)(ws + w.sbase) : nullptr;
   K1* keys1 = (K1*)(ws + w.keys1);
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
@@ -3891,7 +3924,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
       unsigned* band_cnt = p.band ? (unsigned*)(ws + w.band_cnt) : nullptr;
       void* args1[] = {(void*)&kp,   (void*)&pid,   (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
                        (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err,
-                       (void*)&band, (void*)&band_cnt};
+                       (void*)&band, (void*)&band_cnt, (void*)&tile_over};
       PDP_PROF_BEGIN("k_sieve_l1", st);
       // persistent: as many workgroups as fit at once (one per CU at 1,024
       // threads, two at 512), each looping over its tiles
@@ -3915,7 +3948,8 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
     const void* l1 = u16 ? (const void*)k_scatter_l1_local<FMT, true> : (const void*)k_scatter_l1_local<FMT, false>;
     PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
     void* args1[] = {(void*)&kp,         (void*)&pid,  (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
-                     (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err};
+                     (void*)&counts_tm2, (void*)&soff, (void*)&keys1, (void*)&rows1,   (void*)&err,
+                     (void*)&tile_over};
     PDP_PROF_BEGIN("k_scatter_l1", st);
     // (one workgroup per tile: a persistent form with the next stage's loads
     // issued early measured the same at C5, 3.04 vs 3.06 ms -- the 2:1
@@ -3924,13 +3958,14 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
   }
-  const int64_t n_bblk4 = (p.n_buckets + 255) / 256;  // k_gscan_sums: four buckets per lane
+  const int64_t n_bblk8 = (p.n_buckets + 511) / 512;  // k_gscan_sums<true>: eight buckets per lane
   const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
   unsigned* csum = (unsigned*)(ws + w.csum);
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
-  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk4, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)counts_tm2, p.n_tiles, p.n_buckets, kp.cstride, csum, gcur);
+  hipLaunchKernelGGL(k_gscan_sums<true>, dim3((unsigned)n_bblk8, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
+                     (const unsigned*)counts_tm, (const unsigned*)counts_tm2, (const unsigned*)tile_over, p.n_tiles,
+                     p.n_buckets, kp.cstride, csum, gcur);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);
@@ -4038,8 +4073,9 @@ int launch_offsets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   unsigned* csum = (unsigned*)(ws + w.csum);
   unsigned* gcur = (unsigned*)(ws + w.gcur);
   PDP_PROF_BEGIN("k_gscan_sums", st);
-  hipLaunchKernelGGL(k_gscan_sums, dim3((unsigned)n_bblk4, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st, counts_tm,
-                     (const unsigned*)nullptr, p.n_tiles, p.n_buckets, kp.cstride, csum, (unsigned*)nullptr);
+  hipLaunchKernelGGL(k_gscan_sums<false>, dim3((unsigned)n_bblk4, (unsigned)n_sc), dim3(64 * kScanWaves), 0, st,
+                     (const unsigned*)counts_tm, (const unsigned*)nullptr, (const unsigned*)nullptr, p.n_tiles,
+                     p.n_buckets, kp.cstride, csum, (unsigned*)nullptr);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
   PDP_PROF_BEGIN("k_gscan_chunks", st);

@@ -318,3 +318,32 @@ def test_plan_feedback_runs_light_user_tables_unsieved(device):
         X.bound_and_reduce(*t2, n_privacy_ids=U, n_partitions=P, bounding=spec, seed=seed, workspace=ws)
         torch.cuda.synchronize()
         assert ws.stats()["sieve"] > 0
+
+
+@pytest.mark.parametrize("sieve", [-1, 32768], ids=["tile-local", "sieve"])
+def test_tile_with_every_row_in_one_bucket(device, sieve):
+    """Level 1 keeps a tile's bucket counts as u16 (flush_counts16); a bucket
+    holding all 65,536 rows of a tile (counted 65,536, stored as 0 with the
+    bucket in tile_over) must still get all of them.  Tile 0 here: every row
+    from the first 2,048 privacy ids (bucket 0 at b = 11), and with the sieve
+    every such row a candidate (pair hash below t = 1/2); equal to the oracle."""
+    from pipelinedp_amd import executor as X
+    spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    U, P = 300_000, 4096
+    seed = 9191
+    plan = X.bound_plan(3 * 65536, U, P, spec, sieve=sieve)
+    assert plan.bucket_bits == 11 and (plan.sieve > 0) == (sieve > 0)
+    rng = np.random.default_rng(5)
+    cu = rng.integers(0, 2048, 200_000)
+    ck = rng.integers(0, P, 200_000)
+    if sieve > 0:
+        low = O.pair_hash(seed, cu, ck) < np.uint32(1 << 31)
+        cu, ck = cu[low], ck[low]
+    idx = rng.integers(0, len(cu), 65536)
+    pid = np.concatenate([cu[idx], rng.integers(0, U, 2 * 65536 + 321)])
+    pk = np.concatenate([ck[idx], rng.integers(0, P, 2 * 65536 + 321)])
+    n = len(pid)
+    val = rng.random(n) * 10.0
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve), want, scale)
