@@ -606,9 +606,10 @@ def run_hist_workload(args, world, rank, device):
            "k_hb_l2": 32.0 * n, "k_hb_pairs": 16.0 * n,
            # the per-bucket pair pass: 16-byte records in, a 16-byte (partition,
            # rows, sum) record out per distinct pair; the range pass and the
-           # float histograms read those once; per-id / per-partition stats
+           # float histogram's two passes (counts + sums, maxima) read those
+           # once each; per-id / per-partition stats
            "k_hb_pid_pairs": 16.0 * n + 16.0 * pairs, "k_hb_prange": 16.0 * pairs,
-           "k_h_float": 16.0 * pairs, "k_h_ids": 16.0 * (U + P)}
+           "k_h_float": 16.0 * pairs, "k_h_float_max": 16.0 * pairs, "k_h_ids": 16.0 * (U + P)}
     traffic, traffic_src, traffic_refused = load_pmc(PMC_SUMMARY["hist"], "hist", n, world)
     table = {}
     for k, ms in kernel_ms.items():

@@ -23,8 +23,8 @@
 //               :346-370), bit-exact: separate fp64 multiply and add
 //   k_h_float   Linf-sum and sum-per-partition histograms (bisect_right over
 //               the lowers, _bin_lower_index :50-59); the pair histogram's
-//               counts and sums are privatised in LDS (120 KB per workgroup),
-//               bin maxima use a read-filtered atomicMax
+//               counts and sums are privatised in LDS (120 KB per workgroup);
+//               k_h_float_max, a second pass, its bin maxima (80 KB)
 //   k_h_final   derived sums / maxima of the width-1 bins, fp64 maxima decoded
 //
 // Integer histograms use the logarithmic bins of
@@ -129,10 +129,18 @@ constexpr int kHbPidThreads = 1024;
 constexpr int kHbPidSlots = 4032;
 constexpr int kHbPidFill = 3628;         // 90 % of kHbPidSlots
 constexpr int kHbPidPer = (kHbPidSlots + kHbPidThreads - 1) / kHbPidThreads;
+#ifndef PDP_HB_PID_PRE
+#define PDP_HB_PID_PRE 2
+#endif
+constexpr int kHbPidPre = PDP_HB_PID_PRE;  // rows per thread loaded together in k_hb_pid_pairs
 constexpr int kHbRangeBits = 11;
 constexpr int kHbRangeW = 1 << kHbRangeBits;
 constexpr int kHbRangeMax = 128;         // more ranges (P > 262,144): per-pair partition atomics
 constexpr int kHbRangeThreads = 1024;
+#ifndef PDP_HB_RANGE_U
+#define PDP_HB_RANGE_U 4
+#endif
+constexpr int kHbRangeU = PDP_HB_RANGE_U;  // records per thread in flight in k_hb_prange
 static_assert(kHbPidSlots * 12 + kSmallBins * 4 + 3 * (kHbRangeMax + 1) * 4 <= kHbPidSlots * 20,
               "the pid table, Linf bins and range counters reuse the pair table's LDS");
 
@@ -464,6 +472,53 @@ __global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned long long
   flush_small(H, lds, 3, H_PIDS);
 }
 
+// the lowers of k_h_lowers recomputed in registers (same roundings, so the
+// same doubles): a value's bin costs no memory reads
+struct LinBins {
+  double mn, mx, step, delta, inv;
+  int nb;
+};
+__device__ __forceinline__ LinBins lin_bins(const double* __restrict__ L, int nl) {
+  LinBins z{0.0, 0.0, 0.0, 0.0, 0.0, nl - 1};
+  if (nl < 2) return z;
+  z.mn = L[0];
+  z.mx = L[nl - 1];
+  z.delta = __dsub_rn(z.mx, z.mn);
+  z.step = __ddiv_rn(z.delta, (double)kSumBuckets);
+  z.inv = z.delta > 0.0 ? (double)z.nb / z.delta : 0.0;
+  return z;
+}
+// numpy's y = i * step + start (or (i / div) * delta + start when step == 0,
+// a call-uniform case: STEP0), each operation rounded on its own: contraction
+// into an FMA is off in this scope (an FMA moves values across bin edges; the
+// oracle caught one).  Round 4 kept the two forms in one select, which the
+// compiler evaluated both sides of: an fp64 division per lower, 2 per value
+template <bool STEP0>
+__device__ __forceinline__ double lin_lower(const LinBins& z, int i) {
+#pragma clang fp contract(off)
+  if (i == z.nb) return z.mx;
+  const double y = STEP0 ? ((double)i / (double)kSumBuckets) * z.delta : (double)i * z.step;
+  return y + z.mn;
+}
+// bisect_right(lowers, v) - 1 as float_bin, from the recomputed lowers
+template <bool STEP0>
+__device__ __forceinline__ int lin_bin(const LinBins& z, double v) {
+  const int nb = z.nb;
+  if (nb <= 1) return 0;
+  int b = (int)((v - z.mn) * z.inv);  // a guess; the loops make it exact
+  b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+  while (b + 1 < nb && lin_lower<STEP0>(z, b + 1) <= v) ++b;
+  while (b > 0 && lin_lower<STEP0>(z, b) > v) --b;
+  return b;
+}
+__device__ __forceinline__ int lin_bin_any(const LinBins& z, double v) {
+  return z.step == 0.0 ? lin_bin<true>(z, v) : lin_bin<false>(z, v);
+}
+template <bool B>
+struct BoolTag {
+  static constexpr bool value = B;
+};
+
 // np.linspace(mn, mx, 10001) (numpy function_base.linspace): step = delta /
 // div, y = i * step + start with separate roundings, y[-1] = stop; [mn, mn]
 // when mn == mx; no lowers when the histogram is empty.
@@ -481,13 +536,9 @@ __global__ void __launch_bounds__(kBlock) k_h_lowers(const unsigned long long* _
     if (i < 2) L[i] = mn;
     return;
   }
-  const double delta = __dsub_rn(mx, mn);
-  const double step = __ddiv_rn(delta, (double)kSumBuckets);
-  double y;
-  if (step == 0.0) y = __dmul_rn(__ddiv_rn((double)i, (double)kSumBuckets), delta);
-  else y = __dmul_rn((double)i, step);
-  y = __dadd_rn(y, mn);
-  L[i] = i == kNLowers - 1 ? mx : y;
+  LinBins z{mn, mx, 0.0, __dsub_rn(mx, mn), 0.0, kSumBuckets};
+  z.step = __ddiv_rn(z.delta, (double)kSumBuckets);
+  L[i] = z.step == 0.0 ? lin_lower<true>(z, i) : lin_lower<false>(z, i);  // the last is mx
 }
 
 // bisect_right(lowers, v) - 1, the maximum in the last bin (_bin_lower_index)
@@ -512,110 +563,38 @@ __device__ __forceinline__ void max_filtered(unsigned long long* omax, unsigned 
   if (o > __hip_atomic_load(omax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(omax, o);
 }
 
-// the lowers of k_h_lowers recomputed in registers (same roundings, so the
-// same doubles): a value's bin costs no memory reads
-struct LinBins {
-  double mn, mx, step, delta, inv;
-  int nb;
-};
-__device__ __forceinline__ LinBins lin_bins(const double* __restrict__ L, int nl) {
-  LinBins z{0.0, 0.0, 0.0, 0.0, 0.0, nl - 1};
-  if (nl < 2) return z;
-  z.mn = L[0];
-  z.mx = L[nl - 1];
-  z.delta = __dsub_rn(z.mx, z.mn);
-  z.step = __ddiv_rn(z.delta, (double)kSumBuckets);
-  z.inv = z.delta > 0.0 ? (double)z.nb / z.delta : 0.0;
-  return z;
-}
-__device__ __forceinline__ double lin_lower(const LinBins& z, int i) {
-  if (i == z.nb) return z.mx;
-  const double y = z.step == 0.0 ? __dmul_rn(__ddiv_rn((double)i, (double)kSumBuckets), z.delta)
-                                 : __dmul_rn((double)i, z.step);
-  return __dadd_rn(y, z.mn);
-}
-// bisect_right(lowers, v) - 1 as float_bin, from the recomputed lowers
-__device__ __forceinline__ int lin_bin(const LinBins& z, double v) {
-  const int nb = z.nb;
-  if (nb <= 1) return 0;
-  int b = (int)((v - z.mn) * z.inv);  // a guess; the loops make it exact
-  b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
-  while (b + 1 < nb && lin_lower(z, b + 1) <= v) ++b;
-  while (b > 0 && lin_lower(z, b) > v) --b;
-  return b;
-}
-
 constexpr int kFloatBlock = 1024;
+#ifndef PDP_HF_U
+#define PDP_HF_U 4
+#endif
+constexpr int kFloatU = PDP_HF_U;  // pair sums in flight per thread
 
-// pair sums: counts and sums in LDS (one workgroup per CU, 16 waves), flushed
-// once; bin maxima: an LDS word per bin holds the high half of the largest
-// ordered image this workgroup sent to the global atomicMax, so only values
-// that can raise it go out (a value equal to it in the high half first reads
-// the global maximum: an atomic per copy of a clipped value on one address
-// took k_h_float from 1.8 to 53 ms); partition sums (P elements): global atomics
-__global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
-                                                         const double* __restrict__ pairsum,
-                                                         const unsigned* __restrict__ hb_ctl,
-                                                         const unsigned* __restrict__ hb_bstart,
-                                                         const unsigned* __restrict__ hb_pruns,
-                                                         const PRec* __restrict__ hb_prec,
-                                                         const unsigned long long* __restrict__ pkstat,
-                                                         const double* __restrict__ psum,
-                                                         const double* __restrict__ lowers,
-                                                         const int* __restrict__ n_lowers, FloatHists F) {
-  __shared__ unsigned lcnt[kSumBuckets];
-  __shared__ double lsum[kSumBuckets];
-  __shared__ unsigned lmx[kSumBuckets];
-  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
-    lcnt[b] = 0;
-    lsum[b] = 0.0;
-    lmx[b] = 0;
-  }
-  __syncthreads();
-  const int64_t C = (int64_t)t.cap;
+// every pair sum of the call's pair phase, in the form it left them: the pair
+// buckets' list (mode 1), the privacy-id buckets' range-grouped records
+// (mode 2: every bucket's row span holds its pairs, then records marked
+// pk = ~0, so one flat, coalesced pass reads them all), or the pair table
+template <typename Fn>
+__device__ __forceinline__ void for_pair_sums(const HT& t, const Slot* __restrict__ slots,
+                                              const double* __restrict__ pairsum,
+                                              const unsigned* __restrict__ hb_ctl,
+                                              const unsigned* __restrict__ hb_bstart,
+                                              const PRec* __restrict__ hb_prec, Fn&& f) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
-  const LinBins z0 = lin_bins(lowers, nl0);
-  // the last bin's maximum is the global maximum mx, and bin 0's is at least
-  // the global minimum mn when mn falls in bin 0: set up front, so the copies
-  // of a clipped value (mn / mx: ~5 % of the values each for N(5, 3) clipped
-  // to [0, 10]) send nothing; every other value goes through the filter
-  if (nl0 > 0 && blockIdx.x == 0 && threadIdx.x == 0) {
-    atomicMax(F.omax + (z0.nb - 1), ord(z0.mx));
-    if (lin_bin(z0, z0.mn) == 0) atomicMax(F.omax, ord(z0.mn));
-  }
-  auto add = [&](double v) {
-    const int b = lin_bin(z0, v);
-    atomicAdd(lcnt + b, 1u);
-    atomicAdd(lsum + b, v);
-    if (b == z0.nb - 1 || (b == 0 && v == z0.mn)) return;
-    const unsigned long long o = ord(v);
-    const unsigned hi = (unsigned)(o >> 32);
-    const unsigned cur = lmx[b];
-    if (hi > cur) {  // raises the bin's maximum
-      atomicMax(lmx + b, hi);
-      atomicMax(F.omax + b, o);
-    } else if (hi == cur) {  // ties (clipped values: thousands per bin) read the global maximum first
-      max_filtered(F.omax + b, o);
-    }
-  };
-  constexpr int U = 4;  // values in flight per thread
-  if (nl0 > 0 && hb_ctl[0] == 1) {  // the pair buckets' list of pair sums
+  const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int U = kFloatU;
+  if (hb_ctl[0] == 1) {
     const int64_t np = hb_ctl[1];
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < np; i0 += U * stride) {
+    for (int64_t i0 = i00; i0 < np; i0 += U * stride) {
       double v[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < np ? pairsum[i0 + u * stride] : 0.0;
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (i0 + u * stride < np) add(v[u]);
+        if (i0 + u * stride < np) f(v[u]);
     }
-  } else if (nl0 > 0 && hb_ctl[0] == 2) {
-    // the privacy-id buckets' pair records: every bucket's row span holds its
-    // pairs, then records marked pk = ~0 (k_hb_pid_pairs), so one flat,
-    // coalesced pass over [0, valid rows) reads them all
+  } else if (hb_ctl[0] == 2) {
     const int64_t np = hb_bstart[t.nb];
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < np; i0 += U * stride) {
+    for (int64_t i0 = i00; i0 < np; i0 += U * stride) {
       PRec r[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -625,21 +604,72 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (r[u].pk != ~0u) add(r[u].sum);
+        if (r[u].pk != ~0u) f(r[u].sum);
     }
-  } else if (nl0 > 0) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < C; i += stride) {
+  } else {
+    for (int64_t i = i00; i < (int64_t)t.cap; i += stride) {
       const Slot sl = slots[i];
-      if (sl.key == 0) continue;
-      add(sl.sum);
+      if (sl.key != 0) f(sl.sum);
     }
   }
-  if (nl1 > 0) {
+}
+
+// the Linf-sum histogram in two passes over the pair sums, each with its bins
+// privatised in LDS and flushed once per workgroup:
+//   MAX = false  counts (u32) and sums (fp64), 120 KB: one workgroup per CU;
+//                plus the partition-sum histogram (P elements, global atomics)
+//   MAX = true   bin maxima as ordered u64 images, 80 KB; a value
+//                goes to LDS only when it raises the bin's maximum
+// One pass holding all three (200 KB) does not fit; the previous form kept
+// only the high half of each maximum in LDS and sent every raise to a global
+// atomicMax -- at ~4 raises per bin and workgroup those atomics, waited on by
+// the next loads (one in-order vmcnt), took 1.0 of its 1.7 ms
+// (profiles/r05/ab/ab10_hist_latency.txt); the second pass re-reads 1.6 GB.
+template <bool MAX>
+__global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
+                                                         const double* __restrict__ pairsum,
+                                                         const unsigned* __restrict__ hb_ctl,
+                                                         const unsigned* __restrict__ hb_bstart,
+                                                         const PRec* __restrict__ hb_prec,
+                                                         const unsigned long long* __restrict__ pkstat,
+                                                         const double* __restrict__ psum,
+                                                         const double* __restrict__ lowers,
+                                                         const int* __restrict__ n_lowers, FloatHists F) {
+  __shared__ unsigned lcnt[MAX ? 1 : kSumBuckets];
+  __shared__ double lsum[MAX ? 1 : kSumBuckets];
+  __shared__ unsigned long long lmx[MAX ? kSumBuckets : 1];
+  for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
+    if (MAX) {
+      lmx[b] = 0;
+    } else {
+      lcnt[b] = 0;
+      lsum[b] = 0.0;
+    }
+  }
+  __syncthreads();
+  const int nl0 = n_lowers[F_LINF_SUM], nl1 = n_lowers[F_PART_SUM];
+  const LinBins z0 = lin_bins(lowers, nl0);
+  auto bin_add = [&](auto step0, double v) {
+    const int b = lin_bin<decltype(step0)::value>(z0, v);
+    if (MAX) {
+      const unsigned long long o = ord(v);
+      if (o > lmx[b]) atomicMax(lmx + b, o);
+    } else {
+      atomicAdd(lcnt + b, 1u);
+      atomicAdd(lsum + b, v);
+    }
+  };
+  if (nl0 > 0 && z0.step == 0.0)  // call-uniform: one loop per lowers form
+    for_pair_sums(t, slots, pairsum, hb_ctl, hb_bstart, hb_prec, [&](double v) { bin_add(BoolTag<true>{}, v); });
+  else if (nl0 > 0)
+    for_pair_sums(t, slots, pairsum, hb_ctl, hb_bstart, hb_prec, [&](double v) { bin_add(BoolTag<false>{}, v); });
+  if (!MAX && nl1 > 0) {
     const LinBins z1 = lin_bins(lowers + kNLowers, nl1);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < t.P; i += stride) {
       if (pkstat[i] == 0) continue;
       const double v = psum[i];
-      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + lin_bin(z1, v);
+      const int64_t g = (int64_t)F_PART_SUM * kSumBuckets + lin_bin_any(z1, v);
       atomicAdd(F.count + g, 1ULL);
       atomicAdd(F.sum + g, v);
       max_filtered(F.omax + g, ord(v));
@@ -647,10 +677,15 @@ __global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __res
   }
   __syncthreads();
   for (int b = threadIdx.x; b < kSumBuckets; b += blockDim.x) {
-    const unsigned c = lcnt[b];
-    if (c) {
-      atomicAdd(F.count + b, (unsigned long long)c);
-      atomicAdd(F.sum + b, lsum[b]);
+    if (MAX) {
+      const unsigned long long o = lmx[b];
+      if (o) max_filtered(F.omax + b, o);
+    } else {
+      const unsigned c = lcnt[b];
+      if (c) {
+        atomicAdd(F.count + b, (unsigned long long)c);
+        atomicAdd(F.sum + b, lsum[b]);
+      }
     }
   }
 }
@@ -784,27 +819,44 @@ __global__ void __launch_bounds__(kHbThreads) k_hb_l1(HT t, const int64_t* __res
   constexpr int N = kHbStage / kHbThreads;
   const int64_t t0 = (int64_t)blockIdx.x * kHbTileRows;
   const int64_t t1 = t0 + kHbTileRows < t.n ? t0 + kHbTileRows : t.n;
+  // a stage's three columns load together (the values not after the keys'
+  // check: one latency round per stage); rows past the tile load as pid -1
+  // (invalid, like a bad key: no record).  Loading stage s + 1 while stage s
+  // is written measured no faster (profiles/r05/ab/ab10_hist_latency.txt)
+  int64_t ru[N], rk[N];
+  double rv[N];
+  auto load_stage = [&](int64_t c0) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int64_t i = c0 + (int64_t)q * blockDim.x + threadIdx.x;
+      ru[q] = -1;
+      rk[q] = 0;
+      rv[q] = 0.0;
+      if (i >= t1) continue;
+      ru[q] = pid[i];
+      rk[q] = pk[i];
+      if (VK == PDP_VALUE_F64) rv[q] = ((const double*)value)[i];
+      if (VK == PDP_VALUE_I64) rv[q] = (double)((const long long*)value)[i];
+    }
+  };
   for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x)
     cur[b] = sbase[b] + cts[(int64_t)blockIdx.x * t.n_supers + b];
   for (int64_t c0 = t0; c0 < t1; c0 += kHbStage) {
     for (int b = threadIdx.x; b < t.n_supers; b += blockDim.x) hist[b] = 0;
     __syncthreads();
+    load_stage(c0);
     unsigned long long x[N];
     double v[N];
     int d[N];
     unsigned rank[N];
 #pragma unroll
     for (int q = 0; q < N; ++q) {
-      const int64_t i = c0 + (int64_t)q * blockDim.x + threadIdx.x;
+      const int64_t u = ru[q], k = rk[q];
       d[q] = -1;
       x[q] = 0;
-      v[q] = 0.0;
-      if (i >= t1) continue;
-      const int64_t u = pid[i], k = pk[i];
+      v[q] = rv[q];
       if ((uint64_t)u >= (uint64_t)t.U || (uint64_t)k >= (uint64_t)t.P) continue;  // flagged by k_hb_count
       x[q] = ((uint64_t)u << t.pk_bits) | (uint64_t)k;
-      if (VK == PDP_VALUE_F64) v[q] = ((const double*)value)[i];
-      if (VK == PDP_VALUE_I64) v[q] = (double)((const long long*)value)[i];
       d[q] = (int)(hb_bucket_t(t, x[q]) / kHbFan);
     }
 #pragma unroll
@@ -1061,6 +1113,24 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
   unsigned* rcnt = lbins + kSmallBins;                       //          [kHbRangeMax + 1]
   unsigned* rstart = rcnt + kHbRangeMax + 1;                 //          [kHbRangeMax + 1]
   __shared__ unsigned fill, s_base, s_over;
+  const int64_t a = bstart[blockIdx.x], e = bstart[blockIdx.x + 1];
+  // each thread's next kHbPidPre rows (keys and values) are loaded together,
+  // the first batch before the table is cleared: one memory latency per
+  // batch instead of two per row (a bucket averages 1.5 rows per thread).
+  // A persistent form that loaded the next bucket's rows during this one's
+  // phase 2 measured slower (1.71 vs 1.59 ms, profiles/r05/ab/ab10_hist_latency.txt)
+  unsigned long long xs[kHbPidPre];
+  double vs[kHbPidPre];
+  auto load_rows = [&](int64_t i0) {
+#pragma unroll
+    for (int q = 0; q < kHbPidPre; ++q) {
+      const int64_t i = i0 + (int64_t)q * blockDim.x;
+      xs[q] = i < e ? key[i] : 0ULL;
+      vs[q] = HAS_VALUE && i < e ? val[i] : 0.0;
+    }
+  };
+  int64_t i0 = a + threadIdx.x;
+  load_rows(i0);
   for (int i = threadIdx.x; i < kHbPidSlots; i += blockDim.x) {
     tkey[i] = ~0ULL;
     tsum[i] = 0.0;
@@ -1071,32 +1141,36 @@ __global__ void __launch_bounds__(kHbPidThreads) k_hb_pid_pairs(
     s_over = 0;
   }
   __syncthreads();
-  const int64_t a = bstart[blockIdx.x], e = bstart[blockIdx.x + 1];
-  for (int64_t i = a + threadIdx.x; i < e; i += blockDim.x) {
-    const unsigned long long x = key[i];
-    unsigned sl = (unsigned)(((mix64(x) & 0xFFFFFFFFULL) * (uint64_t)kHbPidSlots) >> 32);
-    bool over = false;
-    for (;;) {
-      const unsigned long long cur = tkey[sl];
-      if (cur == x) break;
-      if (cur == ~0ULL) {
-        if (atomicAdd(&fill, 1u) >= (unsigned)kHbPidFill) {
-          over = true;
-          break;
+  // distinct pairs <= rows: only a bucket with more rows than kHbPidFill
+  // counts its new slots (one LDS address for the whole workgroup)
+  const bool may_over = e - a > kHbPidFill;
+  for (bool over = false; i0 < e && !over; i0 += (int64_t)kHbPidPre * blockDim.x) {
+#pragma unroll
+    for (int q = 0; q < kHbPidPre; ++q) {
+      if (over || i0 + (int64_t)q * blockDim.x >= e) break;
+      const unsigned long long x = xs[q];
+      unsigned sl = (unsigned)(((mix64(x) & 0xFFFFFFFFULL) * (uint64_t)kHbPidSlots) >> 32);
+      for (;;) {
+        const unsigned long long cur = tkey[sl];
+        if (cur == x) break;
+        if (cur == ~0ULL) {
+          if (may_over && atomicAdd(&fill, 1u) >= (unsigned)kHbPidFill) {
+            over = true;
+            break;
+          }
+          const unsigned long long old = atomicCAS(tkey + sl, ~0ULL, x);
+          if (old == ~0ULL) break;
+          if (may_over) atomicSub(&fill, 1u);
+          if (old == x) break;
         }
-        const unsigned long long old = atomicCAS(tkey + sl, ~0ULL, x);
-        if (old == ~0ULL) break;
-        atomicSub(&fill, 1u);
-        if (old == x) break;
+        sl = sl + 1 == (unsigned)kHbPidSlots ? 0u : sl + 1;
       }
-      sl = sl + 1 == (unsigned)kHbPidSlots ? 0u : sl + 1;
+      if (over) break;
+      atomicAdd(tcnt + sl, 1u);
+      if (HAS_VALUE) atomicAdd(tsum + sl, vs[q]);
     }
-    if (over) {
-      s_over = 1;
-      break;
-    }
-    atomicAdd(tcnt + sl, 1u);
-    if (HAS_VALUE) atomicAdd(tsum + sl, val[i]);
+    if (over) s_over = 1;
+    else if (i0 + (int64_t)kHbPidPre * blockDim.x < e) load_rows(i0 + (int64_t)kHbPidPre * blockDim.x);
   }
   __syncthreads();
   if (s_over) {  // workgroup-uniform: the call's results are discarded
@@ -1260,28 +1334,40 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
     bex[threadIdx.x] = ex;
     bbase[threadIdx.x] = base;
     __syncthreads();
-    for (unsigned f = threadIdx.x; f < tot; f += blockDim.x) {
-      int lo = 0, hi = kHbRangeThreads;  // the last run starting at or before f
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (bex[mid] <= f) lo = mid;
-        else hi = mid;
+    // kHbRangeU records per thread in flight (one memory latency per batch)
+    for (unsigned f0 = threadIdx.x; f0 < tot; f0 += kHbRangeU * blockDim.x) {
+      PRec recs[kHbRangeU];
+#pragma unroll
+      for (int u = 0; u < kHbRangeU; ++u) {
+        const unsigned f = f0 + u * blockDim.x;
+        if (f >= tot) break;
+        int lo = 0, hi = kHbRangeThreads;  // the last run starting at or before f
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (bex[mid] <= f) lo = mid;
+          else hi = mid;
+        }
+        recs[u] = prec[bbase[lo] + (f - bex[lo])];
       }
-      const PRec rec = prec[bbase[lo] + (f - bex[lo])];
-      const unsigned p = rec.pk & (kHbRangeW - 1);
-      atomicAdd(an + p, 1u);
-      atomicAdd(ar + p, rec.rows);
-      if (HAS_VALUE) atomicAdd(as + p, rec.sum);
-      // Linf bins: the lanes holding the first active lane's value (most
-      // pairs have one row) add once, the others one by one
-      const unsigned long long act = __ballot(true);
-      const unsigned r0 = __shfl(rec.rows, __ffsll((long long)act) - 1, 64);
-      const unsigned long long same = __ballot(rec.rows == r0);
-      if (rec.rows != r0) int_hist_add(H, lbins, H_LINF, 0, rec.rows);
-      else if ((int)(threadIdx.x & 63) == __ffsll((long long)same) - 1) int_hist_add_n(H, lbins, H_LINF, 0, r0, __popcll(same));
-      const unsigned long long o = ord(rec.sum);
-      mn = o < mn ? o : mn;
-      mx = o > mx ? o : mx;
+#pragma unroll
+      for (int u = 0; u < kHbRangeU; ++u) {
+        if (f0 + u * blockDim.x >= tot) break;
+        const PRec rec = recs[u];
+        const unsigned p = rec.pk & (kHbRangeW - 1);
+        atomicAdd(an + p, 1u);
+        atomicAdd(ar + p, rec.rows);
+        if (HAS_VALUE) atomicAdd(as + p, rec.sum);
+        // Linf bins: the lanes holding the first active lane's value (most
+        // pairs have one row) add once, the others one by one
+        const unsigned long long act = __ballot(true);
+        const unsigned r0 = __shfl(rec.rows, __ffsll((long long)act) - 1, 64);
+        const unsigned long long same = __ballot(rec.rows == r0);
+        if (rec.rows != r0) int_hist_add(H, lbins, H_LINF, 0, rec.rows);
+        else if ((int)(threadIdx.x & 63) == __ffsll((long long)same) - 1) int_hist_add_n(H, lbins, H_LINF, 0, r0, __popcll(same));
+        const unsigned long long o = ord(rec.sum);
+        mn = o < mn ? o : mn;
+        mx = o > mx ? o : mx;
+      }
     }
     __syncthreads();
   }
@@ -1832,11 +1918,15 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   const int64_t mf = (int64_t)t.cap > t.P ? (int64_t)t.cap : t.P;
   int64_t gf = (mf + kFloatBlock - 1) / kFloatBlock;
   gf = gf < cus ? gf : cus;
-  PDP_HLAUNCH("k_h_float", st, k_h_float, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, (const Slot*)(ws + w.slots),
-              (const double*)(w.hb_pairsum ? ws + w.hb_pairsum : nullptr), (const unsigned*)(ws + w.hb_ctl),
-              (const unsigned*)(w.hb_bcnt ? ws + w.hb_bcnt : nullptr),
-              (const unsigned*)(w.hb_pruns ? ws + w.hb_pruns : nullptr), (const PRec*)(ws + w.slots), pkstat,
-              psum, out->float_lowers, out->float_n_lowers, c.F);
+  const Slot* fslots = (const Slot*)(ws + w.slots);
+  const double* fpairsum = (const double*)(w.hb_pairsum ? ws + w.hb_pairsum : nullptr);
+  const unsigned* fctl = (const unsigned*)(ws + w.hb_ctl);
+  const unsigned* fbstart = (const unsigned*)(w.hb_bcnt ? ws + w.hb_bcnt : nullptr);
+  const PRec* fprec = (const PRec*)(ws + w.slots);
+  PDP_HLAUNCH("k_h_float", st, k_h_float<false>, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, fslots, fpairsum,
+              fctl, fbstart, fprec, pkstat, psum, out->float_lowers, out->float_n_lowers, c.F);
+  PDP_HLAUNCH("k_h_float_max", st, k_h_float<true>, dim3((unsigned)gf), dim3(kFloatBlock), 0, st, t, fslots,
+              fpairsum, fctl, fbstart, fprec, pkstat, psum, out->float_lowers, out->float_n_lowers, c.F);
   PDP_HLAUNCH("k_h_final", st, k_h_final, dim3((2 * kSumBuckets + kBlock - 1) / kBlock), dim3(kBlock), 0, st, c.H,
               c.F, out->float_max, 0x1F);
   return PDP_OK;
