@@ -107,10 +107,14 @@ struct HWs {
 // back to the pair-table path for the whole call (never for hashed real data).
 constexpr int kHbTileRows = 65536;
 constexpr int kHbThreads = 1024;         // count / level-1 workgroups
-constexpr int kHbStage = 8192;           // level-1 rows per LDS stage (8 per thread)
+constexpr int kHbStage = 8192;           // level-1 rows per LDS stage (8 per thread; 4,096: 1.32 vs 1.16 ms)
 constexpr int kHbFan = 256;              // buckets per super-bucket
-constexpr int kHbL2Threads = 512;
-constexpr int kHbWin = 4096;             // level-2 records per window (8 per thread)
+constexpr int kHbL2Threads = 1024;
+// level-2 records per window (8 per thread; 139 KB of LDS, one workgroup per
+// CU): windows of 2,048 / 4,096 records ran 1.35 / 1.12 ms against 0.95 ms
+// at 1e8 rows -- fewer, longer runs per bucket write more whole lines
+// (profiles/r05/ab/ab10_hist_latency.txt)
+constexpr int kHbWin = 8192;
 constexpr int kHbK = 8;                  // level-2 workgroups per super-bucket
 constexpr int kHbSlots = 3072;           // LDS pair table per bucket
 constexpr int kHbFill = 2760;            // 90 % of kHbSlots: more distinct pairs -> fallback
@@ -255,6 +259,38 @@ __device__ __forceinline__ void int_hist_add_n(const IntHists& H, unsigned* lds_
     atomicAdd(H.count + g, (unsigned long long)n);
     atomicAdd(H.sum + g, v * n);
     atomicMax(H.max + g, v);
+  }
+}
+
+// one element per lane of a whole, converged wave (every lane calls it; valid
+// marks the lanes with an element): small bins count in LDS; the lanes of one
+// larger bin are summed across the wave and sent by one lane -- a bin every
+// partition of a table falls in (1,000-row partitions: all in one or two
+// bins) would otherwise take one global atomic per element on one address
+__device__ __forceinline__ void int_hist_add_wave(const IntHists& H, unsigned* lds_counts, int h, int slot,
+                                                  unsigned long long v, bool valid) {
+  const int b = valid ? log_bin_index(v) : -1;
+  if (valid && b < kSmallBins) atomicAdd(lds_counts + slot * kSmallBins + b, 1u);
+  const int lane = threadIdx.x & 63;
+  unsigned long long todo = __ballot(valid && b >= kSmallBins);
+  while (todo) {  // wave-uniform
+    const int leader = __ffsll((long long)todo) - 1;
+    const int bl = __shfl(b, leader, 64);
+    const bool mine = ((todo >> lane) & 1) && b == bl;
+    const unsigned long long same = __ballot(mine);
+    unsigned long long sum = mine ? v : 0ULL, mx = sum;
+    for (int o = 32; o > 0; o >>= 1) {
+      sum += __shfl_xor(sum, o, 64);
+      const unsigned long long y = __shfl_xor(mx, o, 64);
+      mx = y > mx ? y : mx;
+    }
+    if (lane == leader) {
+      const int64_t g = (int64_t)h * kLogBins + bl;
+      atomicAdd(H.count + g, (unsigned long long)__popcll(same));
+      atomicAdd(H.sum + g, sum);
+      atomicMax(H.max + g, mx);
+    }
+    todo &= ~same;
   }
 }
 
@@ -445,20 +481,22 @@ __global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned long long
   const int64_t m = t.U > t.P ? t.U : t.P;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   unsigned long long mn = ~0ULL, mx = 0ULL;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
-    if (i < t.U) {
-      const unsigned long long st = pidstat[i];
-      if (st) {
-        int_hist_add(H, lds, H_L0, 0, st >> 32);
-        int_hist_add(H, lds, H_L1, 1, st & 0xFFFFFFFFULL);
-      }
-    }
-    if (t.do_parts && i < t.P) {
-      const unsigned long long st = pkstat[i];
-      if (st) {
-        int_hist_add(H, lds, H_COUNT, 2, st & 0xFFFFFFFFULL);
-        int_hist_add(H, lds, H_PIDS, 3, st >> 32);
-        const unsigned long long o = ord(psum[i]);
+  // the loop bound is workgroup-uniform, so every wave stays converged for
+  // int_hist_add_wave; lanes past the end carry no element
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x; i0 < m; i0 += stride) {
+    const int64_t i = i0 + threadIdx.x;
+    // the three loads together (psum not after pkstat's check)
+    const unsigned long long st = i < t.U ? pidstat[i] : 0ULL;
+    const bool part = t.do_parts && i < t.P;
+    const unsigned long long sp = part ? pkstat[i] : 0ULL;
+    const double ps = part ? psum[i] : 0.0;
+    int_hist_add_wave(H, lds, H_L0, 0, st >> 32, st != 0);
+    int_hist_add_wave(H, lds, H_L1, 1, st & 0xFFFFFFFFULL, st != 0);
+    if (t.do_parts) {
+      int_hist_add_wave(H, lds, H_COUNT, 2, sp & 0xFFFFFFFFULL, sp != 0);
+      int_hist_add_wave(H, lds, H_PIDS, 3, sp >> 32, sp != 0);
+      if (sp) {
+        const unsigned long long o = ord(ps);
         mn = o < mn ? o : mn;
         mx = o > mx ? o : mx;
       }
@@ -625,8 +663,11 @@ __device__ __forceinline__ void for_pair_sums(const HT& t, const Slot* __restric
 // atomicMax -- at ~4 raises per bin and workgroup those atomics, waited on by
 // the next loads (one in-order vmcnt), took 1.0 of its 1.7 ms
 // (profiles/r05/ab/ab10_hist_latency.txt); the second pass re-reads 1.6 GB.
+#ifndef PDP_HF_MAXOCC
+#define PDP_HF_MAXOCC 4
+#endif
 template <bool MAX>
-__global__ void __launch_bounds__(kFloatBlock) k_h_float(HT t, const Slot* __restrict__ slots,
+__global__ void __launch_bounds__(kFloatBlock, MAX ? PDP_HF_MAXOCC : 4) k_h_float(HT t, const Slot* __restrict__ slots,
                                                          const double* __restrict__ pairsum,
                                                          const unsigned* __restrict__ hb_ctl,
                                                          const unsigned* __restrict__ hb_bstart,
@@ -914,7 +955,16 @@ __global__ void __launch_bounds__(kHbL2Threads) k_hb_bcount(HT t, const unsigned
   const int64_t a = sbase[s], e = sbase[s + 1];
   for (int64_t w0 = a + (int64_t)k * kHbWin; w0 < e; w0 += (int64_t)kHbK * kHbWin) {
     const int64_t w1 = w0 + kHbWin < e ? w0 + kHbWin : e;
-    for (int64_t i = w0 + threadIdx.x; i < w1; i += blockDim.x) atomicAdd(h + hb_bucket_t(t, key[i]) % kHbFan, 1u);
+    constexpr int N = kHbWin / kHbL2Threads;  // a window's keys in flight at once
+    unsigned long long x[N];
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int64_t i = w0 + (int64_t)q * blockDim.x + threadIdx.x;
+      x[q] = i < w1 ? key[i] : 0ULL;
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+      if (w0 + (int64_t)q * blockDim.x + threadIdx.x < w1) atomicAdd(h + hb_bucket_t(t, x[q]) % kHbFan, 1u);
   }
   __syncthreads();
   for (int b = threadIdx.x; b < kHbFan; b += blockDim.x) {
@@ -1907,7 +1957,9 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   const double* psum = (const double*)(ws + w.psum);
   const int64_t m = t.U > t.P ? t.U : t.P;
   if (m > 0)
-    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 2048)), dim3(kBlock), 0, st, t,
+    // at most 256 workgroups: each flushes its small bins with one global
+    // atomic per bin, and 2,048 of them made those flushes most of the kernel
+    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 256)), dim3(kBlock), 0, st, t,
                 (const unsigned long long*)(ws + w.pidstat), pkstat, psum, c.H, minmax);
   PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
               out->float_lowers, out->float_n_lowers);
