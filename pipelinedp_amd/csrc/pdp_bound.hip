@@ -3231,6 +3231,9 @@ __device__ __forceinline__ void item_rounds(const KP& kp, const PairRecords& rec
   }
 }
 
+#ifndef PDP_SPLIT_STAGED
+#define PDP_SPLIT_STAGED 1
+#endif
 constexpr int kFinePerCoarseMax = 1 << 13;  // 2^(range_bits - kRangeBits) <= 2^13 (P < 2^32, 256 coarse ranges)
 
 // fine-range totals: per item an LDS histogram of its records' fine ranges,
@@ -3320,6 +3323,104 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairReco
                   if (stg.f1) stg.f1[o] = v1[u];
                   if (stg.f2) stg.f2[o] = v2[u];
                 }
+              },
+              [] {});
+}
+
+// k_split_scatter for coarse ranges of <= kSplitStageFan fine ranges (C4 /
+// C5: 32): each round's records are counting-sorted by fine range in LDS
+// first, so a fine range's records leave as one contiguous run (~32 per
+// round) instead of one scattered 8-byte store per record and array
+constexpr int kSplitStageFan = 256;
+constexpr int kSplitStageRows = 4 * kRangeThreads;  // item_rounds' RR records per thread
+__global__ void __launch_bounds__(kRangeThreads) k_split_scatter_staged(KP kp, PairRecords rec, PairRecords stg,
+                                                                       const uint4* __restrict__ items,
+                                                                       const unsigned* __restrict__ n_items,
+                                                                       unsigned* __restrict__ fine_cur,
+                                                                       const unsigned* __restrict__ item_hist) {
+  __shared__ unsigned long long start[kRangeThreads];
+  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned lcur[kSplitStageFan], hist[kSplitStageFan], hstart[kSplitStageFan], gbase[kSplitStageFan];
+  __shared__ unsigned long long skey[kSplitStageRows];
+  __shared__ double sf0[kSplitStageRows], sf1[kSplitStageRows], sf2[kSplitStageRows];
+  __shared__ uint8_t sdest[kSplitStageRows];
+  if (blockIdx.x >= *n_items) return;
+  const uint4 it = items[blockIdx.x];
+  if (it.x >> 31) return;
+  const uint4 nx = items[blockIdx.x + 1];
+  if (nx.z == it.z) return;
+  const int r = (int)it.x;
+  const int F = 1 << (kp.range_bits - kRangeBits);  // <= kSplitStageFan (host-checked)
+  const int64_t f0 = (int64_t)r << (kp.range_bits - kRangeBits);
+  for (int t = threadIdx.x; t < F; t += blockDim.x) {
+    const unsigned c = item_hist[(int64_t)blockIdx.x * F + t];
+    lcur[t] = c ? atomicAdd(fine_cur + f0 + t, c) : 0u;
+    hist[t] = 0;
+  }
+  __syncthreads();
+  item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
+              [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
+                unsigned long long key[4];
+                double v0[4], v1[4], v2[4];
+                int fu[4];
+                unsigned rk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  key[u] = ok[u] ? rec.key[idx[u]] : 0ull;
+                  v0[u] = (ok[u] && stg.f0) ? rec.f0[idx[u]] : 0.0;
+                  v1[u] = (ok[u] && stg.f1) ? rec.f1[idx[u]] : 0.0;
+                  v2[u] = (ok[u] && stg.f2) ? rec.f2[idx[u]] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  const uint64_t f = (key[u] >> (32 + kRangeBits)) - (uint64_t)f0;
+                  // a malformed record is skipped, as k_split_count leaves it uncounted
+                  fu[u] = ok[u] && f < (uint64_t)F && f0 + (int64_t)f < kp.n_fine_ranges ? (int)f : -1;
+                  rk[u] = fu[u] >= 0 ? atomicAdd(hist + fu[u], 1u) : 0u;
+                }
+                __syncthreads();
+                if (threadIdx.x < 64) {  // run starts in the stage; the runs' output positions
+                  const int lane = threadIdx.x;
+                  unsigned carry = 0;
+                  for (int b0 = 0; b0 < F; b0 += 64) {
+                    const unsigned hv = b0 + lane < F ? hist[b0 + lane] : 0u;
+                    unsigned incl = hv;
+                    for (int o = 1; o < 64; o <<= 1) {
+                      const unsigned up = __shfl_up(incl, o, 64);
+                      if (lane >= o) incl += up;
+                    }
+                    if (b0 + lane < F) {
+                      hstart[b0 + lane] = carry + incl - hv;
+                      gbase[b0 + lane] = lcur[b0 + lane];
+                      lcur[b0 + lane] += hv;
+                    }
+                    carry += __shfl(incl, 63, 64);
+                  }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                  if (fu[u] < 0) continue;
+                  const unsigned sl = hstart[fu[u]] + rk[u];
+                  skey[sl] = key[u];
+                  sf0[sl] = v0[u];
+                  sf1[sl] = v1[u];
+                  sf2[sl] = v2[u];
+                  sdest[sl] = (uint8_t)fu[u];
+                }
+                __syncthreads();
+                const unsigned n = hstart[F - 1] + hist[F - 1];
+                for (unsigned i = threadIdx.x; i < n; i += blockDim.x) {
+                  const int f = sdest[i];
+                  const uint64_t o = (uint64_t)gbase[f] + (i - hstart[f]);
+                  stg.key[o] = skey[i];
+                  if (stg.f0) stg.f0[o] = sf0[i];
+                  if (stg.f1) stg.f1[o] = sf1[i];
+                  if (stg.f2) stg.f2[o] = sf2[i];
+                }
+                __syncthreads();
+                for (int t = threadIdx.x; t < F; t += blockDim.x) hist[t] = 0;
+                __syncthreads();
               },
               [] {});
 }
@@ -3817,8 +3918,12 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     if (rc != PDP_OK) return rc;
     PDP_HIP_CHECK(hipMemcpyAsync(fine_cur, fine_total, (uint64_t)p.n_fine * 4, hipMemcpyDeviceToDevice, st));
     PDP_PROF_BEGIN("k_split_scatter", st);
-    hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
-                       (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
+    if ((1 << (kp.range_bits - kRangeBits)) <= kSplitStageFan && PDP_SPLIT_STAGED)
+      hipLaunchKernelGGL(k_split_scatter_staged, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
+                         (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
+    else
+      hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
+                         (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     uint4* fitems = (uint4*)(ws + w.fine_items);
