@@ -81,14 +81,25 @@ constexpr int kMaxRanges = kBucketThreads;    // per-bucket range histogram <= o
 // of them), k_split_* re-sort each coarse range's records into its
 // 2^kRangeBits-partition ranges, k_fine_reduce sums them (two-level merge)
 constexpr int kCoarseRanges = 256;
-constexpr int kRangeThreads = 256;
+#ifndef PDP_RANGE_THREADS
+#define PDP_RANGE_THREADS 1024
+#endif
+constexpr int kRangeThreads = PDP_RANGE_THREADS;  // k_range_plan workgroups
 // range-reduce work item: the records of one partition range from a run of
 // consecutive buckets, cut at bucket boundaries every kRangeChunk records
 // (k_range_plan), so a Zipf-hot range spreads over many workgroups and a cold
 // one is a single item
 constexpr int64_t kRangeChunk = 8192;
 constexpr unsigned kRangeDirect = 256;        // records below which a workgroup adds them directly
-constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kRangeThreads * (8 + 4) + (kRangeThreads / 64 + 1) * 4;
+// k_range_reduce / k_fine_reduce workgroups: 512 threads (two per CU by their
+// 68 KB of LDS: 16 waves, not 8): C3 k_range_reduce 0.275 -> 0.195 ms, C4
+// k_fine_reduce 0.574 -> 0.540 (1,024: 0.212 / 0.537; profiles/r05/ab/ab12_merge_threads.txt)
+constexpr int kReduceThreads = 512;
+#ifndef PDP_SPLIT_THREADS
+#define PDP_SPLIT_THREADS 512
+#endif
+constexpr int kSplitThreads = PDP_SPLIT_THREADS;  // k_split_count / k_split_scatter workgroups
+constexpr size_t kRangeLds = kRangeParts * (3 * 8 + 2 * 4) + kReduceThreads * (8 + 4) + (kReduceThreads / 64 + 1) * 4;
 constexpr int kQueueCap = 128;                // per-wave candidate queue (bucket kernel)
 constexpr int kScanItems = 16;
 constexpr int kScanChunk = kBlock * kScanItems;
@@ -3056,18 +3067,18 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
 // records of partitions [r*2^11, (r+1)*2^11) in LDS, then adds the partial
 // sums with coalesced device atomics (an item of few records adds them
 // directly).
-__global__ void __launch_bounds__(kRangeThreads) k_range_reduce(KP kp, PairRecords rec, const uint4* __restrict__ items,
+__global__ void __launch_bounds__(kReduceThreads) k_range_reduce(KP kp, PairRecords rec, const uint4* __restrict__ items,
                                                                const unsigned* __restrict__ n_items,
                                                                pdp_partition_accumulators acc, unsigned* err) {
   extern __shared__ unsigned long long smem[];
   double* s0 = (double*)smem;               // [kRangeParts] sum
   double* s1 = s0 + kRangeParts;            // normalized sum
   double* s2 = s1 + kRangeParts;            // normalized sum of squares
-  unsigned long long* start = (unsigned long long*)(s2 + kRangeParts);  // [kRangeThreads]
-  unsigned* pc = (unsigned*)(start + kRangeThreads);  // [kRangeParts] kept pairs
+  unsigned long long* start = (unsigned long long*)(s2 + kRangeParts);  // [kReduceThreads]
+  unsigned* pc = (unsigned*)(start + kReduceThreads);  // [kRangeParts] kept pairs
   unsigned* cn = pc + kRangeParts;                    // [kRangeParts] row count
-  unsigned* pre = cn + kRangeParts;                   // [kRangeThreads] run prefix
-  unsigned* wsum = pre + kRangeThreads;               // block-scan scratch
+  unsigned* pre = cn + kRangeParts;                   // [kReduceThreads] run prefix
+  unsigned* wsum = pre + kReduceThreads;              // block-scan scratch
   if (blockIdx.x >= *n_items) return;  // grid is an upper bound on the item count
   const uint4 it = items[blockIdx.x];
   if (it.x >> 31) return;  // sentinel
@@ -3238,12 +3249,12 @@ constexpr int kFinePerCoarseMax = 1 << 13;  // 2^(range_bits - kRangeBits) <= 2^
 
 // fine-range totals: per item an LDS histogram of its records' fine ranges,
 // added to fine_total with one atomic per touched fine range
-__global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecords rec, const uint4* __restrict__ items,
+__global__ void __launch_bounds__(kSplitThreads) k_split_count(KP kp, PairRecords rec, const uint4* __restrict__ items,
                                                               const unsigned* __restrict__ n_items,
                                                               unsigned* __restrict__ fine_total,
                                                               unsigned* __restrict__ item_hist) {
-  __shared__ unsigned long long start[kRangeThreads];
-  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned long long start[kSplitThreads];
+  __shared__ unsigned pre[kSplitThreads], wsum[kSplitThreads / 64 + 1];
   __shared__ unsigned lh[kFinePerCoarseMax];
   if (blockIdx.x >= *n_items) return;
   const uint4 it = items[blockIdx.x];
@@ -3280,13 +3291,13 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_count(KP kp, PairRecord
 // device atomic per touched fine range), then each record takes the next slot
 // of its fine range from an LDS cursor (a returning LDS atomic) -- no
 // barriers between the batches, so their loads overlap
-__global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairRecords rec, PairRecords stg,
+__global__ void __launch_bounds__(kSplitThreads) k_split_scatter(KP kp, PairRecords rec, PairRecords stg,
                                                                 const uint4* __restrict__ items,
                                                                 const unsigned* __restrict__ n_items,
                                                                 unsigned* __restrict__ fine_cur,
                                                                 const unsigned* __restrict__ item_hist) {
-  __shared__ unsigned long long start[kRangeThreads];
-  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned long long start[kSplitThreads];
+  __shared__ unsigned pre[kSplitThreads], wsum[kSplitThreads / 64 + 1];
   __shared__ unsigned lcur[kFinePerCoarseMax];
   if (blockIdx.x >= *n_items) return;
   const uint4 it = items[blockIdx.x];
@@ -3332,14 +3343,14 @@ __global__ void __launch_bounds__(kRangeThreads) k_split_scatter(KP kp, PairReco
 // first, so a fine range's records leave as one contiguous run (~32 per
 // round) instead of one scattered 8-byte store per record and array
 constexpr int kSplitStageFan = 256;
-constexpr int kSplitStageRows = 4 * kRangeThreads;  // item_rounds' RR records per thread
-__global__ void __launch_bounds__(kRangeThreads) k_split_scatter_staged(KP kp, PairRecords rec, PairRecords stg,
+constexpr int kSplitStageRows = 4 * kSplitThreads;  // item_rounds' RR records per thread
+__global__ void __launch_bounds__(kSplitThreads) k_split_scatter_staged(KP kp, PairRecords rec, PairRecords stg,
                                                                        const uint4* __restrict__ items,
                                                                        const unsigned* __restrict__ n_items,
                                                                        unsigned* __restrict__ fine_cur,
                                                                        const unsigned* __restrict__ item_hist) {
-  __shared__ unsigned long long start[kRangeThreads];
-  __shared__ unsigned pre[kRangeThreads], wsum[kRangeThreads / 64 + 1];
+  __shared__ unsigned long long start[kSplitThreads];
+  __shared__ unsigned pre[kSplitThreads], wsum[kSplitThreads / 64 + 1];
   __shared__ unsigned lcur[kSplitStageFan], hist[kSplitStageFan], hstart[kSplitStageFan], gbase[kSplitStageFan];
   __shared__ unsigned long long skey[kSplitStageRows];
   __shared__ double sf0[kSplitStageRows], sf1[kSplitStageRows], sf2[kSplitStageRows];
@@ -3444,7 +3455,7 @@ __global__ void __launch_bounds__(kBlock) k_fine_plan(KP kp, const unsigned* __r
 
 // one workgroup per fine item: contiguous records of one 2^kRangeBits range,
 // summed in LDS (or added directly when few), then coalesced atomics
-__global__ void __launch_bounds__(kRangeThreads) k_fine_reduce(KP kp, PairRecords stg, const uint4* __restrict__ items,
+__global__ void __launch_bounds__(kReduceThreads) k_fine_reduce(KP kp, PairRecords stg, const uint4* __restrict__ items,
                                                               const unsigned* __restrict__ n_items,
                                                               pdp_partition_accumulators acc, unsigned* err) {
   extern __shared__ unsigned long long smem[];
@@ -3892,7 +3903,7 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     PDP_HIP_CHECK(hipGetLastError());
     if (!p.two_level) {
       PDP_PROF_BEGIN("k_range_reduce", st);
-      hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kRangeThreads), kRangeLds, st, kp, rec,
+      hipLaunchKernelGGL(k_range_reduce, dim3((unsigned)p.n_groups), dim3(kReduceThreads), kRangeLds, st, kp, rec,
                          (const uint4*)items, (const unsigned*)n_items, acc, err);
       PDP_PROF_END(st);
       PDP_HIP_CHECK(hipGetLastError());
@@ -3910,7 +3921,7 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     PDP_HIP_CHECK(hipMemsetAsync(fine_total, 0, (uint64_t)(p.n_fine + 1) * 4, st));
     PDP_PROF_BEGIN("k_split_count", st);
     unsigned* item_hist = (unsigned*)(ws + w.item_hist);
-    hipLaunchKernelGGL(k_split_count, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec,
+    hipLaunchKernelGGL(k_split_count, dim3((unsigned)p.n_groups), dim3(kSplitThreads), 0, st, kp, rec,
                        (const uint4*)items, (const unsigned*)n_items, fine_total, item_hist);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
@@ -3919,10 +3930,10 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     PDP_HIP_CHECK(hipMemcpyAsync(fine_cur, fine_total, (uint64_t)p.n_fine * 4, hipMemcpyDeviceToDevice, st));
     PDP_PROF_BEGIN("k_split_scatter", st);
     if ((1 << (kp.range_bits - kRangeBits)) <= kSplitStageFan && PDP_SPLIT_STAGED)
-      hipLaunchKernelGGL(k_split_scatter_staged, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
+      hipLaunchKernelGGL(k_split_scatter_staged, dim3((unsigned)p.n_groups), dim3(kSplitThreads), 0, st, kp, rec, stg,
                          (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
     else
-      hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kRangeThreads), 0, st, kp, rec, stg,
+      hipLaunchKernelGGL(k_split_scatter, dim3((unsigned)p.n_groups), dim3(kSplitThreads), 0, st, kp, rec, stg,
                          (const uint4*)items, (const unsigned*)n_items, fine_cur, (const unsigned*)item_hist);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
@@ -3937,7 +3948,7 @@ int launch_merge(const KP& kp0, const Plan& p, hipStream_t st, char* ws, const W
     PDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_fine_reduce, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)kFineLds));
     PDP_PROF_BEGIN("k_fine_reduce", st);
-    hipLaunchKernelGGL(k_fine_reduce, dim3((unsigned)p.fine_items), dim3(kRangeThreads), kFineLds, st, kp, stg,
+    hipLaunchKernelGGL(k_fine_reduce, dim3((unsigned)p.fine_items), dim3(kReduceThreads), kFineLds, st, kp, stg,
                        (const uint4*)fitems, (const unsigned*)n_fitems, acc, err);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());

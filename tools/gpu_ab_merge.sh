@@ -13,12 +13,12 @@ fi
 for pass in $(seq 1 ${ROUNDS:-2}); do
 for so in abv/*.so; do
   v=$(basename $so .so)
-  for w in c4 c5; do
-    PIPELINEDP_AMD_LIB=$PWD/$so timeout -k 10 240 python -u bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline --no-api > $OUT/$v.$w.$pass.log 2>&1 || { echo "variant $v $w failed"; tail -5 $OUT/$v.$w.$pass.log; exit 1; }
+  for w in ${WORKLOADS:-c4 c5}; do
+    PIPELINEDP_AMD_LIB=$PWD/$so timeout -k 10 240 python -u bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline --no-api --no-secondary > $OUT/$v.$w.$pass.log 2>&1 || { echo "variant $v $w failed"; tail -5 $OUT/$v.$w.$pass.log; exit 1; }
     python3 - $OUT/$v.$w.$pass.log $v.$w.$pass <<'PY'
 import json, sys
 r = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-print(sys.argv[2], "ms/step %.3f" % r["ms_per_step"], {k: round(v["ms"], 3) for k, v in r["kernels"].items() if k.startswith(("k_split", "k_fine", "k_range"))})
+print(sys.argv[2], "ms/step %.3f" % r["ms_per_step"], {k: round(v["ms"], 3) for k, v in r["kernels"].items() if k.startswith(("k_split", "k_fine", "k_range", "k_sieve_l1"))})
 PY
   done
 done
