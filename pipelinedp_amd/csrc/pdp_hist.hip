@@ -471,7 +471,8 @@ __global__ void __launch_bounds__(kPairsBlock) k_h_pairs(HT t, const Slot* __res
   flush_small(H, lds, 0, H_LINF);
 }
 
-__global__ void __launch_bounds__(kBlock) k_h_ids(HT t, const unsigned long long* __restrict__ pidstat,
+constexpr int kIdsThreads = 1024;  // 16 waves per CU at one workgroup per CU (256 threads: 0.20 ms, latency-bound)
+__global__ void __launch_bounds__(kIdsThreads) k_h_ids(HT t, const unsigned long long* __restrict__ pidstat,
                                                   const unsigned long long* __restrict__ pkstat,
                                                   const double* __restrict__ psum, IntHists H,
                                                   unsigned long long* minmax) {
@@ -1959,7 +1960,7 @@ int hist_finish(const HCall& c, const pdp_histogram_bins* out) {
   if (m > 0)
     // at most 256 workgroups: each flushes its small bins with one global
     // atomic per bin, and 2,048 of them made those flushes most of the kernel
-    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3(grid_for(m, 256)), dim3(kBlock), 0, st, t,
+    PDP_HLAUNCH("k_h_ids", st, k_h_ids, dim3((unsigned)((m + kIdsThreads - 1) / kIdsThreads < 256 ? (m + kIdsThreads - 1) / kIdsThreads : 256)), dim3(kIdsThreads), 0, st, t,
                 (const unsigned long long*)(ws + w.pidstat), pkstat, psum, c.H, minmax);
   PDP_HLAUNCH("k_h_lowers", st, k_h_lowers, dim3((kNLowers + kBlock - 1) / kBlock, 2), dim3(kBlock), 0, st, minmax,
               out->float_lowers, out->float_n_lowers);
