@@ -7,7 +7,7 @@ T=${1:-abm}
 OUT=gpurun_out/$T
 mkdir -p $OUT
 if [ -n "$PARITY" ]; then
-  PIPELINEDP_AMD_LIB=$PWD/abv/$PARITY.so timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_scale.py -k "two_level or half_size or range_merge or c4" -x -q --timeout 250 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $OUT/pytest.log; exit 1; }
+  PIPELINEDP_AMD_LIB=$PWD/abv/$PARITY.so timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_scale.py ${PARITY_FILES:-} -k "${PARITY_K:-two_level or half_size or range_merge or c4}" -x -q --timeout 250 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "PYTEST FAILED"; tail -30 $OUT/pytest.log; exit 1; }
   echo "parity $PARITY: $(tail -1 $OUT/pytest.log)"
 fi
 for pass in $(seq 1 ${ROUNDS:-2}); do
