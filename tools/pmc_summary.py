@@ -33,7 +33,8 @@ def short_name(full):
         return "k_h_float_max"
     # the tile-local partition kernels report under the pass names the
     # library's profiler (and bench.py) use
-    return {"k_scatter_l1_local": "k_scatter_l1", "k_scatter_l2_local": "k_scatter_l2"}.get(m.group(1), m.group(1))
+    return {"k_scatter_l1_local": "k_scatter_l1", "k_scatter_l2_local": "k_scatter_l2",
+            "k_split_scatter_staged": "k_split_scatter"}.get(m.group(1), m.group(1))
 
 
 def main():
