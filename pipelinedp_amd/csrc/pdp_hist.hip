@@ -544,8 +544,11 @@ template <bool STEP0>
 __device__ __forceinline__ int lin_bin(const LinBins& z, double v) {
   const int nb = z.nb;
   if (nb <= 1) return 0;
-  int b = (int)((v - z.mn) * z.inv);  // a guess; the loops make it exact
-  b = b < 0 ? 0 : (b > nb - 1 ? nb - 1 : b);
+  // a guess; the loops make it exact.  The guess is converted only when it
+  // lies in [0, nb): a subnormal range overflows inv to inf, and v == mn then
+  // gives 0 * inf = NaN
+  const double g = (v - z.mn) * z.inv;
+  int b = g >= 0.0 && g < (double)nb ? (int)g : (g >= (double)nb ? nb - 1 : 0);
   while (b + 1 < nb && lin_lower<STEP0>(z, b + 1) <= v) ++b;
   while (b > 0 && lin_lower<STEP0>(z, b) > v) --b;
   return b;

@@ -172,6 +172,21 @@ def test_single_row_and_constant_sums():
     assert got.linf_sum_contributions_histogram.bins[0].lower == got.linf_sum_contributions_histogram.bins[0].upper
 
 
+def test_subnormal_value_range():
+    """Pair and partition sums that span a few subnormals: np.linspace's step
+    (delta / 10,000) underflows to 0, so the lowers take numpy's other form,
+    (i / 10,000) * delta + start (k_h_lowers and the float passes' STEP0
+    path), and the bin guess's 1 / delta overflows; bins must still equal the
+    oracle's exactly."""
+    rng = np.random.default_rng(11)
+    n = 50_000
+    pid = rng.integers(0, 5_000, n)
+    pk = rng.integers(0, 500, n)
+    val = rng.integers(0, 4, n) * 5e-324
+    got = _run_codes(pid, pk, val, U=5_000, P=500)
+    _check_all(got, OH.dataset_histograms(pid, pk, val), "subnormal")
+
+
 def test_empty_input():
     got = _run_codes(np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0), U=4, P=4)
     for field in OH.HIST_FIELDS:
