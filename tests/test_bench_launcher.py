@@ -46,3 +46,16 @@ def test_pmc_join_checks_the_source_tree(tmp_path):
     traffic, src, refused = bench.load_pmc(str(f), "c3", 2000, 1)  # another size
     assert traffic == {} and "workload" in refused
     assert bench.load_pmc(str(f), "c3", 1000, 2) == ({}, None, None)  # N > 1: never joined
+
+
+def test_pmc_kernel_names_match_the_library_profiler():
+    """rocprofv3 names the template instances; the PMC summary must file them
+    under the library profiler's names, or bench.py joins no bytes for them."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_summary import short_name
+    ns = "void pdp::(anonymous namespace)::"
+    assert short_name(ns + "k_h_float<true>(pdp::(anonymous namespace)::HT, ...)") == "k_h_float_max"
+    assert short_name(ns + "k_h_float<false>(pdp::(anonymous namespace)::HT, ...)") == "k_h_float"
+    assert short_name(ns + "k_split_scatter_staged(pdp::(anonymous namespace)::KP, ...)") == "k_split_scatter"
+    assert short_name(ns + "k_scatter_l2_local<3, 256>(pdp::(anonymous namespace)::KP, ...)") == "k_scatter_l2"
+    assert short_name(ns + "k_sieve_l1<3, false, true, 1024>(pdp::(anonymous namespace)::KP, ...)") == "k_sieve_l1"
