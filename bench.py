@@ -786,14 +786,16 @@ def run_workload(args, workload, world, rank, device, pmc_file):
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
                            check_keys=False, **tune)
-        mine, first = parallel.exchange_accumulators(acc)  # RCCL reduce-scatter; identity at N=1
+        # RCCL reduce-scatter (identity at N=1); counts are at most the global
+        # row count, so the int32 wire format needs no device read
+        mine, first = parallel.exchange_accumulators(acc, int_bound=n * world)
         if share > 1:  # one rank's share: its slice of the partitions (rank 0's)
             mine = {k: (None if t is None else t[:P_pad // share]) for k, t in mine.items()}
         _, _, n_kept = X.select_and_noise(mine, selection=selection, ops=ops, n_cols=3,
                                           seed_select=seed_base ^ (i * 7919 + 1),
                                           seed_noise=seed_base ^ (i * 104729 + 2),
-                                          partition_offset=first)
-        return n_kept
+                                          partition_offset=first, sync_count=False)
+        return n_kept  # a device count: no host round trip inside a step
 
     for i in range(args.warmup):
         step(i)
@@ -809,6 +811,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kept = int(kept)
     # key-error check of the data once (outside the timed region)
     X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding, seed=1,
                        row_offset=rank * n, acc=acc, workspace=ws, check_keys=True, **tune)

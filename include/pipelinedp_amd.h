@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 13
+#define PDP_ABI_VERSION 14
 
 /* error codes */
 #define PDP_OK 0
@@ -155,6 +155,8 @@ typedef struct pdp_bound_plan_info {
   int32_t band;        /* resolved side band, t2 = band / 2^16 (0 = off) */
   int32_t sieve_threads; /* resolved sieve level-1 workgroup size (0 without the sieve) */
   int32_t bucket_threads; /* resolved bucket-kernel workgroup size (BUCKETED) */
+  int32_t hist_u16;    /* tile-local level 1 keeps its per-tile bucket counts as u16 halves */
+  int32_t reserved;
 } pdp_bound_plan_info;
 
 /* Resolves the execution plan for `cfg` (no device work). */
@@ -328,6 +330,13 @@ int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, const pdp_n
  * rather than assumed).  Reads it from the workspace of pdp_bound_contributions
  * (synchronises `stream`). */
 int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
+
+/* The same error word, copied to `flags` by a copy enqueued on `stream`
+ * (nothing synchronises; `flags` should be pinned host memory, valid until the
+ * stream has passed the copy).  The library's API layer reads it once the
+ * aggregate's result is materialised, so the key check costs no pipeline
+ * drain between bounding and the merge. */
+int pdp_bound_error_flags_async(const void* workspace, uint32_t* flags, void* stream);
 
 /* What the last pdp_bound_contributions (BUCKETED) moved, read from its
  * workspace (synchronises `stream`): rows that entered the partition passes

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("PIPELINEDP_AMD_LIB") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libpipelinedp_amd.so")
 
 # constants (include/pipelinedp_amd.h)
-ABI_VERSION = 13
+ABI_VERSION = 14
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
@@ -61,6 +61,7 @@ EXPORTED_SYMBOLS = (
     "pdp_dataset_histograms_preaggregated_weight_offsets",
     "pdp_dataset_histograms_weight_bins",
     "pdp_bound_error_flags",
+    "pdp_bound_error_flags_async",
     "pdp_owner_mismatches",
     "pdp_bound_stats_read",
     "pdp_bound_stats_async",
@@ -119,6 +120,8 @@ class BoundPlanInfo(ctypes.Structure):
         ("band", ctypes.c_int32),
         ("sieve_threads", ctypes.c_int32),
         ("bucket_threads", ctypes.c_int32),
+        ("hist_u16", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
 
 
@@ -249,6 +252,7 @@ def signatures():
         "pdp_dataset_histograms_preaggregated_weight_offsets": (ctypes.c_int, [i64, i64, P(u64), P(u64), P(u64)]),
         "pdp_dataset_histograms_weight_bins": (ctypes.c_int, [vp, vp, i64, P(HistogramBins), vp]),
         "pdp_bound_error_flags": (ctypes.c_int, [vp, P(ctypes.c_uint32), vp]),
+        "pdp_bound_error_flags_async": (ctypes.c_int, [vp, vp, vp]),
         "pdp_owner_mismatches": (ctypes.c_int, [vp, i64, i32, i32, vp, vp]),
         "pdp_bound_stats_read": (ctypes.c_int, [P(BoundConfig), vp, u64, P(BoundStats), vp]),
         "pdp_bound_stats_async": (ctypes.c_int, [P(BoundConfig), vp, u64, vp, vp]),

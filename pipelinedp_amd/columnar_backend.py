@@ -693,7 +693,7 @@ class AggregateRun:
         spec = self._bounding_spec(vk)
         world, _ = parallel.world_info()
         P, _ = parallel.partition_slices(pk_enc.n, world)  # padded to a multiple of the ranks
-        row_offset = parallel.row_offset(pk_t.numel())
+        row_offset, self._total_rows = parallel.row_offset_and_total(pk_t.numel())
         allowed = None
         if public_codes is not None:
             mask = np.zeros(P, dtype=np.uint8)
@@ -709,7 +709,7 @@ class AggregateRun:
             tune = self.backend._tuning
             acc = X.bound_and_reduce(pid_t, pk_t, val_t, n_privacy_ids=n_pid, n_partitions=P,
                                      bounding=spec, seed=seed_bound, allowed=allowed, row_offset=row_offset,
-                                     workspace=self.backend._workspace, **tune)
+                                     workspace=self.backend._workspace, check_keys="defer", **tune)
             self.backend.last_plan_info = X.bound_plan(pk_t.numel(), n_pid, P, spec, **tune)
             self.backend.last_bounding = spec
         return acc, spec, pk_enc, allowed
@@ -744,7 +744,10 @@ class AggregateRun:
         import torch
         from pipelinedp_amd import executor as X
         acc, spec, pk_enc, allowed = self._bound()
-        acc, first = parallel.exchange_accumulators(acc)  # identity on one rank
+        # int64 fields: counts and privacy-id counts are at most the global
+        # row count; an int SUM has no such bound (its maximum is read back)
+        int_bound = None if spec.sum_is_int else self._total_rows
+        acc, first = parallel.exchange_accumulators(acc, int_bound=int_bound)  # identity on one rank
         sel = self._selection()
         public = self.plan.public_keys is not None or self.plan.public_padding is not None
         public_mask = None
@@ -757,6 +760,7 @@ class AggregateRun:
                                                 seed_noise=seed_noise, public_mask=public_mask,
                                                 partition_offset=first)
         idx = index.cpu().numpy()
+        self._raise_key_errors()  # the deferred key check (its copy has landed: index.cpu() synchronised)
         if self.plan.keys_only:  # select_partitions: "Drop accumulators, keep only partition keys"
             return pk_enc.keys_of(first + idx).tolist()
         nf = len(self.prog.fields)
@@ -771,6 +775,7 @@ class AggregateRun:
     def raw_accumulators(self):
         acc, spec, pk_enc, allowed = self._bound()
         host = {k: (None if v is None else v.cpu().numpy()) for k, v in acc.items()}
+        self._raise_key_errors()
         public = allowed.cpu().numpy().astype(bool) if allowed is not None else None
         out = {}
         for p in range(pk_enc.n):
@@ -797,6 +802,11 @@ class AggregateRun:
             row_count = rc + (1 if public is not None else 0)  # empty public accumulator
             out[pk_enc.key_of(p)] = (row_count, tuple(children))
         return out
+
+    def _raise_key_errors(self):
+        from pipelinedp_amd import executor as X
+        if self.backend._workspace is not None:
+            X.raise_key_errors(self.backend._workspace)
 
     @property
     def _seeds(self):

@@ -129,6 +129,12 @@ int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream) 
   return PDP_OK;
 }
 
+int pdp_bound_error_flags_async(const void* workspace, uint32_t* flags, void* stream) {
+  if (workspace == nullptr || flags == nullptr) return pdp::set_error(PDP_E_INVALID, "NULL argument");
+  PDP_HIP_CHECK(hipMemcpyAsync(flags, workspace, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  return PDP_OK;
+}
+
 int pdp_profiler_enable(int enable) {
   std::lock_guard<std::mutex> lock(pdp::g_prof_mu);
   for (auto& r : pdp::g_prof) {

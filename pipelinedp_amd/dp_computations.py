@@ -21,6 +21,7 @@ These are scalars computed once per aggregation on the host; the per-partition
 work (noise draws, keep decisions) runs in the HIP kernels.
 """
 import dataclasses
+import functools
 import math
 from typing import Any, List, Optional, Tuple
 
@@ -577,6 +578,14 @@ def adjusted_delta(delta: float, max_partitions_contributed: int) -> float:
 
 def truncated_geometric_keep_table(eps: float, delta: float, max_partitions_contributed: int,
                                    max_len: int = 1 << 22) -> np.ndarray:
+    """The table below, computed once per parameter set (an aggregation
+    recomputes it per call otherwise: a Python loop over the table's length).
+    The returned array is read-only (it is shared)."""
+    return _keep_table(float(eps), float(delta), int(max_partitions_contributed), int(max_len))
+
+
+@functools.lru_cache(maxsize=256)
+def _keep_table(eps: float, delta: float, max_partitions_contributed: int, max_len: int) -> np.ndarray:
     """pi[n] = probability that truncated-geometric selection keeps a partition
     with n privacy units (PyDP "truncated_geometric", the optimal (eps, delta)
     partition selection of Desfontaines et al.), n = 0..len-1; pi[len-1]
@@ -599,7 +608,9 @@ def truncated_geometric_keep_table(eps: float, delta: float, max_partitions_cont
             break
         if d == 0.0 and len(table) > 1:  # delta = 0: never keep
             break
-    return np.asarray(table, dtype=np.float64)
+    out = np.asarray(table, dtype=np.float64)
+    out.flags.writeable = False
+    return out
 
 
 def truncated_geometric_keep_probability(n: int, eps: float, delta: float,

@@ -252,6 +252,28 @@ class BoundWorkspace:
     def __init__(self):
         self.buf = None
         self.last_cfg = None
+        self._err_host = None   # pinned u32: the deferred copy of the error word
+        self._err_event = None  # recorded after that copy
+        self._err_keys = None   # (n_privacy_ids, n_partitions) for the message
+
+    def defer_error_check(self, ws, sobj, n_privacy_ids, n_partitions):
+        torch = _torch()
+        if self._err_event is not None:  # an unread check: read it first (its copy owns the block)
+            self.raise_deferred()
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        N.check(N.lib().pdp_bound_error_flags_async(_ptr(ws), ctypes.c_void_p(self._err_host.data_ptr()),
+                                                    int(sobj.cuda_stream)), "pdp_bound_error_flags_async")
+        self._err_event = torch.cuda.Event()
+        self._err_event.record(sobj)
+        self._err_keys = (n_privacy_ids, n_partitions)
+
+    def raise_deferred(self):
+        ev, self._err_event = self._err_event, None
+        if ev is None:
+            return
+        ev.synchronize()
+        _raise_error_flags(int(self._err_host.item()) & 0xFFFFFFFF, *self._err_keys)
 
     def stats(self, stream=None) -> dict:
         """pdp_bound_stats_read of the last bound_and_reduce on this workspace
@@ -296,11 +318,23 @@ _feedback = {}
 class _PlanFeedback:
     def __init__(self):
         torch = _torch()
-        self.host = torch.zeros(4, dtype=torch.int32, pin_memory=True)  # uint32 counters
+        self.host = torch.zeros(4, dtype=torch.int32, pin_memory=True)  # uint32 counters (read & 0xFFFFFFFF)
         self.event = None    # recorded after the copies into `host`
         self.band = False    # the measured plan had the side band
         self.unsieved = False
         self.calls = 0
+
+    def idle(self) -> bool:
+        """No copy into `host` is pending (the pinned block may be released)."""
+        return self.event is None or self.event.query()
+
+
+def _evict_feedback():
+    """Drops idle entries; an entry whose pinned counters are still the
+    target of an enqueued copy stays (its block must not be reused before the
+    copy lands)."""
+    for key in [k for k, fb in _feedback.items() if fb.idle()]:
+        del _feedback[key]
 
 
 def _feedback_key(pid, pk, n, U, P, bounding, row_offset):
@@ -315,7 +349,7 @@ def _feedback_sieve(key) -> int:
     if fb is None:
         return 0
     if fb.event is not None and fb.event.query():
-        c = fb.host.tolist()
+        c = [v & 0xFFFFFFFF for v in fb.host.tolist()]
         slow = (c[2] if fb.band else c[0]) > RESCAN_BLOOM_MAX
         fb.unsieved = fb.unsieved or slow
         fb.event = None
@@ -338,7 +372,7 @@ def plan_feedback_state(pid, pk, *, n_privacy_ids, n_partitions, bounding, row_o
 def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                      bounding: BoundingSpec, seed: int, row_offset: int = 0, allowed=None,
                      acc=None, workspace: Optional[BoundWorkspace] = None, stream=None,
-                     check_keys: bool = True, timer: Optional["StageTimer"] = None,
+                     check_keys=True, timer: Optional["StageTimer"] = None,
                      algorithm: int = N.ALGO_AUTO, merge: int = N.MERGE_AUTO,
                      key_format: int = N.KEYS_AUTO, sieve: int = 0, sieve_band: int = 0,
                      sieve_threads: int = 0, bucket_threads: int = 0):
@@ -374,6 +408,8 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     if bounding.linf < 0 or bounding.linf > N.MAX_LINF:
         raise NotImplementedError(f"max_contributions_per_partition={bounding.linf} is outside "
                                   f"the supported range [1, {N.MAX_LINF}]")
+    if check_keys == "defer" and workspace is None:  # nowhere to leave the deferred word
+        check_keys = True
     feedback = (sieve == 0 and algorithm == N.ALGO_AUTO and n > 0)
     fkey = _feedback_key(pid, pk, n, n_privacy_ids, n_partitions, bounding, row_offset) if feedback else None
     if feedback:
@@ -388,21 +424,23 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     wsobj.last_cfg = cfg
     if acc is None:
         acc = new_accumulators(n_partitions, bounding, device)
-    st = _stream(stream)
+    # one stream object for the launches and for every event recorded after them
+    sobj = stream if stream is not None else torch.cuda.current_stream(device)
+    st = int(sobj.cuda_stream)
     _mark(timer, "bound")
     N.check(lib.pdp_bound_contributions(ctypes.byref(cfg), _ptr(pid), _ptr(pk), _ptr(value),
                                         _ptr(allowed), _ptr(ws), ws.numel(), st),
             "pdp_bound_contributions")
     _mark(timer, "reduce")
-    if check_keys:
+    if check_keys == "defer":
+        # the error word copied into pinned memory behind the launches; read by
+        # raise_key_errors() once the caller synchronises anyway (the public
+        # API: when the result is materialised), so no drain here
+        wsobj.defer_error_check(ws, sobj, n_privacy_ids, n_partitions)
+    elif check_keys:
         flags = ctypes.c_uint32(0)
         N.check(lib.pdp_bound_error_flags(_ptr(ws), ctypes.byref(flags), st), "pdp_bound_error_flags")
-        if flags.value & 1:
-            raise ValueError("privacy_id / partition_key outside the dense key range "
-                             f"[0, {n_privacy_ids}) x [0, {n_partitions})")
-        if flags.value & 2:
-            raise N.NativeLibraryError("the sieve's fix-up row list outgrew its workspace region "
-                                       "(pdp_bound_error_flags bit 1; a library bug)")
+        _raise_error_flags(flags.value, n_privacy_ids, n_partitions)
     N.check(lib.pdp_reduce_partitions(ctypes.byref(cfg), _ptr(value), _ptr(ws), ws.numel(),
                                       ctypes.byref(_acc_struct(acc)), st),
             "pdp_reduce_partitions")
@@ -412,7 +450,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
             fb = _feedback.get(fkey)
             if fb is None:
                 if len(_feedback) > 256:
-                    _feedback.clear()
+                    _evict_feedback()
                 fb = _feedback[fkey] = _PlanFeedback()
             if fb.event is None:
                 N.check(lib.pdp_bound_stats_async(ctypes.byref(cfg), _ptr(ws), ws.numel(),
@@ -420,9 +458,43 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
                         "pdp_bound_stats_async")
                 fb.band = bool(info.band)
                 fb.event = torch.cuda.Event()
-                fb.event.record(stream if stream is not None else torch.cuda.current_stream(device))
+                fb.event.record(sobj)
     _mark(timer, "end_bound")
     return acc
+
+
+def _raise_error_flags(flags: int, n_privacy_ids, n_partitions):
+    if flags & 1:
+        raise ValueError("privacy_id / partition_key outside the dense key range "
+                         f"[0, {n_privacy_ids}) x [0, {n_partitions})")
+    if flags & 2:
+        raise N.NativeLibraryError("the sieve's fix-up row list outgrew its workspace region "
+                                   "(pdp_bound_error_flags bit 1; a library bug)")
+
+
+def raise_key_errors(workspace: "BoundWorkspace"):
+    """The deferred key check of the last bound_and_reduce(check_keys="defer")
+    on `workspace`: waits for its error-word copy (the caller has normally
+    synchronised already) and raises as check_keys=True would have."""
+    workspace.raise_deferred()
+
+
+_tables = {}
+
+
+def _device_table(values, device):
+    """The truncated-geometric keep table on `device`, copied once per
+    (device, contents): a pageable host-to-device copy per call would
+    synchronise the stream between bounding and selection."""
+    torch = _torch()
+    arr = np.ascontiguousarray(values, dtype=np.float64)
+    key = (str(device), arr.tobytes())
+    t = _tables.get(key)
+    if t is None:
+        if len(_tables) > 64:
+            _tables.clear()
+        t = _tables[key] = torch.as_tensor(arr).to(device)
+    return t
 
 
 def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], n_cols: int,
@@ -451,7 +523,7 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
     sc.max_rows_per_privacy_id = int(selection.max_rows_per_privacy_id)
     sc.pre_threshold = int(selection.pre_threshold or 0)
     if selection.strategy == N.SELECT_TRUNCATED_GEOMETRIC:
-        table = torch.as_tensor(np.ascontiguousarray(selection.keep_prob, dtype=np.float64)).to(device)
+        table = _device_table(selection.keep_prob, device)
         sc.keep_table_len = int(table.numel())
         sc.keep_prob = _ptr(table)
     sc.noise = (selection.noise or NO_NOISE).to_c()

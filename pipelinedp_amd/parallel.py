@@ -26,13 +26,17 @@ def partition_slices(n_partitions: int, world: int) -> Tuple[int, int]:
     return padded, padded // world
 
 
-def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None, narrow_ints: bool = True):
+def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None, narrow_ints: bool = True,
+                          int_bound: Optional[int] = None):
     """Sums the dense accumulators of all ranks and returns (this rank's
     slice of every accumulator, global index of the slice's first partition).
     Accumulator tensors must have the padded length partition_slices(...)[0].
     narrow_ints: int64 fields (counts, privacy-id counts, int sums) travel as
-    int32 when the global maximum proves no sum can overflow (exact either
-    way; half the bytes of those fields over xGMI)."""
+    int32 when no sum can overflow (exact either way; half the bytes of those
+    fields over xGMI).  int_bound: a host-known bound on every int64 entry's
+    sum over the ranks (counts and privacy-id counts are at most the global
+    row count) -- then the choice needs no device read; without it the global
+    maximum is read back (one MAX all-reduce and a device-to-host copy)."""
     import torch
     import torch.distributed as dist
     world, rank = world_info(group)
@@ -57,7 +61,10 @@ def exchange_accumulators(acc: Dict[str, Optional["torch.Tensor"]], group=None, 
     for dtype, names in by_dtype.items():
         stacked = torch.stack([acc[n].reshape(world, slice_len) for n in names], dim=1).contiguous()
         wire = stacked
-        if dtype == torch.int64 and narrow_ints:
+        if dtype == torch.int64 and narrow_ints and int_bound is not None:
+            if 0 <= int_bound < 2 ** 31:
+                wire = stacked.to(torch.int32)
+        elif dtype == torch.int64 and narrow_ints:
             # counts and privacy-id counts travel as int32 when no sum over
             # ranks can reach 2^31: every rank's entries lie in [0, m] with m
             # the global maximum (one all-reduce of 8 bytes), so every sum of
@@ -134,10 +141,16 @@ def _all_gather_var(arr, group=None):
 def row_offset(n_rows: int, group=None) -> int:
     """Global index of this rank's first row (ranks' shards concatenated in
     rank order); row sampling priorities are keyed by it."""
+    return row_offset_and_total(n_rows, group)[0]
+
+
+def row_offset_and_total(n_rows: int, group=None) -> Tuple[int, int]:
+    """(row_offset, rows over all ranks) from one all-gather of the sizes."""
     world, rank = world_info(group)
     if world == 1:
-        return 0
-    return int(sum(_all_gather_sizes(n_rows, group)[:rank]))
+        return 0, int(n_rows)
+    sizes = _all_gather_sizes(n_rows, group)
+    return int(sum(sizes[:rank])), int(sum(sizes))
 
 
 def _key_kind(decode) -> str:

@@ -416,3 +416,32 @@ def test_parquet_ingest_matches_reference_golden(device, tmp_path, name):
     assert set(G._key(k) for k in got) == set(want)
     for k, v in got.items():
         G.assert_acc_equal(want[G._key(k)], v, f"{name}[{k}]")
+
+
+def test_out_of_range_keys_raise_when_the_result_is_read(device):
+    """The key-range check of the API path is deferred (the error word is
+    copied to pinned memory behind the bounding launches):
+    an out-of-range partition code still raises ValueError, at the first read
+    of the result, and the same backend then aggregates a valid table."""
+    import torch
+    rng = np.random.default_rng(3)
+    n, U, P = 100_000, 5_000, 100
+    pid = torch.as_tensor(rng.integers(0, U, n)).to(device)
+    pk = torch.as_tensor(rng.integers(0, P, n)).to(device)
+    v = torch.as_tensor(rng.random(n)).to(device)
+    bad = pk.clone()
+    bad[777] = P + 5
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM], noise_kind=pdp.NoiseKind.LAPLACE,
+                                 max_partitions_contributed=2, max_contributions_per_partition=1,
+                                 min_value=0.0, max_value=1.0)
+    backend = CB.ColumnarBackend(device=device, seed=3)
+    for col, raises in ((bad, True), (pk, False), (bad, True)):
+        acc = pdp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+        table = pdp.ColumnTable({"pid": pid, "pk": col, "v": v}, n_privacy_ids=U, n_partitions=P)
+        sink = pdp.DPEngine(acc, backend).aggregate(table, params, _ext())
+        acc.compute_budgets()
+        if raises:
+            with pytest.raises(ValueError, match="outside the dense key range"):
+                list(sink)
+        else:
+            assert len(list(sink)) > 0

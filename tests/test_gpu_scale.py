@@ -133,6 +133,30 @@ def test_packed_sparse_super_bucket_spans_many_tiles(device):
     _compare(got, want, _scale(pk, val, P, spec))
 
 
+# ---------------------------------------------------------------------- C1 --
+def test_c1_movie_view_matches_oracle(device):
+    """BASELINE config 1 itself: 1e6 movie_view rows
+    (oracle/local_backend_port.movie_view_rows, the CPU baseline's input),
+    COUNT + SUM of int ratings clipped to [1, 5], L0 = 2, Linf = 1 (both
+    samplings fire: ~10 rows per user, Zipf movies).  Movie ids are dense
+    codes (17,771 partitions, code 0 unused).  Counts, privacy-id counts and
+    the int64 SUM bit-exact against the oracle (the auto plan)."""
+    from oracle.local_backend_port import movie_view_rows
+    from pipelinedp_amd import executor as X
+    rows = np.asarray(movie_view_rows(1_000_000, seed=0), dtype=np.int64)
+    pid, pk, val = rows[:, 0].copy(), rows[:, 1].copy(), rows[:, 2].copy()
+    U, P = 100_000, 17_771
+    spec = X.BoundingSpec(l0=2, linf=1, value_kind=O.VALUE_I64, flags=O.ACC_SUM | O.SUM_INT, min_value=1,
+                          max_value=5, middle=3.0)
+    plan = _plan(len(pid), U, P, spec)
+    want = _oracle(pid, pk, val, U, P, spec, 1234, plan.rand_shift)
+    got = _gpu(device, pid, pk, val, U, P, spec, 1234)
+    for k in ("privacy_id_count", "count", "sum"):
+        np.testing.assert_array_equal(got[k], want[k])
+    assert (got["count"] == got["privacy_id_count"]).all()  # Linf = 1: one row per kept pair
+    assert got["privacy_id_count"].sum() < len(pid)  # cross-partition sampling fired
+
+
 # ---------------------------------------------------------------------- C2 --
 def _c2(seed=1):
     rng = np.random.default_rng(seed)

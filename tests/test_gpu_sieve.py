@@ -320,24 +320,31 @@ def test_plan_feedback_runs_light_user_tables_unsieved(device):
         assert ws.stats()["sieve"] > 0
 
 
-@pytest.mark.parametrize("sieve", [-1, 32768], ids=["tile-local", "sieve"])
-def test_tile_with_every_row_in_one_bucket(device, sieve):
+@pytest.mark.parametrize("sieve,U,u16", [(-1, 300_000, 0), (32768, 300_000, 0), (-1, 40_000_000, 1),
+                                         (16384, 20_000_000, 1)],
+                         ids=["tile-local", "sieve", "tile-local-u16", "sieve-band-u16"])
+def test_tile_with_every_row_in_one_bucket(device, sieve, U, u16):
     """Level 1 keeps a tile's bucket counts as u16 (flush_counts16); a bucket
     holding all 65,536 rows of a tile (counted 65,536, stored as 0 with the
     bucket in tile_over) must still get all of them.  Tile 0 here: every row
     from the first 2,048 privacy ids (bucket 0 at b = 11), and with the sieve
-    every such row a candidate (pair hash below t = 1/2); equal to the oracle."""
+    every such row a candidate (pair hash below t); equal to the oracle.
+    u16: so many buckets that level 1 counts each half tile in u16 lanes
+    (counts_tm / counts_tm2, Plan.hist_u16): the bucket's two halves are
+    32,768 each and their sum 65,536 carries out of its lane in the column
+    scan unless the lanes are added apart (k_gscan_sums)."""
     from pipelinedp_amd import executor as X
     spec = _spec((2, 1, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
-    U, P = 300_000, 4096
+    P = 4096
     seed = 9191
-    plan = X.bound_plan(3 * 65536, U, P, spec, sieve=sieve)
-    assert plan.bucket_bits == 11 and (plan.sieve > 0) == (sieve > 0)
+    plan = X.bound_plan(3 * 65536 + 321, U, P, spec, sieve=sieve)
+    assert plan.bucket_bits == 11 and (plan.sieve > 0) == (sieve > 0) and plan.hist_u16 == u16, \
+        (plan.bucket_bits, plan.sieve, plan.hist_u16)
     rng = np.random.default_rng(5)
     cu = rng.integers(0, 2048, 200_000)
     ck = rng.integers(0, P, 200_000)
     if sieve > 0:
-        low = O.pair_hash(seed, cu, ck) < np.uint32(1 << 31)
+        low = O.pair_hash(seed, cu, ck) < np.uint32(sieve << 16)
         cu, ck = cu[low], ck[low]
     idx = rng.integers(0, len(cu), 65536)
     pid = np.concatenate([cu[idx], rng.integers(0, U, 2 * 65536 + 321)])
@@ -347,3 +354,33 @@ def test_tile_with_every_row_in_one_bucket(device, sieve):
     want = _want(pid, pk, val, U, P, spec, seed)
     scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
     _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve), want, scale)
+
+
+def test_fixup_list_capacity_guard_raises(device, monkeypatch):
+    """The fix-up row list's writes are guarded by its capacity and an
+    overflow sets bit 1 of the error word, which bound_and_reduce raises
+    (the guard was untested).  The region cannot overflow
+    for real (each list holds distinct rows), so the test hook
+    PIPELINEDP_AMD_FIX_CAP shrinks it to 64 entries under a table whose
+    fix-up lists thousands of rows; afterwards the device is healthy and the
+    full region gives the oracle's result."""
+    from pipelinedp_amd import _native as N
+    spec = _spec((3, 2, O.VALUE_F64, O.ACC_SUM | O.ACC_NSUM, 0.0, 10.0, None, 0))
+    U, P = 120_000, 50_000
+    rng = np.random.default_rng(31)
+    big = rng.integers(0, 100_000, 100 * 100_000)
+    small = np.repeat(np.arange(100_000, U), rng.integers(1, 4, U - 100_000))
+    pid = rng.permutation(np.concatenate([big, small]))
+    n = len(pid)
+    pk = rng.integers(0, P, n)
+    val = rng.random(n) * 10.0
+    seed = 5150
+    monkeypatch.setenv("PIPELINEDP_AMD_TEST_HOOKS", "1")
+    monkeypatch.setenv("PIPELINEDP_AMD_FIX_CAP", "64")
+    for band in (0, -1):  # the band's lists and the whole-column re-read both fill the list
+        with pytest.raises(N.NativeLibraryError, match="outgrew its workspace region"):
+            _run(device, pid, pk, val, U, P, spec, seed, 6000, band=band)
+    monkeypatch.delenv("PIPELINEDP_AMD_FIX_CAP")
+    want = _want(pid, pk, val, U, P, spec, seed)
+    _compare(_run(device, pid, pk, val, U, P, spec, seed, 6000), want,
+             _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle))

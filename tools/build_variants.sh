@@ -17,8 +17,15 @@ for src in pipelinedp_amd/csrc/*.hip; do
   common+=($obj)
 done
 wait
+# a variant named NAME builds abv_src/NAME/pdp_bound.hip instead when that file
+# exists (e.g. an older revision: git show REV:pipelinedp_amd/csrc/pdp_bound.hip)
 build() {
-  /opt/rocm/bin/hipcc $FLAGS "${@:2}" -c pipelinedp_amd/csrc/pdp_bound.hip -o build/abv_common/bound_$1.o
+  local src=pipelinedp_amd/csrc/pdp_bound.hip
+  if [ -f abv_src/$1/pdp_bound.hip ]; then
+    cp pipelinedp_amd/csrc/pdp_internal.h abv_src/$1/
+    src=abv_src/$1/pdp_bound.hip
+  fi
+  /opt/rocm/bin/hipcc $FLAGS "${@:2}" -c $src -o build/abv_common/bound_$1.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abv/$1.so build/abv_common/bound_$1.o "${common[@]}"
 }
 for spec in "$@"; do
