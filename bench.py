@@ -780,9 +780,7 @@ def run_workload(args, workload, world, rank, device, pmc_file):
     seed_base = args.seed
 
     def step(i):
-        for t in acc.values():
-            if t is not None:
-                t.zero_()
+        X.zero_accumulators(acc)  # one fill: the fields share a block
         X.bound_and_reduce(pid, pk, value, n_privacy_ids=U, n_partitions=P_pad, bounding=bounding,
                            seed=seed_base + i, row_offset=rank * n, acc=acc, workspace=ws,
                            check_keys=False, **tune)

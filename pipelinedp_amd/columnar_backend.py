@@ -759,12 +759,13 @@ class AggregateRun:
                                                 n_cols=len(self.prog.fields), seed_select=seed_select,
                                                 seed_noise=seed_noise, public_mask=public_mask,
                                                 partition_offset=first)
-        idx = index.cpu().numpy()
-        self._raise_key_errors()  # the deferred key check (its copy has landed: index.cpu() synchronised)
+        idx, vals = X.kept_to_host(index, out, n_kept, keys_only=self.plan.keys_only)
+        self._raise_key_errors()  # the deferred key check (its copy has landed: the stream was synchronised)
         if self.plan.keys_only:  # select_partitions: "Drop accumulators, keep only partition keys"
             return pk_enc.keys_of(first + idx).tolist()
         nf = len(self.prog.fields)
-        vals = out[:, :n_kept].cpu().numpy() if n_kept else np.zeros((nf, 0))
+        if not n_kept:
+            vals = np.zeros((nf, 0))
         keep = np.ones(len(idx), dtype=bool)
         if self.prog.threshold_combiner is not None:  # dp_engine.py:544-549: drop thresholded None (NaN)
             keep = ~np.isnan(vals[self.prog.fields.index("privacy_id_count")])

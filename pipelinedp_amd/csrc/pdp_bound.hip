@@ -192,18 +192,12 @@ constexpr int kSieveL2Groups = 4;
 constexpr double kL2Target = 7000.0;
 size_t sieve_stage_bytes(int key_format, int threads);  // LDS of the sieve's level-1 stage (after StageLds)
 // the side band (Plan.band): rows with t <= pair hash < t2 = 2t leave level 1
-// in one list per (tile, wave): the row's 32-bit privacy id, through a
-// per-wave LDS queue written out 64 entries (256 bytes) at a time, in the
-// order the wave met the rows, plus a bitmap of the wave's rows of the tile
-// (bit = the wave's ballot of band rows, word = chunk x item) whose k-th set
-// bit is entry k's row.  4 bytes per band row + 1 bit per row instead of an
-// 8-byte (id, row) pair (C3: 0.75 instead of 1.23 GB written by level 1 and
-// read by k_band_scan); the scan decodes a row only for an entry whose id
-// passes its filter.  The fix-up reads those lists instead of the whole
-// privacy-id column, and only a privacy id with fewer than l0 distinct pairs
-// below t2 still needs the rescan
+// as (privacy id << 32 | row) in a per-tile list, through a per-wave LDS queue
+// written out 64 entries at a time; the fix-up reads that list instead of the
+// whole privacy-id column, and only a privacy id with fewer than l0 distinct
+// pairs below t2 still needs the rescan
 constexpr int kBandQueue = 128;
-inline int64_t sieve_band_lds(int threads) { return (threads / 64) * kBandQueue * 4; }
+inline int64_t sieve_band_lds(int threads) { return (threads / 64) * kBandQueue * 8; }
 // LDS of a sieve workgroup: stage, bucket counts (u32, or u16 pairs), band queues
 inline int64_t sieve_lds(int key_format, int threads, int64_t n_buckets, bool u16, bool band) {
   return ((int64_t)sieve_stage_bytes(key_format, threads) + 7) / 8 * 8 + l1_hist_bytes(n_buckets, u16) +
@@ -469,7 +463,7 @@ struct Ws {
   // side band: per-tile (pid << 32 | row) lists and their lengths; the ids
   // still unresolved after the band fix-up (bitmap, list, {count, rows}) and
   // their rescan's per-bucket counts / cursors
-  uint64_t band, band_cnt, band_bits, unres2_bits, unres2_list, sctl2, fix_cnt2, fix_cur2;
+  uint64_t band, band_cnt, unres2_bits, unres2_list, sctl2, fix_cnt2, fix_cur2;
   uint64_t fix_blist;  // fix-up bucket launches: {count, buckets holding fix-up rows...}
   uint64_t tile_over;  // tile-local level 1: per tile, the bucket holding all 65,536 of its rows (else ~0)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
@@ -547,9 +541,8 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.fix_cur = off; off = align256(off + (uint64_t)p.n_buckets * 4);
       w.fix_blist = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
       if (p.band) {  // the band lists; the second fix-up's unresolved ids and counts
-        w.band = off; off = align256(off + (uint64_t)p.n_tiles * kBandTileStride * 4);
-        w.band_cnt = off; off = align256(off + (uint64_t)p.n_tiles * (kL1Threads / 64) * 4);
-        w.band_bits = off; off = align256(off + (uint64_t)p.n_tiles * kBandTileStride / 8);
+        w.band = off; off = align256(off + (uint64_t)p.n_tiles * kBandTileStride * 8);
+        w.band_cnt = off; off = align256(off + (uint64_t)p.n_tiles * 4);
         w.unres2_bits = off; off = align256(off + ids / 8);
         w.unres2_list = off; off = align256(off + ids * 4);
         w.sctl2 = off; off = align256(off + 16);
@@ -662,7 +655,6 @@ struct KP {  // kernel parameters
   int slot_bits;        // level-1 blocks per tile = 2^slot_bits (Plan.slot_bits)
   int64_t fix_cap;      // sieve: entries the fix-up row list (fix_rec, Ws.fix_rec) holds
   int row_shift;        // PACKED64 level-2 records: the row's first bit (pk_bits + bucket_bits)
-  int band_waves;       // side band: waves of the level-1 workgroup = band lists per tile
 };
 
 KP make_kp(const pdp_bound_config* c, const Plan& p) {
@@ -692,7 +684,6 @@ KP make_kp(const pdp_bound_config* c, const Plan& p) {
   k.slot_bits = p.slot_bits;
   k.fix_cap = 0;  // set from the layout (Ws.fix_cap) where the fix-up runs
   k.row_shift = p.pk_bits + p.bucket_bits;
-  k.band_waves = p.sieve_threads / 64;
   k.pk_mask = (1ULL << p.pk_bits) - 1;
   k.seed = c->seed;
   k.row_seed = derive_row_seed(c->seed);
@@ -1655,14 +1646,10 @@ __device__ __forceinline__ void wave_lds_fence() {
 #ifdef PDP_PHASE_CLOCK
 __device__ unsigned g_phase_l1, g_phase_l2, g_phase_bk;  // profiling builds: prints so far per kernel
 #endif
-// BAND: rows with sieve_t32 <= pair hash < band_t32 also go to the band
-// list of (this tile, this wave): band[t * 65,536 + wave * RW ...] (RW =
-// 65,536 / waves: the wave's rows of the tile) holds their privacy ids in the
-// order the wave met them, through a per-wave LDS queue flushed 64 entries
-// (256 contiguous bytes) at a time; band_cnt[t * waves + wave] = the list's
-// length; band_bits[(t * waves + wave) * RW / 64 + c * Q + q] = the wave's
-// ballot of band rows for item q of chunk c (bit = lane), so entry k's row
-// is the k-th set bit's (band_row_of)
+// BAND: rows with sieve_t32 <= pair hash < band_t32 also go, as (privacy id
+// << 32 | row), to this tile's band list band[t * 65,536 ...], through a
+// per-wave LDS queue flushed 64 entries (512 contiguous bytes) at a time;
+// band_cnt[t] = the list's length
 template <int FMT, bool U16, bool BAND, int TH>
 __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp, const int64_t* __restrict__ pid,
                                                          const int64_t* __restrict__ pk,
@@ -1672,9 +1659,8 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
                                                          uint16_t* __restrict__ soff, unsigned* __restrict__ sbase,
                                                          L1Key<FMT>* __restrict__ keys1,
                                                          unsigned* __restrict__ rows1, unsigned* err,
-                                                         unsigned* __restrict__ band,
+                                                         unsigned long long* __restrict__ band,
                                                          unsigned* __restrict__ band_cnt,
-                                                         unsigned long long* __restrict__ band_bits,
                                                          unsigned* __restrict__ tile_over) {
   using K = L1Key<FMT>;
   using SS = SieveShape<TH>;
@@ -1687,13 +1673,16 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
   SL& s = *reinterpret_cast<SL*>(stage_raw);
   unsigned* bh = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8);
   // BAND: the per-wave queues after the bucket counts (l1_hist_bytes)
-  unsigned* const bq = reinterpret_cast<unsigned*>(stage_raw + (sizeof(SL) + 7) / 8 +
-                                                   (((U16 ? 2 : 4) * kp.n_buckets + 15) / 16 * 16) / 8);
-  __shared__ unsigned fill;
+  unsigned long long* const bq =
+      stage_raw + (sizeof(SL) + 7) / 8 + (((U16 ? 2 : 4) * kp.n_buckets + 15) / 16 * 16) / 8;
+  __shared__ unsigned fill, bfill;
   const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
   for (int64_t b = threadIdx.x; b < n_words; b += TH) bh[b] = 0;
   for (int B = threadIdx.x; B < (int)kp.n_supers; B += TH) s.hist[B] = 0;
-  if (threadIdx.x == 0) fill = 0;
+  if (threadIdx.x == 0) {
+    fill = 0;
+    bfill = 0;
+  }
   __syncthreads();
   // persistent: workgroup g takes tiles g, g + G, ... (G = gridDim.x, about
   // one per CU), so a tile's last chunks prefetch the next tile's first ones
@@ -1709,19 +1698,8 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
   const unsigned long long below = (1ULL << lane) - 1;
   K* blk = nullptr;
   unsigned* rblk = nullptr;
-  // the band: this wave's list and bitmap in the current tile
-  constexpr int kBandWaves = TH / 64;
-  constexpr int64_t kBandRows = kTileRows / kBandWaves;  // the wave's rows of a tile: its list's capacity
-  constexpr int kBandWords = (int)(kBandRows / 64);      // its bitmap words: one per (chunk, item)
-  constexpr int kBandWordsLane = kBandWords / 64;        // ... held by each lane (word lane + 64 k)
-  static_assert(kBandWords == (kTileRows / kSieveChunk) * Q && kBandWords % 64 == 0, "band bitmap words");
-  const int wave = threadIdx.x >> 6;
-  unsigned* band_w = nullptr;
-  unsigned long long bw[kBandWordsLane];
-#pragma unroll
-  for (int k = 0; k < kBandWordsLane; ++k) bw[k] = 0;
-  unsigned wn = 0;       // wave-uniform: entries of the wave's list written out in this tile
-  unsigned* const wq = bq + wave * kBandQueue;
+  unsigned long long* band_tile = nullptr;
+  unsigned long long* const wq = bq + (threadIdx.x >> 6) * kBandQueue;
   int qn = 0;            // wave-uniform: entries waiting in this wave's band queue
   unsigned written = 0;  // block-uniform: this tile's records already written
   int slot = 0;
@@ -1732,7 +1710,7 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     t1 = t0 + kTileRows < kp.n ? t0 + kTileRows : kp.n;
     blk = keys1 + tt * kSieveTileStride;
     rblk = ROWS ? rows1 + tt * kSieveTileStride : nullptr;
-    band_w = BAND ? band + tt * kBandTileStride + wave * kBandRows : nullptr;
+    band_tile = BAND ? band + tt * kBandTileStride : nullptr;
     written = 0;
     slot = 0;
     split = U16 && t1 - t0 > kTileRows / 2 - kSieveChunk;
@@ -1795,20 +1773,20 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
   // end of a tile: the band queues' rest and the list length, the unused
   // flush slots, the bucket counts; leaves the LDS state zeroed for the next
   auto end_tile = [&]() {
-    if constexpr (BAND) {  // the wave's queue rest, its list length and bitmap (one 512 B store per word row)
+    if constexpr (BAND) {
       wave_lds_fence();
-      if (lane < qn) band_w[wn + lane] = wq[lane];
-      wn += (unsigned)qn;
-      qn = 0;
-      const int64_t unit = t * kBandWaves + wave;
-      if (lane == 0) band_cnt[unit] = wn;
-      wn = 0;
-#pragma unroll
-      for (int k = 0; k < kBandWordsLane; ++k) {
-        band_bits[unit * kBandWords + lane + 64 * k] = bw[k];
-        bw[k] = 0;
+      if (qn > 0) {
+        unsigned bb = 0;
+        if (lane == 0) bb = atomicAdd(&bfill, (unsigned)qn);
+        bb = __shfl(bb, 0, 64);
+        if (lane < qn) band_tile[bb + lane] = wq[lane];
+        qn = 0;
       }
-      wave_lds_fence();
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        band_cnt[t] = bfill;
+        bfill = 0;
+      }
     }
 #ifdef PDP_PHASE_CLOCK
     if (threadIdx.x == 0 && blockIdx.x % 97 == 5 && atomicAdd(&g_phase_l1, 1u) < 40u)
@@ -1945,22 +1923,22 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
         }
         base += (unsigned)__popcll(m[q]);
       }
-      if constexpr (BAND) {  // band rows' ids -> the wave's queue (64 out at once); ballots -> bitmap words
-        const int chunk = (int)((c0 - t0) / kSieveChunk);  // block-uniform
+      if constexpr (BAND) {  // band rows -> the wave's queue; 64 of them out at once
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           const unsigned long long mb = __ballot(bnd[q]);
-          const int j = chunk * Q + q;  // the wave's bitmap word (wave-uniform)
-#pragma unroll
-          for (int k = 0; k < kBandWordsLane; ++k) bw[k] = (j == lane + 64 * k) ? mb : bw[k];
           if (mb == 0) continue;  // wave-uniform
-          if (bnd[q]) wq[qn + __popcll(mb & below)] = (uint32_t)x[q];  // a band row's key slot holds its id
+          const int64_t i = c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1);
+          if (bnd[q]) wq[qn + __popcll(mb & below)] = ((unsigned long long)(uint32_t)x[q] << 32) | (uint32_t)i;
           qn += __popcll(mb);
           if (qn >= 64) {
             wave_lds_fence();
-            band_w[wn + lane] = wq[lane];
-            wn += 64u;
-            const unsigned rest = lane + 64 < qn ? wq[lane + 64] : 0u;
+            const unsigned long long e = wq[lane];
+            unsigned bb = 0;
+            if (lane == 0) bb = atomicAdd(&bfill, 64u);
+            bb = __shfl(bb, 0, 64);
+            band_tile[bb + lane] = e;
+            const unsigned long long rest = lane + 64 < qn ? wq[lane + 64] : 0ULL;
             wave_lds_fence();
             if (lane + 64 < qn) wq[lane] = rest;
             qn -= 64;
@@ -2864,47 +2842,20 @@ __global__ void __launch_bounds__(kRescanThreads) k_sieve_rescan(KP kp, const in
   }
 }
 
-// Fix-up step 1, side band: the (tile, level-1 wave) band lists (privacy
-// ids, written by k_sieve_l1<BAND>) instead of the whole privacy-id column,
-// with the same Bloom filter, per-wave queues and output (fix_rec as (id <<
-// 32 | row), sctl[1]) as k_sieve_rescan; the unresolved ids' candidate rows
-// are already on fix_rec (the main bucket launch put them there).  Each wave
-// takes a contiguous span of whole lists (the next list's first entries loaded
-// while this one's are tested);
-// an entry whose id passes the filter gets its row from the list's bitmap
-// (band_row_of: the wave loads the bitmap and its prefix counts into LDS the
-// first time one of its lists has such an entry).  Every lane of a wave runs
-// the same trips (a list is wave-uniform), so the queues stay wave-uniform.
-constexpr int kBandMaxWords = kTileRows / kSieveThreads2;  // bitmap words of one list, at most (128)
-__device__ __forceinline__ uint32_t band_row_of(const KP& kp, int64_t t, int v, unsigned k,
-                                                const unsigned long long* words, const unsigned* pre,
-                                                int n_words) {
-  int lo = 0, hi = n_words - 1;  // the last word with pre <= k (it holds entry k's bit)
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (pre[mid] <= k) lo = mid;
-    else hi = mid - 1;
-  }
-  unsigned long long m = words[lo];
-  for (unsigned r = k - pre[lo]; r; --r) m &= m - 1;  // drop the word's first k - pre bits
-  const int b = __ffsll((long long)m) - 1;            // the level-1 lane
-  const int th = kp.band_waves * 64;                  // the level-1 workgroup
-  const int chunk = lo / kSieveChunkItems, q = lo % kSieveChunkItems;
-  return (uint32_t)(t * kTileRows + (int64_t)chunk * th * kSieveChunkItems +
-                    2 * (v * 64 + b + (q / 2) * th) + (q & 1));
-}
-
-__global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsigned* __restrict__ band,
+// Fix-up step 1, side band: the tiles' band lists (privacy id << 32 | row,
+// written by k_sieve_l1<BAND>) instead of the whole privacy-id column, with
+// the same Bloom filter, per-wave queues and output (fix_rec, sctl[1]) as
+// k_sieve_rescan; the unresolved ids' candidate rows are already on fix_rec
+// (the main bucket launch put them there).  Every lane of a wave runs the
+// same trips (band_cnt[t] is block-uniform), so the queues stay wave-uniform.
+__global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsigned long long* __restrict__ band,
                                                               const unsigned* __restrict__ band_cnt,
-                                                              const unsigned long long* __restrict__ band_bits,
                                                               const unsigned* __restrict__ unres_bits,
                                                               const unsigned* __restrict__ unres_list,
                                                               unsigned* __restrict__ sctl,
                                                               unsigned long long* __restrict__ fix_rec) {
   __shared__ unsigned bloom[kBloomWords];
   __shared__ unsigned long long queue[kRescanThreads / 64][kRescanQueue];
-  __shared__ unsigned long long words[kRescanThreads / 64][kBandMaxWords];
-  __shared__ unsigned pre[kRescanThreads / 64][kBandMaxWords];
   const unsigned n_unres = sctl[0];
   if (n_unres == 0) return;  // grid-uniform
   const bool use_bloom = n_unres <= kBloomMaxIds;  // grid-uniform
@@ -2915,11 +2866,9 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
     atomicOr(bloom + bloom_word(h), bloom_bits(h));
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ULL << lane) - 1;
-  unsigned long long* const wq = queue[wv];
-  unsigned long long* const ww = words[wv];
-  unsigned* const wp = pre[wv];
+  unsigned long long* const wq = queue[threadIdx.x >> 6];
   int qn = 0;
   auto enqueue = [&](bool pos, unsigned long long e) {
     const unsigned long long m = __ballot(pos);
@@ -2940,100 +2889,29 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
       wave_lds_fence();
     }
   };
-  const int nw = kp.band_waves;                        // lists per tile
-  const int64_t rows_w = kTileRows / nw;               // a list's capacity
-  const int n_words = (int)(rows_w / 64);              // its bitmap words
-  const int64_t n_units = kp.n_tiles * nw;
-  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x / 64) + wv;
-  // each wave takes a contiguous span of lists; a trip is 1,024 entries (four
-  // 16-byte loads per lane), and the next list's first trip is loaded before
-  // this one's is tested, so a wave always has a trip of loads in flight (C3:
-  // ~630 entries per list, one trip)
-  constexpr int KV = 4;
-  constexpr unsigned kTrip = 64 * 4 * KV;
-  static_assert(kTileRows / 16 % kTrip == 0, "a list's capacity is whole trips");
-  const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x / 64);
-  const int64_t per = (n_units + n_waves - 1) / n_waves;
-  const int64_t u_begin = gw * per < n_units ? gw * per : n_units;
-  const int64_t u_end = u_begin + per < n_units ? u_begin + per : n_units;
-  auto load_trip = [&](int64_t u, unsigned j0, uint4 (&x)[KV]) {  // in the list's region: no guard
-    const uint4* p = reinterpret_cast<const uint4*>(band + u * rows_w + j0) + lane;
-#pragma unroll
-    for (int k = 0; k < KV; ++k) x[k] = ld_maybe_nt<PDP_NT_BS>(p + 64 * k);
-  };
+  // entries per lane and trip, loaded together (8: at an N = 8 rank's share a
+  // block sees ~2 tiles, so its trips are latency rounds, not a stream)
+  constexpr int KU = 8;
+  const int64_t w0 = (int64_t)(threadIdx.x >> 6) * 64 * KU;
   auto run = [&](auto bloom_tag) {
     constexpr bool BLOOM = decltype(bloom_tag)::value;
-    bool decoded = false;  // wave-uniform: the current list's bitmap is in LDS
-    // entries j0 + 256 k + 4 lane + c of list u: test, decode the hits' rows, queue them
-    auto scan = [&](int64_t u, unsigned cnt, unsigned j0, const uint4 (&x)[KV]) {
-      bool hit[KV][4];
-      bool any = false;
+    for (int64_t t = blockIdx.x; t < kp.n_tiles; t += gridDim.x) {
+      const unsigned long long* __restrict__ bt = band + t * kBandTileStride;
+      unsigned cnt = band_cnt[t];
+      cnt = cnt <= (unsigned)kTileRows ? cnt : (unsigned)kTileRows;
+      for (int64_t j0 = w0; j0 < cnt; j0 += (int64_t)blockDim.x * KU) {  // wave-uniform trips
+        unsigned long long e[KU];
 #pragma unroll
-      for (int k = 0; k < KV; ++k) {
-        const unsigned e4[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
+        for (int v = 0; v < KU; ++v) {
+          const int64_t j = j0 + v * 64 + lane;
+          e[v] = j < cnt ? ld_maybe_nt<PDP_NT_BS>(bt + j) : ~0ULL;
+        }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const unsigned j = j0 + 256u * k + 4u * lane + c;
-          hit[k][c] = j < cnt && rescan_maybe<BLOOM>(kp, (int64_t)e4[c], bloom, unres_bits);
-          any |= hit[k][c];
+        for (int v = 0; v < KU; ++v) {
+          const int64_t u = e[v] == ~0ULL ? -1 : (int64_t)(e[v] >> 32);
+          enqueue(u >= 0 && rescan_maybe<BLOOM>(kp, u, bloom, unres_bits), e[v]);
         }
       }
-      if (__ballot(any) == 0) return;  // wave-uniform: usually no entry of the trip passes
-      if (!decoded) {  // the list's bitmap and its exclusive prefix counts
-        unsigned carry = 0;
-        for (int w0 = 0; w0 < n_words; w0 += 64) {
-          const unsigned long long b = band_bits[u * n_words + w0 + lane];
-          const unsigned c = (unsigned)__popcll(b);
-          unsigned incl = c;
-          for (int off = 1; off < 64; off <<= 1) {
-            const unsigned up = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += up;
-          }
-          ww[w0 + lane] = b;
-          wp[w0 + lane] = carry + incl - c;
-          carry += __shfl(incl, 63, 64);
-        }
-        wave_lds_fence();
-        decoded = true;
-      }
-      const int64_t t = u / nw;
-      const int v = (int)(u % nw);
-#pragma unroll
-      for (int k = 0; k < KV; ++k) {
-        const unsigned e4[4] = {x[k].x, x[k].y, x[k].z, x[k].w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          unsigned long long rec = 0;
-          if (hit[k][c])
-            rec = ((unsigned long long)e4[c] << 32) |
-                  band_row_of(kp, t, v, j0 + 256u * k + 4u * lane + c, ww, wp, n_words);
-          enqueue(hit[k][c], rec);
-        }
-      }
-    };
-    if (u_begin >= u_end) return;  // wave-uniform
-    unsigned cl = u_begin + lane < u_end ? band_cnt[u_begin + lane] : 0u;  // 64 lists' lengths at a time
-    uint4 cur[KV], nxt[KV];
-    load_trip(u_begin, 0, cur);
-    unsigned cnt = __shfl(cl, 0, 64);
-    for (int64_t u = u_begin; u < u_end; ++u) {  // wave-uniform trips
-      const int64_t i = u - u_begin;
-      cnt = cnt <= (unsigned)rows_w ? cnt : (unsigned)rows_w;
-      const bool more = u + 1 < u_end;
-      if (more && ((i + 1) & 63) == 0) cl = u + 1 + lane < u_end ? band_cnt[u + 1 + lane] : 0u;
-      const unsigned cnt_n = more ? __shfl(cl, (int)((i + 1) & 63), 64) : 0u;
-      load_trip(more ? u + 1 : u, 0, nxt);
-      decoded = false;
-      scan(u, cnt, 0, cur);
-      for (unsigned j0 = kTrip; j0 < cnt; j0 += kTrip) {  // long lists (rare at C3)
-        uint4 x[KV];
-        load_trip(u, j0, x);
-        scan(u, cnt, j0, x);
-      }
-      if (decoded) wave_lds_fence();  // the next list's bitmap may overwrite this one's
-#pragma unroll
-      for (int k = 0; k < KV; ++k) cur[k] = nxt[k];
-      cnt = cnt_n;
     }
   };
   if (use_bloom) run(std::true_type{});
@@ -4013,8 +3891,7 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   // that marks the ids still unresolved -> their rescan -> a third launch
   PDP_PROF_BEGIN("k_band_scan", st);
   hipLaunchKernelGGL(k_band_scan, dim3(kRescanBlocks), dim3(kRescanThreads), 0, st, kp,
-                       (const unsigned*)(ws + w.band), (const unsigned*)(ws + w.band_cnt),
-                       (const unsigned long long*)(ws + w.band_bits),
+                       (const unsigned long long*)(ws + w.band), (const unsigned*)(ws + w.band_cnt),
                        (const unsigned*)m1.bits, (const unsigned*)m1.list, sctl, fix_rec);
   PDP_PROF_END(st);
   PDP_HIP_CHECK(hipGetLastError());
@@ -4153,6 +4030,34 @@ int64_t device_cus() {
   return cached[dev];
 }
 
+// The small control regions a bounding call starts from (error word, the
+// tiles' overflow marks, the fix-ups' counters and cursors), set by ONE
+// launch instead of a memset each (C3: eight fills of 16 B - 20 KB, ~4 us
+// apiece on the stream)
+constexpr int kMaxFills = 10;
+struct Fills {
+  unsigned* p[kMaxFills];
+  int64_t n[kMaxFills];  // u32 words
+  unsigned v[kMaxFills];
+  int k;
+};
+__global__ void __launch_bounds__(kBlock) k_fill(Fills f) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int j = 0; j < f.k; ++j)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < f.n[j]; i += stride) f.p[j][i] = f.v[j];
+}
+
+int launch_fills(const Fills& f, hipStream_t st) {
+  int64_t most = 0;
+  for (int j = 0; j < f.k; ++j) most = std::max(most, f.n[j]);
+  if (most == 0) return PDP_OK;
+  PDP_PROF_BEGIN("k_fill", st);
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)std::min<int64_t>((most + kBlock - 1) / kBlock, 256)), dim3(kBlock), 0, st, f);
+  PDP_PROF_END(st);
+  PDP_HIP_CHECK(hipGetLastError());
+  return PDP_OK;
+}
+
 // tile-local level 1 -> level-2 cursors and bucket starts -> tile-local level 2
 template <int FMT>
 int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid, const int64_t* pk,
@@ -4165,8 +4070,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
   unsigned* counts_tm2 = u16 ? (unsigned*)(ws + w.counts_tm2) : nullptr;
   unsigned* counts = (unsigned*)(ws + w.counts);
   uint16_t* soff = (uint16_t*)(ws + w.soff);
-  unsigned* tile_over = (unsigned*)(ws + w.tile_over);  // all ones unless a tile's rows are all one bucket's
-  PDP_HIP_CHECK(hipMemsetAsync(tile_over, 0xFF, (uint64_t)p.n_tiles * 4, st));
+  unsigned* tile_over = (unsigned*)(ws + w.tile_over);  // all ones (k_fill) unless a tile's rows are all one bucket's
   unsigned* sbase = p.sieve ? (unsigned*)(ws + w.sbase) : nullptr;
   K1* keys1 = (K1*)(ws + w.keys1);
   unsigned* rows1 = ROWS1 ? (unsigned*)(ws + w.rows1) : nullptr;
@@ -4182,12 +4086,11 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
       const void* l1 = th == kSieveThreads2 ? pick(std::integral_constant<int, kSieveThreads2>{})
                                             : pick(std::integral_constant<int, kL1Threads>{});
       PDP_HIP_CHECK(hipFuncSetAttribute(l1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
-      unsigned* band = p.band ? (unsigned*)(ws + w.band) : nullptr;
+      unsigned long long* band = p.band ? (unsigned long long*)(ws + w.band) : nullptr;
       unsigned* band_cnt = p.band ? (unsigned*)(ws + w.band_cnt) : nullptr;
-      unsigned long long* band_bits = p.band ? (unsigned long long*)(ws + w.band_bits) : nullptr;
       void* args1[] = {(void*)&kp,   (void*)&pid,   (void*)&pk,    (void*)&allowed, (void*)&counts_tm,
                        (void*)&counts_tm2, (void*)&soff, (void*)&sbase, (void*)&keys1, (void*)&rows1, (void*)&err,
-                       (void*)&band, (void*)&band_cnt, (void*)&band_bits, (void*)&tile_over};
+                       (void*)&band, (void*)&band_cnt, (void*)&tile_over};
       PDP_PROF_BEGIN("k_sieve_l1", st);
       // persistent: as many workgroups as fit at once (one per CU at 1,024
       // threads, two at 512), each looping over its tiles
@@ -4488,7 +4391,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     if (v > 0 && v < kp.fix_cap) kp.fix_cap = v;
   }
   unsigned* err = (unsigned*)(ws + w.err);
-  PDP_HIP_CHECK(hipMemsetAsync(err, 0, 16, st));
+  if (p.algorithm != PDP_ALGO_BUCKETED || cfg->n_rows == 0) PDP_HIP_CHECK(hipMemsetAsync(err, 0, 16, st));
   if (p.algorithm == PDP_ALGO_GLOBAL_SKETCH) {
     const uint64_t slots = (uint64_t)cfg->n_privacy_ids * (uint64_t)cfg->l0;
     PDP_HIP_CHECK(hipMemsetAsync(ws + w.sketch, 0xFF, slots * 8, st));
@@ -4509,6 +4412,29 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
   if (cfg->n_rows == 0) {
     PDP_HIP_CHECK(hipMemsetAsync(counts, 0, (p.n_buckets + 1) * 4, st));
     return PDP_OK;
+  }
+  {  // the control regions: one k_fill launch
+    Fills f{};
+    auto add = [&](uint64_t off, int64_t words, unsigned v) {
+      f.p[f.k] = (unsigned*)(ws + off);
+      f.n[f.k] = words;
+      f.v[f.k] = v;
+      ++f.k;
+    };
+    add(w.err, 4, 0u);
+    if (p.l1_local) add(w.tile_over, p.n_tiles, ~0u);
+    if (p.merge == PDP_MERGE_RANGES && p.sieve) {
+      add(w.sctl, 4, 0u);
+      add(w.fix_cnt, p.n_buckets + 1, 0u);
+      add(w.fix_cur, p.n_buckets, 0u);
+    }
+    if (p.merge == PDP_MERGE_RANGES && p.band) {
+      add(w.sctl2, 4, 0u);
+      add(w.fix_cnt2, p.n_buckets + 1, 0u);
+      add(w.fix_cur2, p.n_buckets, 0u);
+    }
+    const int rcf = launch_fills(f, st);
+    if (rcf != PDP_OK) return rcf;
   }
   int rc2 = PDP_OK;
   if (p.l1_local) {
@@ -4536,16 +4462,6 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     rc2 = launch_debug_corrupt(kp, p, st, ws, w);
     if (rc2 != PDP_OK) return rc2;
   }
-  if (p.sieve) {
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.sctl, 0, 16, st));
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cnt, 0, ((uint64_t)p.n_buckets + 1) * 4, st));
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cur, 0, (uint64_t)p.n_buckets * 4, st));
-  }
-  if (p.band) {
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.sctl2, 0, 16, st));
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cnt2, 0, ((uint64_t)p.n_buckets + 1) * 4, st));
-    PDP_HIP_CHECK(hipMemsetAsync(ws + w.fix_cur2, 0, (uint64_t)p.n_buckets * 4, st));
-  }
   const pdp_partition_accumulators none{};
   return dispatch<Buckets>(cfg->value_kind, cfg->linf == 0, kp, p, st, privacy_id, partition_key, pk_allowed, value,
                            none, ws, w);
@@ -4570,8 +4486,8 @@ int pdp_bound_stats_read(const pdp_bound_config* cfg, const void* workspace, uin
   std::vector<unsigned> bc;
   if (bucketed && p.band) {
     PDP_HIP_CHECK(hipMemcpyAsync(ctl2, ws + w.sctl2, 8, hipMemcpyDeviceToHost, st));
-    bc.resize((size_t)p.n_tiles * (p.sieve_threads / 64));  // one list per (tile, level-1 wave)
-    PDP_HIP_CHECK(hipMemcpyAsync(bc.data(), ws + w.band_cnt, bc.size() * 4, hipMemcpyDeviceToHost, st));
+    bc.resize((size_t)p.n_tiles);
+    PDP_HIP_CHECK(hipMemcpyAsync(bc.data(), ws + w.band_cnt, (size_t)p.n_tiles * 4, hipMemcpyDeviceToHost, st));
   }
   PDP_HIP_CHECK(hipStreamSynchronize(st));
   out->rows_partitioned = rows;

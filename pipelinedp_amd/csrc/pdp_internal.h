@@ -208,13 +208,27 @@ __device__ __forceinline__ double round_to_multiple(double x, double base) {
 __device__ __forceinline__ int64_t secure_geometric(double lambda, uint64_t seed, int64_t gidx, uint32_t slot,
                                                     uint32_t& k) {
   int64_t lo = 0, hi = INT64_MAX;
-  U4 blk{0, 0, 0, 0};
-  int half = 0;  // 0: next uniform from a fresh block's (x, y); 1: from (z, w)
+  // The far tail, without an expm1: while lambda (mid - lo) >= 40 both
+  // expm1 terms round to exactly -1 (e^-40 < 2^-54), so q == 1 and the step
+  // only halves hi -- the (lo, hi) sequence of the loop below, bit for bit
+  // (C3's Laplace draws skip ~20 of their ~60 steps here)
   while (lo + 1 < hi) {
     const int64_t mid = lo + ((hi - lo) >> 1);
-    const double q = expm1(lambda * (double)(lo - mid)) / expm1(lambda * (double)(lo - hi));
+    if (!(lambda * (double)(lo - mid) <= -40.0)) break;
+    hi = mid;
+  }
+  U4 blk{0, 0, 0, 0};
+  int half = 0;  // 0: next uniform from a fresh block's (x, y); 1: from (z, w)
+  // den = expm1(lambda (lo - hi)) of the current (lo, hi): after hi = mid it
+  // is the step's numerator (same expression), so only lo = mid recomputes it
+  double den = expm1(lambda * (double)(lo - hi));
+  while (lo + 1 < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    const double num = expm1(lambda * (double)(lo - mid));
+    const double q = num / den;
     if (q >= 1.0) {
       hi = mid;
+      den = num;
       continue;
     }
     double u;
@@ -225,8 +239,13 @@ __device__ __forceinline__ int64_t secure_geometric(double lambda, uint64_t seed
       u = u01(blk.z, blk.w);
     }
     half ^= 1;
-    if (u <= q) hi = mid;
-    else lo = mid;
+    if (u <= q) {
+      hi = mid;
+      den = num;
+    } else {
+      lo = mid;
+      den = lo + 1 < hi ? expm1(lambda * (double)(lo - hi)) : den;
+    }
   }
   return hi - 1;
 }

@@ -188,6 +188,19 @@ def new_accumulators(n_partitions: int, bounding: BoundingSpec, device) -> Dict[
     return acc
 
 
+def zero_accumulators(acc):
+    """Zeroes accumulators from new_accumulators in one fill (their fields
+    are views of one block); any other dict field by field."""
+    fields = [t for t in acc.values() if t is not None]
+    bases = {id(t._base): t._base for t in fields if t._base is not None}
+    if len(bases) == 1 and all(t._base is not None for t in fields):
+        next(iter(bases.values())).zero_()
+    else:
+        for t in fields:
+            t.zero_()
+    return acc
+
+
 def _acc_struct(acc) -> N.PartitionAccumulators:
     s = N.PartitionAccumulators()
     s.privacy_id_count = _ptr(acc["privacy_id_count"])
@@ -493,7 +506,7 @@ def _device_table(values, device):
     if t is None:
         if len(_tables) > 64:
             _tables.clear()
-        t = _tables[key] = torch.as_tensor(arr).to(device)
+        t = _tables[key] = torch.from_numpy(arr.copy()).to(device)  # (the cached table is read-only)
     return t
 
 
@@ -541,7 +554,7 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
     N.check(lib.pdp_compact_workspace_bytes(P, ctypes.byref(cbytes)), "pdp_compact_workspace_bytes")
     cws = torch.empty(int(cbytes.value), dtype=torch.uint8, device=device)
     index = torch.empty(max(P, 1), dtype=torch.int64, device=device)
-    n_kept_dev = torch.zeros(1, dtype=torch.int64, device=device)
+    n_kept_dev = torch.empty(1, dtype=torch.int64, device=device)  # pdp_compact writes it
     N.check(lib.pdp_compact(_ptr(keep), P, _ptr(index), _ptr(n_kept_dev), _ptr(cws), cws.numel(), st),
             "pdp_compact")
     out = torch.empty((max(n_cols, 1), max(P, 1)), dtype=torch.float64, device=device)
@@ -559,6 +572,26 @@ def select_and_noise(acc, *, selection: SelectionSpec, ops: List[MetricOpSpec], 
         n_kept = int(n_kept_dev.item())
         return index[:n_kept], out, n_kept
     return index, out, n_kept_dev
+
+
+def kept_to_host(index, out, n_kept: int, keys_only: bool = False):
+    """(index[:n_kept], out[:, :n_kept]) as host NumPy arrays through ONE
+    packed device copy and ONE device-to-host copy into pinned memory (the
+    public API's result; two pageable copies of a strided view cost two more
+    synchronisations)."""
+    torch = _torch()
+    n_cols = 0 if keys_only else int(out.shape[0])
+    if n_kept == 0:
+        return np.zeros(0, dtype=np.int64), np.zeros((n_cols, 0))
+    rows = [index[:n_kept].view(torch.float64).unsqueeze(0)]
+    if n_cols:
+        rows.append(out[:, :n_kept])
+    packed = torch.cat(rows) if len(rows) > 1 else rows[0]
+    host = torch.empty(packed.shape, dtype=torch.float64, pin_memory=True)
+    host.copy_(packed, non_blocking=True)
+    torch.cuda.current_stream(index.device).synchronize()
+    h = host.numpy()
+    return h[0].view(np.int64).copy(), h[1:].copy()
 
 
 def add_noise(values, *, noise: NoiseParams, seed: int, index_offset: int = 0, out=None, stream=None):
