@@ -13,6 +13,7 @@ Stage order (reference dp_engine.py:109-187):
 """
 import ctypes
 import dataclasses
+import weakref
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -325,40 +326,92 @@ class BoundWorkspace:
 # contents changed in place is re-measured.
 RESCAN_BLOOM_MAX = 8192  # pdp_bound.hip kBloomMaxIds: above it the re-read tests a bitmap per row
 FEEDBACK_REPROBE = 64
-_feedback = {}
+# Entries live as long as the key columns: a weak map from the partition-key
+# tensor object to its entries (keyed by the privacy-id tensor's identity, the
+# columns' in-place version counters and the bounding parameters), so a table
+# allocated at a freed table's address starts fresh and an in-place write to
+# the columns through torch re-measures.  The counters sit in slots of one
+# pinned block the process never frees: a dropped entry whose copy is still
+# in flight returns its slot only once the copy's event has completed
+# (a freed pinned block could be handed out again under a
+# pending device-to-host copy).
+_feedback = weakref.WeakKeyDictionary()
+_FB_SLOTS = 1024
+_fb_pool = None          # pinned int32 [_FB_SLOTS, 4]
+_fb_free = []            # free slot indices
+_fb_draining = []        # (slot, event): slots of dropped entries whose copy may be pending
+
+
+def _fb_take_slot():
+    global _fb_pool
+    torch = _torch()
+    if _fb_pool is None:
+        _fb_pool = torch.zeros((_FB_SLOTS, 4), dtype=torch.int32, pin_memory=True)
+        _fb_free.extend(range(_FB_SLOTS))
+    for item in [d for d in _fb_draining if d[1] is None or d[1].query()]:
+        _fb_draining.remove(item)
+        _fb_free.append(item[0])
+    return _fb_free.pop() if _fb_free else None
+
+
+def _fb_release(state):
+    """weakref.finalize callback of a dropped _PlanFeedback (state: [slot, event])."""
+    slot, event = state
+    if slot is not None:
+        _fb_draining.append((slot, event))
 
 
 class _PlanFeedback:
-    def __init__(self):
-        torch = _torch()
-        self.host = torch.zeros(4, dtype=torch.int32, pin_memory=True)  # uint32 counters (read & 0xFFFFFFFF)
-        self.event = None    # recorded after the copies into `host`
+    def __init__(self, slot):
+        self.slot = slot
+        self.host = _fb_pool[slot]  # uint32 counters (read & 0xFFFFFFFF)
+        self.state = [slot, None]   # [slot, event recorded after the copies into `host`]
         self.band = False    # the measured plan had the side band
         self.unsieved = False
         self.calls = 0
+        self.sieved_calls = 0
+        weakref.finalize(self, _fb_release, self.state)
+
+    @property
+    def event(self):
+        return self.state[1]
+
+    @event.setter
+    def event(self, ev):
+        self.state[1] = ev
 
     def idle(self) -> bool:
-        """No copy into `host` is pending (the pinned block may be released)."""
+        """No copy into `host` is pending."""
         return self.event is None or self.event.query()
 
 
-def _evict_feedback():
-    """Drops idle entries; an entry whose pinned counters are still the
-    target of an enqueued copy stays (its block must not be reused before the
-    copy lands)."""
-    for key in [k for k, fb in _feedback.items() if fb.idle()]:
-        del _feedback[key]
+def _feedback_entries(pk, create=False):
+    d = _feedback.get(pk)
+    if d is None and create:
+        d = _feedback[pk] = {}
+    return d
 
 
 def _feedback_key(pid, pk, n, U, P, bounding, row_offset):
-    return (_ptr(pid) or 0, _ptr(pk), n, int(U), int(P), int(bounding.l0), int(bounding.linf),
-            int(bounding.flags), int(row_offset), pk.device.index)
+    return (id(pid), None if pid is None else pid._version, pk._version, n, int(U), int(P), int(bounding.l0),
+            int(bounding.linf), int(bounding.flags), int(row_offset))
 
 
-def _feedback_sieve(key) -> int:
+def _feedback_get(pid, pk, key):
+    d = _feedback_entries(pk)
+    e = None if d is None else d.get(key)
+    if e is None:
+        return None
+    pid_ref, fb = e
+    if (pid_ref() if pid_ref is not None else None) is not pid:  # another privacy-id tensor at that id
+        return None
+    return fb
+
+
+def _feedback_sieve(pid, pk, key) -> int:
     """The sieve argument the auto plan takes for these columns: 0 (auto) or
     -1 (off) after a measured call whose re-read covered many ids."""
-    fb = _feedback.get(key)
+    fb = _feedback_get(pid, pk, key)
     if fb is None:
         return 0
     if fb.event is not None and fb.event.query():
@@ -371,14 +424,15 @@ def _feedback_sieve(key) -> int:
     fb.calls += 1
     if fb.calls % FEEDBACK_REPROBE == 0:
         fb.unsieved = False  # measure the sieved plan again
+        fb.sieved_calls = 0  # (its counters are read: the next sieved call arms the copy)
         return 0
     return -1
 
 
 def plan_feedback_state(pid, pk, *, n_privacy_ids, n_partitions, bounding, row_offset=0):
     """Tests / diagnostics: None, or {"unsieved": bool, "pending": bool}."""
-    fb = _feedback.get(_feedback_key(pid, pk, int(pk.shape[0]), n_privacy_ids, n_partitions, bounding,
-                                     row_offset))
+    fb = _feedback_get(pid, pk, _feedback_key(pid, pk, int(pk.shape[0]), n_privacy_ids, n_partitions, bounding,
+                                              row_offset))
     return None if fb is None else {"unsieved": fb.unsieved, "pending": fb.event is not None}
 
 
@@ -426,7 +480,7 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     feedback = (sieve == 0 and algorithm == N.ALGO_AUTO and n > 0)
     fkey = _feedback_key(pid, pk, n, n_privacy_ids, n_partitions, bounding, row_offset) if feedback else None
     if feedback:
-        sieve = _feedback_sieve(fkey)
+        sieve = _feedback_sieve(pid, pk, fkey)
     cfg = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
                        key_format, sieve, sieve_band, sieve_threads, bucket_threads)
     nbytes = ctypes.c_uint64(0)
@@ -460,12 +514,20 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     if feedback and sieve == 0:
         info = bound_plan_info(cfg)
         if info.sieve:  # a sieved call: its fix-up counters for the next one
-            fb = _feedback.get(fkey)
+            fb = _feedback_get(pid, pk, fkey)
             if fb is None:
-                if len(_feedback) > 256:
-                    _evict_feedback()
-                fb = _feedback[fkey] = _PlanFeedback()
-            if fb.event is None:
+                slot = _fb_take_slot()
+                if slot is not None:
+                    entries = _feedback_entries(pk, create=True)
+                    if len(entries) > 16:  # the same columns under many parameter sets: keep the newest
+                        entries.clear()
+                    fb = _PlanFeedback(slot)
+                    entries[fkey] = (None if pid is None else weakref.ref(pid), fb)
+            if fb is not None:
+                fb.sieved_calls += 1
+            # counters of the first sieved call, then of every FEEDBACK_REPROBE-th
+            # (a copy per call would cost a stream slot each time for no news)
+            if fb is not None and fb.event is None and (fb.sieved_calls - 1) % FEEDBACK_REPROBE == 0:
                 N.check(lib.pdp_bound_stats_async(ctypes.byref(cfg), _ptr(ws), ws.numel(),
                                                   ctypes.c_void_p(fb.host.data_ptr()), st),
                         "pdp_bound_stats_async")
@@ -483,6 +545,9 @@ def _raise_error_flags(flags: int, n_privacy_ids, n_partitions):
     if flags & 2:
         raise N.NativeLibraryError("the sieve's fix-up row list outgrew its workspace region "
                                    "(pdp_bound_error_flags bit 1; a library bug)")
+    if flags & 4:
+        raise N.NativeLibraryError("a cooperative fix-up launch timed out at its grid barrier (pdp_bound_error_flags "
+                                   "bit 2: its workgroups were not all resident); the result is incomplete")
 
 
 def raise_key_errors(workspace: "BoundWorkspace"):

@@ -309,6 +309,15 @@ def test_plan_feedback_runs_light_user_tables_unsieved(device):
     _compare(call(), want, scale)
     assert ws.stats()["sieve"] == 0  # measured slow: unsieved now
     assert X.plan_feedback_state(tp, tk, n_privacy_ids=U, n_partitions=P, bounding=spec)["unsieved"]
+    # the decision belongs to these tensor objects and their contents: a copy
+    # (as a new table allocated at a freed one's address would be) starts
+    # fresh, and an in-place write through torch re-measures
+    tp2, tk2 = tp.clone(), tk.clone()
+    assert X.plan_feedback_state(tp2, tk2, n_privacy_ids=U, n_partitions=P, bounding=spec) is None
+    tk.add_(0)
+    assert X.plan_feedback_state(tp, tk, n_privacy_ids=U, n_partitions=P, bounding=spec) is None
+    _compare(call(), want, scale)  # measured again: sieved, equal to the oracle
+    assert ws.stats()["sieve"] > 0
     # a table of heavy users only keeps the sieved plan
     pid2 = rng.integers(0, U, 100 * U)
     pk2 = rng.integers(0, P, len(pid2))
