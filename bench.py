@@ -69,7 +69,9 @@ PMC_SUMMARY = {w: os.path.join(HERE, "profiles", "r05", f"{w}_pmc.json") for w i
 # profiled launches moved about the same bytes each.
 DATA_DEPENDENT = {
     "k_band_scan": ("unresolved_ids", "band_rows"),
-    "k_fix_prep": ("fixup_rows", "fixup2_rows", "unresolved_ids", "unresolved2_ids"),
+    "k_fix_filter": ("fixup_rows", "fixup2_rows"),
+    "k_fix_scatter": ("fixup_rows", "fixup2_rows"),
+    "k_fix_buckets": ("unresolved_ids", "unresolved2_ids"),
     "k_bucket_fix": ("unresolved_ids", "fixup_rows"),
     "k_sieve_rescan": ("unresolved_ids", "unresolved2_ids", "fixup2_rows"),
     "k_bucket_fix2": ("unresolved2_ids", "fixup2_rows"),
@@ -692,7 +694,7 @@ def kernel_alg_bytes(plan, n, kept_pairs, kept_rows, n_fields, stats, P=0):
             # privacy ids in, (id, row) per fix-up row out; with no unresolved
             # privacy id the rescan exits before reading anything
             out["k_sieve_rescan"] = (8.0 * n + 8.0 * fix) if stats.get("unresolved_ids", 1) else 0.0
-        out["k_fix_prep"] = (8.0 + 8.0 + rec2) * (fix + fix2)  # list in, partition gathered, record out
+        out["k_fix_scatter"] = (8.0 + 8.0 + rec2) * (fix + fix2)  # list in, partition gathered, record out
         out["k_bucket_fix"] = key2 * fix
     out["k_range_reduce"] = 2.0 * pair_rec * kept_pairs
     # two-level merge (P > 2^21): the coarse records' keys counted per fine

@@ -327,10 +327,7 @@ int pdp_add_noise(const void* values, int32_t value_kind, int64_t n, const pdp_n
  * [0, n_privacy_ids) x [0, n_partitions) (the row is skipped, never read out
  * of bounds), bit 1 if the sieve's fix-up row list would outgrow its
  * workspace region (cannot happen: each list holds distinct rows; checked
- * rather than assumed), bit 2 if the fix-up's cooperative launch (one
- * workgroup per CU, grid barriers) waited more than ~1 s at a barrier (its
- * workgroups were not all resident, e.g. on a device shared with other
- * work): it stops instead of hanging, and the result is incomplete.  Reads it from the workspace of pdp_bound_contributions
+ * rather than assumed).  Reads it from the workspace of pdp_bound_contributions
  * (synchronises `stream`). */
 int pdp_bound_error_flags(const void* workspace, uint32_t* flags, void* stream);
 

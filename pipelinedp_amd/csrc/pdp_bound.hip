@@ -165,9 +165,6 @@ constexpr int64_t kSieveLds2 = 80 * 1024 - 256;  // two 512-thread workgroups pe
 // lists k_band_scan streams (C3 0.277 -> 0.255 ms); measured neutral or worse
 // and not used: k_scatter_l1_local's key loads (C4 +0.03 ms), level 2's run
 // loads and the bucket kernel's record stream (profiles/r05/ab/ab5_nt_loads.txt)
-#ifndef PDP_BUCKET_SKEW
-#define PDP_BUCKET_SKEW 0
-#endif
 #ifndef PDP_L1_NT
 #define PDP_L1_NT 1
 #endif
@@ -200,7 +197,6 @@ size_t sieve_stage_bytes(int key_format, int threads);  // LDS of the sieve's le
 // whole privacy-id column, and only a privacy id with fewer than l0 distinct
 // pairs below t2 still needs the rescan
 constexpr int kBandQueue = 128;
-constexpr int kCoopWords = 1024;  // k_fix_prep, per fix-up: barrier word + partials of <= 1,023 workgroups
 inline int64_t sieve_band_lds(int threads) { return (threads / 64) * kBandQueue * 8; }
 // LDS of a sieve workgroup: stage, bucket counts (u32, or u16 pairs), band queues
 inline int64_t sieve_lds(int key_format, int threads, int64_t n_buckets, bool u16, bool band) {
@@ -469,7 +465,6 @@ struct Ws {
   // their rescan's per-bucket counts / cursors
   uint64_t band, band_cnt, unres2_bits, unres2_list, sctl2, fix_cnt2, fix_cur2;
   uint64_t fix_blist;  // fix-up bucket launches: {count, buckets holding fix-up rows...}
-  uint64_t coop;       // k_fix_prep, per fix-up: {grid barrier word, per-workgroup partial sums}
   uint64_t tile_over;  // tile-local level 1: per tile, the bucket holding all 65,536 of its rows (else ~0)
   // bucketed PDP_MERGE_RANGES: pair records per bucket block, grouped by range
   uint64_t runs, rec_key, rec_f0, rec_f1, rec_f2;
@@ -545,7 +540,6 @@ Ws layout(const pdp_bound_config* c, const Plan& p) {
       w.fix_cnt = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
       w.fix_cur = off; off = align256(off + (uint64_t)p.n_buckets * 4);
       w.fix_blist = off; off = align256(off + ((uint64_t)p.n_buckets + 1) * 4);
-      w.coop = off; off = align256(off + 2 * kCoopWords * 4);
       if (p.band) {  // the band lists; the second fix-up's unresolved ids and counts
         w.band = off; off = align256(off + (uint64_t)p.n_tiles * kBandTileStride * 8);
         w.band_cnt = off; off = align256(off + (uint64_t)p.n_tiles * 4);
@@ -1692,22 +1686,15 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
   // BAND: the per-wave queues after the bucket counts (l1_hist_bytes)
   unsigned long long* const bq =
       stage_raw + (sizeof(SL) + 7) / 8 + (((U16 ? 2 : 4) * kp.n_buckets + 15) / 16 * 16) / 8;
-  // fill3[c % 3]: chunk c's candidate count, reserved by its waves' atomics
-  // and read by every thread after the chunk's one barrier; thread 0 clears
-  // the counter of chunk c + 1 before that barrier (its last reader, chunk
-  // c - 2, has passed the barrier of chunk c - 1), so a chunk needs one block
-  // barrier, not two
-  __shared__ unsigned fill3[3], bfill;
+  __shared__ unsigned fill, bfill;
   const int64_t n_words = U16 ? (kp.n_buckets + 1) / 2 : kp.n_buckets;
   for (int64_t b = threadIdx.x; b < n_words; b += TH) bh[b] = 0;
   for (int B = threadIdx.x; B < (int)kp.n_supers; B += TH) s.hist[B] = 0;
   if (threadIdx.x == 0) {
-    fill3[0] = fill3[1] = fill3[2] = 0;
+    fill = 0;
     bfill = 0;
   }
   __syncthreads();
-  unsigned staged = 0;  // block-uniform: records of earlier chunks in the stage
-  int cc = 0;           // block-uniform: chunks run so far (mod 3)
   // persistent: workgroup g takes tiles g, g + G, ... (G = gridDim.x, about
   // one per CU), so a tile's last chunks prefetch the next tile's first ones
   // and no tile starts with its loads' latency exposed
@@ -1782,7 +1769,10 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
     const int64_t sl = t * SS::kSlots + slot;
     for (int B = threadIdx.x; B <= nd; B += TH)
       soff[sl * (nd + 1) + B] = (uint16_t)(B < nd ? s.start[B] - written : total);
-    if (threadIdx.x == 0) sbase[sl] = written;
+    if (threadIdx.x == 0) {
+      sbase[sl] = written;
+      fill = 0;
+    }
     written += total;
     ++slot;
     __syncthreads();
@@ -1926,13 +1916,24 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
         m[q] = __ballot(cand[q]);
         nw += (unsigned)__popcll(m[q]);
       }
-      // reserve this wave's range of the chunk's candidates; where the chunk
-      // lands in the stage is known after the barrier below
       unsigned base = 0;
-      if (lane == 0 && nw) base = atomicAdd(fill3 + cc, nw);
+      if (lane == 0 && nw) base = atomicAdd(&fill, nw);
       base = __shfl(base, 0, 64);
-      const int cn = cc == 2 ? 0 : cc + 1;
-      if (threadIdx.x == 0) fill3[cn] = 0;  // the next chunk's counter (see fill3)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        if (cand[q]) {
+          const unsigned pos = base + (unsigned)__popcll(m[q] & below);
+          s.keys[pos] = x[q];
+          s.dest[pos] = (typename SL::D)d[q];
+          if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1));
+          // the stage's run lengths and the tile's bucket counts (bucket = id >> bucket_bits)
+          atomicAdd(s.hist + d[q], 1u);
+          const unsigned bkt = ul[q] >> kp.bucket_bits;
+          if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
+          else atomicAdd(bh + bkt, 1u);
+        }
+        base += (unsigned)__popcll(m[q]);
+      }
       if constexpr (BAND) {  // band rows -> the wave's queue; 64 of them out at once
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -1957,39 +1958,11 @@ __global__ void __launch_bounds__(TH, TH == kL1Threads ? 1 : 4) k_sieve_l1(KP kp
         }
       }
       __syncthreads();
-      const unsigned nc = fill3[cc];  // the chunk's candidates (block-uniform)
-      cc = cn;
-      // the stage is flushed only when the chunk does not fit behind the
-      // staged records (and at the tile's end): one flush per C3 tile
-      if (staged + nc > (unsigned)kSieveCap) {
-        flush(staged);  // (its barriers order the reads of the staged records before the appends below)
-        staged = 0;
-      }
-      base += staged;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        if (cand[q]) {
-          const unsigned pos = base + (unsigned)__popcll(m[q] & below);
-          s.keys[pos] = x[q];
-          s.dest[pos] = (typename SL::D)d[q];
-          if (ROWS) s.rows[pos] = (unsigned)(c0 + 2 * ((int64_t)threadIdx.x + (int64_t)(q / 2) * TH) + (q & 1));
-          // the stage's run lengths and the tile's bucket counts (bucket = id >> bucket_bits)
-          atomicAdd(s.hist + d[q], 1u);
-          const unsigned bkt = ul[q] >> kp.bucket_bits;
-          if constexpr (U16) atomicAdd(bh + (bkt >> 1), 1u << (16 * (bkt & 1)));
-          else atomicAdd(bh + bkt, 1u);
-        }
-        base += (unsigned)__popcll(m[q]);
-      }
-      staged += nc;
-      if (!more && staged > 0) {  // the tile's last chunk: its block
-        __syncthreads();
-        flush(staged);
-        staged = 0;
-      }
+      const unsigned f = fill;
+      if (f > 0 && (f > (unsigned)(kSieveCap - kSieveChunk) || !more)) flush(f);  // block-uniform
+      else __syncthreads();  // every thread has read `fill` before the next chunk's appends
       if constexpr (!kEarly) prefetch();
       if (split && c0 - t0 == kTileRows / 2 - kSieveChunk) {  // first half tile counted
-        __syncthreads();
         flush_counts(counts_tm + t * (kp.cstride / 2));
         __syncthreads();
       }
@@ -2731,13 +2704,6 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
 #endif
   };
   if (blist == nullptr) {
-#if PDP_BUCKET_SKEW
-    // A/B knob: the first wave of workgroups starts in two phases half a
-    // bucket apart, so the CUs' B2.5 gather bursts do not all coincide
-    if (blockIdx.x < 256 && (blockIdx.x & 1)) {
-      for (int i = 0; i < PDP_BUCKET_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
     // XCD-aware bucket order: workgroups are dispatched round-robin over the
     // 8 XCDs (blockIdx % 8), so XCD x takes one contiguous block of buckets
     // and its writes to the range-major run table (and the records) share L2
@@ -2970,167 +2936,105 @@ __global__ void __launch_bounds__(kRescanThreads) k_band_scan(KP kp, const unsig
   }
 }
 
-// Grid barrier of a cooperative launch: every workgroup resident (grid <=
-// the CUs, one small workgroup each) and `bar` zeroed before the launch
-// (k_fill); barrier k waits for k * gridDim.x arrivals.  A wait past ~1 s sets
-// error bit 2 and gives up -- wrong results the host then raises, never a
-// hung device.  Vector atomics only.
-__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& k, unsigned* err) {
-  __syncthreads();
-  ++k;
-  if (threadIdx.x == 0) {
-    __threadfence();
-    atomicAdd(bar, 1u);
-    const unsigned target = k * gridDim.x;
-    unsigned spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        atomicOr(err, 4u);
-        break;
-      }
-    }
-    __threadfence();
-  }
-  __syncthreads();
-}
-
-// Fix-up steps 1b-3a in ONE cooperative launch (four launches and a scan
-// before; at C3 ~15 us of a step per fix-up, most of them near-empty):
-//  A. the exact test of every listed row (the unresolved ids' bitmap): a
-//     false positive's entry becomes ~0, a true one is counted for its bucket;
-//     a list longer than its region (cannot happen: each list holds distinct
-//     rows) sets error bit 1 instead of being read past the region;
-//  B. the per-bucket counts -> starts (exclusive, total at [n_buckets]): each
-//     workgroup sums its share of the buckets, every workgroup scans the
-//     partial sums, then its share in place;
-//  C. the listed rows -> bucket order as the bucket kernel's records
-//     ((bucket-local pid << pk_bits | partition), dead bit for a non-public or
-//     invalid partition, and the row);
-//  D. the buckets the fix-up's bucket launch must run: only buckets holding
-//     fix-up rows are listed (blist[1 + i], blist[0] of them); an empty
-//     bucket's launch work is done here instead: its column of the range-major
-//     run table (`runs` already offset to the launch's record segment) gets
-//     empty runs and, in the band's fix-up (prev != NULL), the ids the main
-//     launch left unresolved stay unresolved -- none of their pairs lies
-//     below t2 -- so they are copied to the second bitmap and list (what
-//     k_bucket_bound's mark(false) does for an empty bucket).
-// coop: [0] the barrier word, [1 + g] workgroup g's partial sum.
-constexpr int kFixThreads = 256;
-template <int REC>
-__global__ void __launch_bounds__(kFixThreads) k_fix_prep(KP kp, const int64_t* __restrict__ pk,
-                                                          const uint8_t* __restrict__ allowed,
-                                                          const unsigned* __restrict__ unres_bits,
-                                                          const unsigned* __restrict__ sctl,
-                                                          unsigned long long* __restrict__ fix_rec,
-                                                          unsigned* __restrict__ fix_cnt, unsigned* __restrict__ fix_cur,
-                                                          RecKey<REC == kRecCompact>* __restrict__ keys,
-                                                          unsigned* __restrict__ rows, unsigned* __restrict__ runs,
-                                                          int64_t run_stride, unsigned* __restrict__ blist,
-                                                          const unsigned* __restrict__ prev,
-                                                          unsigned* __restrict__ bits2, unsigned* __restrict__ list2,
-                                                          unsigned* __restrict__ sctl2, unsigned* __restrict__ coop,
-                                                          unsigned* __restrict__ err) {
-  __shared__ unsigned wsum[kFixThreads / 64 + 1];
-  __shared__ unsigned s_off;
-  unsigned k = 0;  // barriers passed
-  const int64_t G = gridDim.x, tid = threadIdx.x;
-  const int64_t gstride = G * blockDim.x, gid = (int64_t)blockIdx.x * blockDim.x + tid;
-  const int64_t nb = kp.n_buckets;
-  // A.
+// Fix-up step 1b: the exact test of every listed row (the bitmap of the
+// unresolved ids); a false positive's entry becomes ~0 (skipped by
+// k_fix_scatter), a true one is counted for its bucket.
+__global__ void __launch_bounds__(kBlock) k_fix_filter(KP kp, const unsigned* __restrict__ unres_bits,
+                                                       const unsigned* __restrict__ sctl,
+                                                       unsigned long long* __restrict__ fix_rec,
+                                                       unsigned* __restrict__ fix_cnt, unsigned* err,
+                                                       unsigned* __restrict__ blist) {
+  // a list longer than its region cannot happen (each list holds distinct
+  // rows); were it to, error bit 1 says so instead of reading past the region
   const int64_t listed = sctl[1];
-  if (blockIdx.x == 0 && tid == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (listed > kp.fix_cap) atomicOr(err, 2u);
-    blist[0] = 0;  // (the previous fix-up launch is done with it)
+    blist[0] = 0;  // k_fix_buckets' count (the previous fix-up launch is done with it)
   }
   const int64_t total = listed < kp.fix_cap ? listed : kp.fix_cap;
-  for (int64_t i = gid; i < total; i += gstride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t u = fix_rec[i] >> 32;
     if ((unres_bits[u >> 5] >> (u & 31)) & 1u) atomicAdd(fix_cnt + (u >> kp.bucket_bits), 1u);
     else fix_rec[i] = ~0ULL;
   }
-  grid_barrier(coop, k, err);
-  // B.
-  const int64_t per = (nb + G - 1) / G;
-  const int64_t lo = blockIdx.x * per < nb ? blockIdx.x * per : nb;
-  const int64_t hi = lo + per < nb ? lo + per : nb;
-  unsigned part = 0;
-  for (int64_t i = lo + tid; i < hi; i += blockDim.x) part += fix_cnt[i];
-  {
-    unsigned tot;
-    block_excl_scan(part, wsum, &tot);
-    if (tid == 0) coop[1 + blockIdx.x] = tot;
-  }
-  grid_barrier(coop, k, err);
-  {
-    unsigned run = 0;
-    for (int64_t g0 = 0; g0 < G; g0 += blockDim.x) {  // the partials before this workgroup's
-      const int64_t g = g0 + tid;
-      const unsigned x = g < G ? coop[1 + g] : 0u;
-      unsigned tot;
-      const unsigned ex = block_excl_scan(x, wsum, &tot);
-      if (g == blockIdx.x) s_off = run + ex;
-      if (g0 + blockDim.x >= G && blockIdx.x == 0 && tid == 0) fix_cnt[nb] = run + tot;  // the total
-      run += tot;
-      __syncthreads();
-    }
-    run = s_off;
-    for (int64_t b0 = lo; b0 < hi; b0 += blockDim.x) {
-      const int64_t i = b0 + tid;
-      const unsigned v = i < hi ? fix_cnt[i] : 0u;
-      unsigned tot;
-      const unsigned ex = block_excl_scan(v, wsum, &tot);
-      if (i < hi) fix_cnt[i] = run + ex;
-      run += tot;
-      __syncthreads();
-    }
-  }
-  grid_barrier(coop, k, err);
-  // C.
+}
+
+// Fix-up step 2: the listed rows -> bucket order (fix_start = exclusive scan
+// of the per-bucket counts; a slot per row from the bucket's cursor), as the
+// bucket kernel's records: (bucket-local pid << pk_bits | partition), dead
+// bit for a non-public or invalid partition, and the row.
+template <int REC>
+__global__ void __launch_bounds__(kBlock) k_fix_scatter(KP kp, const int64_t* __restrict__ pk,
+                                                        const uint8_t* __restrict__ allowed,
+                                                        const unsigned long long* __restrict__ fix_rec,
+                                                        const unsigned* __restrict__ sctl,
+                                                        const unsigned* __restrict__ fix_start,
+                                                        unsigned* __restrict__ fix_cur,
+                                                        RecKey<REC == kRecCompact>* __restrict__ keys,
+                                                        unsigned* __restrict__ rows) {
+  const int64_t total = (int64_t)sctl[1] < kp.fix_cap ? (int64_t)sctl[1] : kp.fix_cap;
   const uint64_t lmask = ((uint64_t)1 << kp.bucket_bits) - 1;
-  for (int64_t i = gid; i < total; i += gstride) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t e = fix_rec[i];
-    if (e == ~0ULL) continue;  // a Bloom false positive (A.)
+    if (e == ~0ULL) continue;  // a Bloom false positive (k_fix_filter)
     const uint64_t u = e >> 32;
     const uint32_t r = (uint32_t)e;
-    const int64_t kk = pk[r];
-    const bool dead = kk < 0 || kk >= kp.P || (allowed != nullptr && allowed[kk] == 0);
+    const int64_t k = pk[r];
+    const bool dead = k < 0 || k >= kp.P || (allowed != nullptr && allowed[k] == 0);
     const uint64_t lpk = (u & lmask) << kp.pk_bits;
     const int64_t b = (int64_t)(u >> kp.bucket_bits);
-    const unsigned pos = fix_cnt[b] + atomicAdd(fix_cur + b, 1u);
+    const unsigned pos = fix_start[b] + atomicAdd(fix_cur + b, 1u);
     if constexpr (REC == kRecCompact)
-      keys[pos] = (uint32_t)(dead ? (0x80000000ull | lpk) : (lpk | (uint64_t)kk));
+      keys[pos] = (uint32_t)(dead ? (0x80000000ull | lpk) : (lpk | (uint64_t)k));
     else if constexpr (REC == kRecWide)
-      keys[pos] = dead ? ((1ull << 63) | lpk) : (lpk | (uint64_t)kk);
+      keys[pos] = dead ? ((1ull << 63) | lpk) : (lpk | (uint64_t)k);
     else  // PACKED64: the row in the key, all ones if dead
-      keys[pos] = dead ? ~0ull : (((uint64_t)r << kp.row_shift) | lpk | (uint64_t)kk);
+      keys[pos] = dead ? ~0ull : (((uint64_t)r << kp.row_shift) | lpk | (uint64_t)k);
     if constexpr (REC != kRecP64) rows[pos] = r;
   }
-  // D. (fix_cnt holds the starts since the last barrier; C does not touch them)
-  if (runs != nullptr) {
-    const int64_t cells = nb * (int64_t)(kp.n_ranges + 1);  // run-table rows x buckets, row-major
-    for (int64_t c = gid; c < cells; c += gstride) {
-      const int64_t b = c % nb, r = c / nb;
-      if (fix_cnt[b + 1] == fix_cnt[b]) runs[r * run_stride + b] = 0;
-    }
+}
+
+// Fix-up step 3a: the buckets a fix-up bucket launch must run.  Only buckets
+// holding fix-up rows are listed (blist[1 + i], blist[0] of them): their
+// count is at most the unresolved ids', a small fraction of the buckets.  An
+// empty bucket's launch work is done here instead: its run-table column
+// (range-major, `runs` already offset to the launch's record segment) gets
+// empty runs and, in the band's fix-up (prev != NULL), the ids the main
+// launch left unresolved stay unresolved -- none of their pairs lies below t2
+// -- so they are copied to the second bitmap and list (what k_bucket_bound's
+// mark(false) does for an empty bucket).  blist[0] is zeroed by the caller.
+// Grid (buckets / kBlock, kFixRunRows): blockIdx.y = 0 lists and marks,
+// every y writes its share of the run-table rows (consecutive threads:
+// consecutive columns of one row)
+constexpr int kFixRunRows = 16;
+__global__ void __launch_bounds__(kBlock) k_fix_buckets(KP kp, const unsigned* __restrict__ fix_start,
+                                                        unsigned* __restrict__ runs, int64_t run_stride,
+                                                        unsigned* __restrict__ blist,
+                                                        const unsigned* __restrict__ prev,
+                                                        unsigned* __restrict__ bits2,
+                                                        unsigned* __restrict__ list2,
+                                                        unsigned* __restrict__ sctl2) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= kp.n_buckets) return;
+  const bool empty = fix_start[b + 1] == fix_start[b];
+  if (runs != nullptr && empty)
+    for (int r = blockIdx.y; r <= kp.n_ranges; r += gridDim.y) runs[(int64_t)r * run_stride + b] = 0;
+  if (blockIdx.y != 0) return;
+  if (!empty) {
+    blist[1 + atomicAdd(blist, 1u)] = (unsigned)b;
+    return;
   }
-  for (int64_t b = gid; b < nb; b += gstride) {
-    if (fix_cnt[b + 1] != fix_cnt[b]) {
-      blist[1 + atomicAdd(blist, 1u)] = (unsigned)b;
-      continue;
-    }
-    if (prev == nullptr) continue;
-    const int64_t id0 = b << kp.bucket_bits;  // bucket_bits >= 6: whole u64 words
-    for (int64_t w = 0; w < ((int64_t)1 << kp.bucket_bits) / 64; ++w) {
-      const int64_t i0 = id0 + 64 * w;
-      const uint2 pw = reinterpret_cast<const uint2*>(prev)[i0 >> 6];
-      unsigned long long m = (unsigned long long)pw.x | ((unsigned long long)pw.y << 32);
-      if (i0 + 64 > kp.U) m &= kp.U > i0 ? (1ULL << (kp.U - i0)) - 1 : 0ULL;  // ids >= U are no ids
-      reinterpret_cast<uint2*>(bits2)[i0 >> 6] = make_uint2((unsigned)m, (unsigned)(m >> 32));
-      if (m == 0) continue;
-      unsigned at = atomicAdd(sctl2, (unsigned)__popcll(m));
-      for (; m; m &= m - 1) list2[at++] = (unsigned)(i0 + __ffsll((long long)m) - 1);
-    }
+  if (prev == nullptr) return;
+  const int64_t id0 = b << kp.bucket_bits;  // bucket_bits >= 6: whole u64 words
+  for (int64_t w = 0; w < ((int64_t)1 << kp.bucket_bits) / 64; ++w) {
+    const int64_t i0 = id0 + 64 * w;
+    const uint2 pw = reinterpret_cast<const uint2*>(prev)[i0 >> 6];
+    unsigned long long m = (unsigned long long)pw.x | ((unsigned long long)pw.y << 32);
+    if (i0 + 64 > kp.U) m &= kp.U > i0 ? (1ULL << (kp.U - i0)) - 1 : 0ULL;  // ids >= U are no ids
+    reinterpret_cast<uint2*>(bits2)[i0 >> 6] = make_uint2((unsigned)m, (unsigned)(m >> 32));
+    if (m == 0) continue;
+    unsigned at = atomicAdd(sctl2, (unsigned)__popcll(m));
+    for (; m; m &= m - 1) list2[at++] = (unsigned)(i0 + __ffsll((long long)m) - 1);
   }
 }
 
@@ -3926,7 +3830,30 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
   // bucket order -> a bucket launch over them into record segment `seg`
   auto fixup = [&](unsigned* bits, unsigned* sctl, unsigned* fix_cnt, unsigned* fix_cur, int seg, const Marks& mk,
                    int mark, const char* name) -> int {
+    PDP_PROF_BEGIN("k_fix_filter", st);
     unsigned* blist = (unsigned*)(ws + w.fix_blist);
+    hipLaunchKernelGGL(k_fix_filter, dim3(grid_for(kp.n, 1024)), dim3(kBlock), 0, st, kp, (const unsigned*)bits,
+                       (const unsigned*)sctl, fix_rec, fix_cnt, (unsigned*)(ws + w.err), blist);
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
+    int r = scan_u32(fix_cnt, p.n_buckets, (unsigned*)(ws + w.chunk_sums), st);  // -> starts
+    if (r != PDP_OK) return r;
+    const unsigned fix_grid = grid_for(kp.n, 2048);
+    PDP_PROF_BEGIN("k_fix_scatter", st);
+    if (kind == kRecCompact)
+      hipLaunchKernelGGL(k_fix_scatter<kRecCompact>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    else if (kind == kRecWide)
+      hipLaunchKernelGGL(k_fix_scatter<kRecWide>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    else
+      hipLaunchKernelGGL(k_fix_scatter<kRecP64>, dim3(fix_grid), dim3(kBlock), 0, st, kp, pk, allowed,
+                         (const unsigned long long*)fix_rec, (const unsigned*)sctl, (const unsigned*)fix_cnt, fix_cur,
+                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2));
+    PDP_PROF_END(st);
+    PDP_HIP_CHECK(hipGetLastError());
     KP kf = kp;
     kf.sieve_mark = mark;
     kf.sieve_emit = 0;
@@ -3936,31 +3863,15 @@ int launch_buckets(const KP& kp, const Plan& p, hipStream_t st, const int64_t* p
     if (fr.f0) fr.f0 += seg * p.n_buckets * n_slots;
     if (fr.f1) fr.f1 += seg * p.n_buckets * n_slots;
     if (fr.f2) fr.f2 += seg * p.n_buckets * n_slots;
-    // the exact test, bucket starts, bucket order and the list of buckets
-    // with rows (k_fix_prep, one cooperative launch: a workgroup per CU); the
-    // listed buckets then run on 512 threads (the kernel sizes its queues
-    // from blockDim)
-    unsigned* coop = (unsigned*)(ws + w.coop) + (seg - 1) * kCoopWords;
-    unsigned* err = (unsigned*)(ws + w.err);
-    unsigned* runs = p.merge == PDP_MERGE_RANGES ? fr.runs : nullptr;
-    const unsigned* prev = mark ? mk.prev : nullptr;
-    const unsigned G = (unsigned)std::min<int64_t>(device_cus(), kCoopWords - 1);
-    PDP_PROF_BEGIN("k_fix_prep", st);
-    if (kind == kRecCompact)
-      hipLaunchKernelGGL(k_fix_prep<kRecCompact>, dim3(G), dim3(kFixThreads), 0, st, kf, pk, allowed,
-                         (const unsigned*)bits, (const unsigned*)sctl, fix_rec, fix_cnt, fix_cur,
-                         (uint32_t*)(ws + w.keys2), (unsigned*)(ws + w.rows2), runs, fr.run_stride, blist, prev,
-                         mk.bits, mk.list, mk.sctl, coop, err);
-    else if (kind == kRecWide)
-      hipLaunchKernelGGL(k_fix_prep<kRecWide>, dim3(G), dim3(kFixThreads), 0, st, kf, pk, allowed,
-                         (const unsigned*)bits, (const unsigned*)sctl, fix_rec, fix_cnt, fix_cur,
-                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2), runs, fr.run_stride, blist,
-                         prev, mk.bits, mk.list, mk.sctl, coop, err);
-    else
-      hipLaunchKernelGGL(k_fix_prep<kRecP64>, dim3(G), dim3(kFixThreads), 0, st, kf, pk, allowed,
-                         (const unsigned*)bits, (const unsigned*)sctl, fix_rec, fix_cnt, fix_cur,
-                         (unsigned long long*)(ws + w.keys2), (unsigned*)(ws + w.rows2), runs, fr.run_stride, blist,
-                         prev, mk.bits, mk.list, mk.sctl, coop, err);
+    // fix-up buckets hold only unresolved ids' rows and most are empty: the
+    // buckets with rows are listed (k_fix_buckets, which also writes the
+    // empty ones' runs and marks) and run on 512 threads (the kernel sizes its
+    // queues from blockDim)
+    PDP_PROF_BEGIN("k_fix_buckets", st);
+    hipLaunchKernelGGL(k_fix_buckets, dim3(grid_for(p.n_buckets), kFixRunRows), dim3(kBlock), 0, st, kf,
+                       (const unsigned*)fix_cnt,
+                       p.merge == PDP_MERGE_RANGES ? fr.runs : nullptr, fr.run_stride, blist,
+                       mark ? mk.prev : nullptr, mk.bits, mk.list, mk.sctl);
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
     Plan pf = p;
@@ -4524,8 +4435,6 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     add(w.err, 4, 0u);
     if (p.l1_local) add(w.tile_over, p.n_tiles, ~0u);
     if (p.merge == PDP_MERGE_RANGES && p.sieve) {
-      add(w.coop, 1, 0u);                         // the fix-ups' grid barrier words
-      add(w.coop + kCoopWords * 4, 1, 0u);
       add(w.sctl, 4, 0u);
       add(w.fix_cnt, p.n_buckets + 1, 0u);
       add(w.fix_cur, p.n_buckets, 0u);

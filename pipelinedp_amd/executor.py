@@ -306,6 +306,7 @@ class BoundWorkspace:
     def get(self, nbytes: int, device):
         torch = _torch()
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
+            self.buf = None
             self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         return self.buf
 
@@ -335,7 +336,7 @@ FEEDBACK_REPROBE = 64
 # in flight returns its slot only once the copy's event has completed
 # (a freed pinned block could be handed out again under a
 # pending device-to-host copy).
-_feedback = weakref.WeakKeyDictionary()
+_feedback = {}  # id(partition-key tensor) -> (weak reference to it, {key: (pid ref, _PlanFeedback)})
 _FB_SLOTS = 1024
 _fb_pool = None          # pinned int32 [_FB_SLOTS, 4]
 _fb_free = []            # free slot indices
@@ -386,9 +387,16 @@ class _PlanFeedback:
 
 
 def _feedback_entries(pk, create=False):
-    d = _feedback.get(pk)
-    if d is None and create:
-        d = _feedback[pk] = {}
+    """The entries of this tensor object (identity, not equality: tensors
+    compare elementwise); dropped when the tensor is freed."""
+    e = _feedback.get(id(pk))
+    if e is not None and e[0]() is pk:
+        return e[1]
+    if not create:
+        return None
+    d = {}
+    _feedback[id(pk)] = (weakref.ref(pk), d)
+    weakref.finalize(pk, _feedback.pop, id(pk), None)
     return d
 
 
@@ -545,9 +553,6 @@ def _raise_error_flags(flags: int, n_privacy_ids, n_partitions):
     if flags & 2:
         raise N.NativeLibraryError("the sieve's fix-up row list outgrew its workspace region "
                                    "(pdp_bound_error_flags bit 1; a library bug)")
-    if flags & 4:
-        raise N.NativeLibraryError("a cooperative fix-up launch timed out at its grid barrier (pdp_bound_error_flags "
-                                   "bit 2: its workgroups were not all resident); the result is incomplete")
 
 
 def raise_key_errors(workspace: "BoundWorkspace"):

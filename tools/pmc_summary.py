@@ -52,10 +52,10 @@ def main():
             if did not in label:
                 name = short_name(r["Kernel_Name"])
                 # the sieve's fix-up launches of the bucket kernel follow
-                # k_fix_prep (k_fix_buckets in round 5, k_fix_scatter before): the first after
+                # k_fix_buckets (k_fix_scatter before round 5): the first after
                 # a main launch is the library profiler's k_bucket_fix, the
                 # second its k_bucket_fix2
-                if name == "k_bucket_bound" and prev in ("k_fix_prep", "k_fix_buckets", "k_fix_scatter"):
+                if name == "k_bucket_bound" and prev in ("k_fix_buckets", "k_fix_scatter"):
                     fixes += 1
                     name = "k_bucket_fix" if fixes == 1 else "k_bucket_fix2"
                 elif name == "k_bucket_bound":
