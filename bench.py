@@ -902,7 +902,8 @@ def run_workload(args, workload, world, rank, device, pmc_file):
                            plan.key_format, plan.key_format),
                        "sieve": plan.sieve / 65536.0, "band": plan.band / 65536.0,
                        "sieve_threads": plan.sieve_threads, "bucket_threads": plan.bucket_threads,
-                       "stats": stats, "plan_feedback": feedback},
+                       "stats": stats, "plan_feedback": feedback,
+                       "placement": list(X._placement_log)},
         "seed": args.seed,
         "partitions_kept": kept, "kept_pairs": kept_pairs, "kept_rows": kept_rows,
         "api": api, "privacy_id_verify_ms": verify_ms,

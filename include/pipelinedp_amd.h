@@ -46,6 +46,9 @@ extern "C" {
 #define PDP_ACC_NSUM2 0x4          /* Variance: sum of (clip(v) - middle)^2 */
 #define PDP_SUM_PER_PARTITION 0x8  /* SumCombiner bounds_per_partition: clip(sum_pair) */
 #define PDP_SUM_INT 0x10           /* SUM accumulator is int64 (int values, int bounds) */
+#define PDP_PROBE_LEVEL1 0x20000000 /* placement probe: pdp_bound_contributions runs the partition pass's
+                                      level 1 only (its output is not a bounding result); the API layer
+                                      times it on candidate workspaces (executor.py, placement probe) */
 #define PDP_DEBUG_CORRUPT_RECORDS 0x40000000 /* tests only: overwrite the level-2 records of buckets 0
                                                 and 1 with an out-of-range partition / row before the
                                                 bucket kernel, which must flag them in the error word

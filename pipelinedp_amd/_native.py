@@ -21,6 +21,7 @@ ABI_VERSION = 14
 VALUE_NONE, VALUE_F64, VALUE_I64 = 0, 1, 2
 ACC_SUM, ACC_NSUM, ACC_NSUM2, SUM_PER_PARTITION, SUM_INT = 0x1, 0x2, 0x4, 0x8, 0x10
 DEBUG_CORRUPT_RECORDS = 0x40000000  # tests only (pipelinedp_amd.h)
+PROBE_LEVEL1 = 0x20000000  # placement probe: level 1 only (pipelinedp_amd.h)
 SELECT_ALL_NONEMPTY = 0
 SELECT_TRUNCATED_GEOMETRIC = 1
 SELECT_LAPLACE_THRESHOLDING = 2

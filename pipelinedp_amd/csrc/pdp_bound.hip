@@ -4119,6 +4119,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
       PDP_HIP_CHECK(hipGetLastError());
     }
   }
+  if ((kp.clip.flags & PDP_PROBE_LEVEL1) && p.sieve) return PDP_OK;  // placement probe: level 1 only
   if (test_hooks_enabled() && std::getenv("PIPELINEDP_AMD_STOP_AFTER_L1") != nullptr && p.sieve) return PDP_OK;
   if (!p.sieve) {
     const size_t lds1 = (l1_stage_bytes(FMT) + 7) / 8 * 8 + (size_t)l1_hist_bytes(p.n_buckets, u16);
@@ -4134,6 +4135,7 @@ int launch_local(const KP& kp, const Plan& p, hipStream_t st, const int64_t* pid
     PDP_HIP_CHECK(hipLaunchKernel(l1, dim3((unsigned)p.n_tiles), dim3(kL1Threads), args1, lds1, st));
     PDP_PROF_END(st);
     PDP_HIP_CHECK(hipGetLastError());
+    if (kp.clip.flags & PDP_PROBE_LEVEL1) return PDP_OK;  // placement probe: level 1 only
   }
   const int64_t n_bblk8 = (p.n_buckets + 511) / 512;  // k_gscan_sums<true>: eight buckets per lane
   const int64_t n_sc = (p.n_tiles + kScanChunkTiles - 1) / kScanChunkTiles;
@@ -4462,6 +4464,7 @@ int pdp_bound_contributions(const pdp_bound_config* cfg, const int64_t* privacy_
     rc2 = launch_offsets(kp, p, st, privacy_id, partition_key, pk_allowed, ws, w, err);
   }
   if (rc2 != PDP_OK) return rc2;
+  if (cfg->flags & PDP_PROBE_LEVEL1) return PDP_OK;  // placement probe: level 1 only
   // test hook (tools/l1_probe.py): level 1 alone, timed by the profiler;
   // nothing downstream reads what it wrote
   if (test_hooks_enabled() && std::getenv("PIPELINEDP_AMD_STOP_AFTER_L1") != nullptr) return PDP_OK;

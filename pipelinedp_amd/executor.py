@@ -13,6 +13,7 @@ Stage order (reference dp_engine.py:109-187):
 """
 import ctypes
 import dataclasses
+import os
 import weakref
 from typing import Dict, List, Optional, Sequence
 
@@ -303,12 +304,61 @@ class BoundWorkspace:
                 "band_rows": out.band_rows, "unresolved2_ids": out.unresolved2_ids,
                 "fixup2_rows": out.fixup2_rows, "band": out.band}
 
-    def get(self, nbytes: int, device):
+    def get(self, nbytes: int, device, probe=None, stream=None):
+        """The workspace (grown when too small).  probe(buf) -> None runs a
+        level-1 pass into `buf`: with it, a new workspace of at least
+        PLACEMENT_PROBE_MIN bytes is placed by measurement (_place)."""
         torch = _torch()
         if self.buf is None or self.buf.numel() < nbytes or self.buf.device != device:
             self.buf = None
-            self.buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+            size = max(int(nbytes), 256)
+            if probe is not None and size >= PLACEMENT_PROBE_MIN and PLACEMENT_PROBE > 1:
+                self.buf = _place(size, device, probe,
+                                  stream if stream is not None else torch.cuda.current_stream(device))
+            else:
+                self.buf = torch.empty(size, dtype=torch.uint8, device=device)
         return self.buf
+
+
+# Workspace placement (DESIGN.md §3, "Level 1's placement").  Level 1's rate
+# depends on where the driver places a large workspace: in one process, the
+# same C3 level 1 ran at 3.12-3.80 ms on workspaces allocated side by side
+# (the input columns unchanged; profiles/r06/ab/ab4_l1_mode_probe.txt), and
+# each workspace kept its speed.  So a new workspace of at least
+# PLACEMENT_PROBE_MIN bytes is chosen among up to PLACEMENT_PROBE candidates
+# held at once (as free memory allows), by one timed level-1 pass each (the
+# PDP_PROBE_LEVEL1 flag; the call that asked for the workspace then runs
+# normally on the winner).  One-time cost per workspace (C3: ~4 x 4 ms);
+# PIPELINEDP_AMD_PLACEMENT_PROBE=1 turns it off.  The choice affects speed only.
+PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "4"))
+PLACEMENT_PROBE_MIN = 8 << 30
+
+
+def _place(size, device, probe, sobj):
+    torch = _torch()
+    free, _ = torch.cuda.mem_get_info(device)
+    k = max(1, min(PLACEMENT_PROBE, int((free - (4 << 30)) // size)))
+    cands, times = [], []
+    for _ in range(k):
+        buf = torch.empty(size, dtype=torch.uint8, device=device)
+        probe(buf)  # warm
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(sobj)
+        probe(buf)
+        b.record(sobj)
+        b.synchronize()
+        cands.append(buf)
+        times.append(a.elapsed_time(b))
+    best = min(range(k), key=lambda i: times[i])
+    keep = cands[best]
+    del cands
+    if k > 1:
+        torch.cuda.empty_cache()  # the other candidates back to the driver
+    _placement_log.append({"candidates_ms": [round(t, 4) for t in times], "chosen": best, "bytes": size})
+    return keep
+
+
+_placement_log = []  # diagnostics (bench.py reports it)
 
 
 # Plan feedback (VERDICT r04 #3, "light users").  The threshold sieve leaves
@@ -495,7 +545,16 @@ def bound_and_reduce(pid, pk, value, *, n_privacy_ids: int, n_partitions: int,
     N.check(lib.pdp_bound_workspace_bytes(ctypes.byref(cfg), ctypes.byref(nbytes)),
             "pdp_bound_workspace_bytes")
     wsobj = workspace or BoundWorkspace()
-    ws = wsobj.get(nbytes.value, device)
+    s_probe = stream if stream is not None else torch.cuda.current_stream(device)
+    st_probe = int(s_probe.cuda_stream)
+
+    def probe(buf):  # level 1 alone into a candidate workspace (placement)
+        pc = bound_config(n, n_privacy_ids, n_partitions, bounding, seed, row_offset, algorithm, merge,
+                          key_format, sieve, sieve_band, sieve_threads, bucket_threads)
+        pc.flags = int(pc.flags) | N.PROBE_LEVEL1
+        N.check(lib.pdp_bound_contributions(ctypes.byref(pc), _ptr(pid), _ptr(pk), _ptr(value), _ptr(allowed),
+                                            _ptr(buf), buf.numel(), st_probe), "pdp_bound_contributions (probe)")
+    ws = wsobj.get(nbytes.value, device, probe=probe if pid is not None else None, stream=s_probe)
     wsobj.last_cfg = cfg
     if acc is None:
         acc = new_accumulators(n_partitions, bounding, device)

@@ -393,3 +393,28 @@ def test_fixup_list_capacity_guard_raises(device, monkeypatch):
     want = _want(pid, pk, val, U, P, spec, seed)
     _compare(_run(device, pid, pk, val, U, P, spec, seed, 6000), want,
              _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle))
+
+
+def test_workspace_placement_probe_keeps_results(device, monkeypatch):
+    """A workspace placed by measurement (executor._place: level-1 passes
+    with PDP_PROBE_LEVEL1 into candidate workspaces, the fastest kept; here
+    forced at test size) gives the oracle's result, and the probe passes
+    leave nothing behind that the real call reads."""
+    import torch
+    from pipelinedp_amd import executor as X
+    spec = _spec(CASES[0])
+    U, P, n = 200_000, 3001, 1_500_000
+    pid, pk, val = _gen(61, n, U, P, spec.value_kind, skew=True)
+    seed = 808
+    want = _want(pid, pk, val, U, P, spec, seed)
+    scale = _abs_scale(pid, pk, val, P, spec.min_value, spec.max_value, spec.middle)
+    monkeypatch.setattr(X, "PLACEMENT_PROBE_MIN", 0)
+    monkeypatch.setattr(X, "PLACEMENT_PROBE", 3)
+    before = len(X._placement_log)
+    ws = X.BoundWorkspace()
+    for sieve in (4096, -1):  # sieved (level 1 = k_sieve_l1) and tile-local (k_scatter_l1_local)
+        ws.buf = None  # a new workspace: placed again
+        _compare(_run(device, pid, pk, val, U, P, spec, seed, sieve, workspace=ws), want, scale)
+    log = X._placement_log[before:]
+    assert len(log) == 2 and all(len(e["candidates_ms"]) == 3 for e in log), log
+    torch.cuda.synchronize()
