@@ -2618,13 +2618,55 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   });
   __syncthreads();
   PDP_PHASE(3);
-  if (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) {
-    // B2.5: the kept rows' values replace their row keys in the row sketches,
-    // all of a thread's gathers in flight together (B3 then reads LDS only;
-    // same rows, same order, so the sums are unchanged)
-    constexpr int G = 4;
+  // B2.5: the kept rows' values replace their row keys in the row sketches
+  // (B3 then reads LDS only; same rows, same order, so the sums are
+  // unchanged), all of a thread's gathers in flight together.  The first
+  // batch (entry 0 of the thread's first G slots: all of them at C3's
+  // 2,048 x l0 = 2 slots and Linf = 1) is issued before B3a's LDS histogram,
+  // scan and run-table stores, which then run under the gathers' latency
+  constexpr int G = 4;
+  constexpr bool B25 = !KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE;
+  long long bits0[G];
+  bool live0[G];
+  if constexpr (B25) {
+    uint32_t rr[G];
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      const int64_t slot = (int64_t)threadIdx.x + (int64_t)u * blockDim.x;
+      live0[u] = slot < n_slots && sk[slot] != kEmpty && 0u < cnt[slot];
+      rr[u] = live0[u] ? (uint32_t)rsk[slot] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < G; ++u) bits0[u] = live0[u] ? ((const long long*)value)[rr[u]] : 0;
+  }
+  PDP_PHASE(4);
+  const void* const b3_value = B25 ? nullptr : value;
+  if (RANGES) {
+    // B3a: kept pairs per partition range -> this bucket's run starts
+    for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
+      const uint64_t x = sk[slot];
+      if (x == kEmpty || cnt[slot] == 0 || (int64_t)(x & kp.pk_mask) >= kp.P) continue;
+      atomicAdd(rh + ((x & kp.pk_mask) >> kp.range_bits), 1u);
+    }
+    __syncthreads();
+    const unsigned h = threadIdx.x < kp.n_ranges ? rh[threadIdx.x] : 0u;  // n_ranges <= blockDim
+    unsigned total;
+    const unsigned ex = block_excl_scan(h, wsum, &total);
+    if (threadIdx.x < kp.n_ranges) {
+      rec.runs[threadIdx.x * rec.run_stride + b] = ex;
+      rcur[threadIdx.x] = ex;
+    }
+    if (threadIdx.x == 0) rec.runs[kp.n_ranges * rec.run_stride + b] = total;
+    __syncthreads();
+  }
+  if constexpr (B25) {
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+      if (live0[u]) rsk[(int64_t)threadIdx.x + (int64_t)u * blockDim.x] = (unsigned long long)bits0[u];
+    // the rest (more slots than G per thread, or Linf > 1), G at a time
     for (int t = 0; t < kp.linf; ++t) {
-      for (int64_t s0 = threadIdx.x; s0 < n_slots; s0 += (int64_t)G * blockDim.x) {
+      for (int64_t s0 = threadIdx.x + (t == 0 ? (int64_t)G * blockDim.x : 0); s0 < n_slots;
+           s0 += (int64_t)G * blockDim.x) {
         uint32_t rr[G];
         bool live[G];
 #pragma unroll
@@ -2642,26 +2684,6 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
           if (live[u]) rsk[t * n_slots + s0 + (int64_t)u * blockDim.x] = (unsigned long long)bits[u];
       }
     }
-    __syncthreads();
-  }
-  PDP_PHASE(4);
-  const void* const b3_value = (!KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE) ? nullptr : value;
-  if (RANGES) {
-    // B3a: kept pairs per partition range -> this bucket's run starts
-    for (int64_t slot = threadIdx.x; slot < n_slots; slot += blockDim.x) {
-      const uint64_t x = sk[slot];
-      if (x == kEmpty || cnt[slot] == 0 || (int64_t)(x & kp.pk_mask) >= kp.P) continue;
-      atomicAdd(rh + ((x & kp.pk_mask) >> kp.range_bits), 1u);
-    }
-    __syncthreads();
-    const unsigned h = threadIdx.x < kp.n_ranges ? rh[threadIdx.x] : 0u;  // n_ranges <= blockDim
-    unsigned total;
-    const unsigned ex = block_excl_scan(h, wsum, &total);
-    if (threadIdx.x < kp.n_ranges) {
-      rec.runs[threadIdx.x * rec.run_stride + b] = ex;
-      rcur[threadIdx.x] = ex;
-    }
-    if (threadIdx.x == 0) rec.runs[kp.n_ranges * rec.run_stride + b] = total;
     __syncthreads();
   }
   // B3: merge every kept pair into its partition (RANGES: emit a pair record)
@@ -3064,6 +3086,42 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
     const unsigned* run = runs + r * stride + b;
     return run[stride] - run[0];
   };
+  // fast path: each thread owns a contiguous slice of <= M buckets, its
+  // lengths loaded together into registers, one block scan of the slice sums
+  // (C3: 2 x 4,883 columns per range, 10 scans of 1,024 before)
+  constexpr int M = 16;
+  if (n_buckets <= (int64_t)M * blockDim.x) {  // block-uniform
+    const int64_t m = (n_buckets + blockDim.x - 1) / blockDim.x;
+    const int64_t b0 = (int64_t)threadIdx.x * m;
+    unsigned len[M];
+    unsigned sum = 0;
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      len[j] = (j < m) ? len_of(b0 + j) : 0u;
+      sum += len[j];
+    }
+    unsigned total;
+    unsigned ex = block_excl_scan(sum, wsum, &total);
+    if (total == 0) return;  // block-uniform: no items
+    const unsigned C = (unsigned)kRangeChunk;
+    const unsigned K = (total + C - 1) / C;
+    if (threadIdx.x == 0) s_base = atomicAdd(n_items, K + 1);
+    __syncthreads();
+    const unsigned base = s_base;
+    if (threadIdx.x == 0) items[base] = make_uint4((unsigned)r, 0u, 0u, 0u);
+    if (threadIdx.x == 0 && total % C != 0)
+      items[base + K] = make_uint4((unsigned)r | 0x80000000u, (unsigned)n_buckets, total, 0u);
+#pragma unroll
+    for (int j = 0; j < M; ++j) {
+      if (len[j] > 0) {  // items k >= 1 with k * C in (ex, ex + len] start after this bucket
+        const unsigned e = ex + len[j];
+        for (unsigned k = ex / C + 1; k * C <= e; ++k)
+          items[base + k] = make_uint4((unsigned)r | (k == K ? 0x80000000u : 0u), (unsigned)(b0 + j + 1), e, 0u);
+      }
+      ex += len[j];
+    }
+    return;
+  }
   unsigned total = 0;
   for (int64_t c = 0; c < n_buckets; c += blockDim.x) {
     unsigned t;
@@ -3101,6 +3159,14 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
 // records of partitions [r*2^11, (r+1)*2^11) in LDS, then adds the partial
 // sums with coalesced device atomics (an item of few records adds them
 // directly).
+// workgroup -> work item: i * p mod n for the prime p = 2^31 - 1 > n (a
+// bijection on [0, n)), so the many items of a Zipf-hot range, which k_range_plan
+// lists together, run spread over the launch instead of side by side (their
+// device atomics go to the same partitions)
+__device__ __forceinline__ unsigned item_order(unsigned i, unsigned n) {
+  return (unsigned)(((uint64_t)i * 2147483647ull) % (uint64_t)n);
+}
+
 __global__ void __launch_bounds__(kReduceThreads) k_range_reduce(KP kp, PairRecords rec, const uint4* __restrict__ items,
                                                                const unsigned* __restrict__ n_items,
                                                                pdp_partition_accumulators acc, unsigned* err) {
@@ -3113,10 +3179,12 @@ __global__ void __launch_bounds__(kReduceThreads) k_range_reduce(KP kp, PairReco
   unsigned* cn = pc + kRangeParts;                    // [kRangeParts] row count
   unsigned* pre = cn + kRangeParts;                   // [kReduceThreads] run prefix
   unsigned* wsum = pre + kReduceThreads;              // block-scan scratch
-  if (blockIdx.x >= *n_items) return;  // grid is an upper bound on the item count
-  const uint4 it = items[blockIdx.x];
+  const unsigned n_it = *n_items;
+  if (blockIdx.x >= n_it) return;  // grid is an upper bound on the item count
+  const unsigned iw = item_order(blockIdx.x, n_it);
+  const uint4 it = items[iw];
   if (it.x >> 31) return;  // sentinel
-  const uint4 nx = items[blockIdx.x + 1];
+  const uint4 nx = items[iw + 1];
   const int r = (int)it.x;
   const int64_t b_lo = it.y, b_hi = nx.y;
   const unsigned item_total = nx.z - it.z;

@@ -716,11 +716,18 @@ def kept_to_host(index, out, n_kept: int, keys_only: bool = False):
     if n_cols:
         rows.append(out[:, :n_kept])
     packed = torch.cat(rows) if len(rows) > 1 else rows[0]
-    host = torch.empty(packed.shape, dtype=torch.float64, pin_memory=True)
+    global _pinned_out
+    need = packed.numel()
+    if _pinned_out is None or _pinned_out.numel() < need:  # grow-only: no pinned allocation per call
+        _pinned_out = torch.empty(max(need, 1 << 16), dtype=torch.float64, pin_memory=True)
+    host = _pinned_out[:need].view(packed.shape)
     host.copy_(packed, non_blocking=True)
     torch.cuda.current_stream(index.device).synchronize()
     h = host.numpy()
     return h[0].view(np.int64).copy(), h[1:].copy()
+
+
+_pinned_out = None  # kept_to_host's pinned staging block
 
 
 def add_noise(values, *, noise: NoiseParams, seed: int, index_offset: int = 0, out=None, stream=None):
