@@ -3086,42 +3086,6 @@ __global__ void __launch_bounds__(kRangeThreads) k_range_plan(KP kp, const unsig
     const unsigned* run = runs + r * stride + b;
     return run[stride] - run[0];
   };
-  // fast path: each thread owns a contiguous slice of <= M buckets, its
-  // lengths loaded together into registers, one block scan of the slice sums
-  // (C3: 2 x 4,883 columns per range, 10 scans of 1,024 before)
-  constexpr int M = 16;
-  if (n_buckets <= (int64_t)M * blockDim.x) {  // block-uniform
-    const int64_t m = (n_buckets + blockDim.x - 1) / blockDim.x;
-    const int64_t b0 = (int64_t)threadIdx.x * m;
-    unsigned len[M];
-    unsigned sum = 0;
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      len[j] = (j < m) ? len_of(b0 + j) : 0u;
-      sum += len[j];
-    }
-    unsigned total;
-    unsigned ex = block_excl_scan(sum, wsum, &total);
-    if (total == 0) return;  // block-uniform: no items
-    const unsigned C = (unsigned)kRangeChunk;
-    const unsigned K = (total + C - 1) / C;
-    if (threadIdx.x == 0) s_base = atomicAdd(n_items, K + 1);
-    __syncthreads();
-    const unsigned base = s_base;
-    if (threadIdx.x == 0) items[base] = make_uint4((unsigned)r, 0u, 0u, 0u);
-    if (threadIdx.x == 0 && total % C != 0)
-      items[base + K] = make_uint4((unsigned)r | 0x80000000u, (unsigned)n_buckets, total, 0u);
-#pragma unroll
-    for (int j = 0; j < M; ++j) {
-      if (len[j] > 0) {  // items k >= 1 with k * C in (ex, ex + len] start after this bucket
-        const unsigned e = ex + len[j];
-        for (unsigned k = ex / C + 1; k * C <= e; ++k)
-          items[base + k] = make_uint4((unsigned)r | (k == K ? 0x80000000u : 0u), (unsigned)(b0 + j + 1), e, 0u);
-      }
-      ex += len[j];
-    }
-    return;
-  }
   unsigned total = 0;
   for (int64_t c = 0; c < n_buckets; c += blockDim.x) {
     unsigned t;

@@ -328,9 +328,9 @@ class BoundWorkspace:
 # PLACEMENT_PROBE_MIN bytes is chosen among up to PLACEMENT_PROBE candidates
 # held at once (as free memory allows), by one timed level-1 pass each (the
 # PDP_PROBE_LEVEL1 flag; the call that asked for the workspace then runs
-# normally on the winner).  One-time cost per workspace (C3: ~4 x 4 ms);
+# normally on the winner).  One-time cost per workspace (C3: ~6 x 7 ms);
 # PIPELINEDP_AMD_PLACEMENT_PROBE=1 turns it off.  The choice affects speed only.
-PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "4"))
+PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "6"))
 PLACEMENT_PROBE_MIN = 8 << 30
 
 
