@@ -2621,23 +2621,28 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   // B2.5: the kept rows' values replace their row keys in the row sketches
   // (B3 then reads LDS only; same rows, same order, so the sums are
   // unchanged), all of a thread's gathers in flight together.  The first
-  // batch (entry 0 of the thread's first G slots: all of them at C3's
-  // 2,048 x l0 = 2 slots and Linf = 1) is issued before B3a's LDS histogram,
-  // scan and run-table stores, which then run under the gathers' latency
+  // batch (entries 0 and 1 of the thread's first G slots: all of them at C3,
+  // C2 and C4) is issued before B3a's LDS histogram, scan and run-table
+  // stores, which then run under the gathers' latency
   constexpr int G = 4;
+  constexpr int T0 = 2;  // row-sketch entries of the pre-issued batch (C2 / C4: Linf = 2)
   constexpr bool B25 = !KEEP_ALL_ROWS && VALUE_KIND != PDP_VALUE_NONE;
-  long long bits0[G];
-  bool live0[G];
+  long long bits0[T0][G];
+  bool live0[T0][G];
   if constexpr (B25) {
-    uint32_t rr[G];
+    uint32_t rr[T0][G];
 #pragma unroll
-    for (int u = 0; u < G; ++u) {
-      const int64_t slot = (int64_t)threadIdx.x + (int64_t)u * blockDim.x;
-      live0[u] = slot < n_slots && sk[slot] != kEmpty && 0u < cnt[slot];
-      rr[u] = live0[u] ? (uint32_t)rsk[slot] : 0u;
-    }
+    for (int t = 0; t < T0; ++t)
 #pragma unroll
-    for (int u = 0; u < G; ++u) bits0[u] = live0[u] ? ((const long long*)value)[rr[u]] : 0;
+      for (int u = 0; u < G; ++u) {
+        const int64_t slot = (int64_t)threadIdx.x + (int64_t)u * blockDim.x;
+        live0[t][u] = t < kp.linf && slot < n_slots && sk[slot] != kEmpty && (unsigned)t < cnt[slot];
+        rr[t][u] = live0[t][u] ? (uint32_t)rsk[t * n_slots + slot] : 0u;
+      }
+#pragma unroll
+    for (int t = 0; t < T0; ++t)
+#pragma unroll
+      for (int u = 0; u < G; ++u) bits0[t][u] = live0[t][u] ? ((const long long*)value)[rr[t][u]] : 0;
   }
   PDP_PHASE(4);
   const void* const b3_value = B25 ? nullptr : value;
@@ -2661,11 +2666,13 @@ __global__ void __launch_bounds__(kBucketThreads) k_bucket_bound(KP kp, const Re
   }
   if constexpr (B25) {
 #pragma unroll
-    for (int u = 0; u < G; ++u)
-      if (live0[u]) rsk[(int64_t)threadIdx.x + (int64_t)u * blockDim.x] = (unsigned long long)bits0[u];
-    // the rest (more slots than G per thread, or Linf > 1), G at a time
+    for (int t = 0; t < T0; ++t)
+#pragma unroll
+      for (int u = 0; u < G; ++u)
+        if (live0[t][u]) rsk[t * n_slots + (int64_t)threadIdx.x + (int64_t)u * blockDim.x] = (unsigned long long)bits0[t][u];
+    // the rest (more slots than G per thread, or Linf > T0), G at a time
     for (int t = 0; t < kp.linf; ++t) {
-      for (int64_t s0 = threadIdx.x + (t == 0 ? (int64_t)G * blockDim.x : 0); s0 < n_slots;
+      for (int64_t s0 = threadIdx.x + (t < T0 ? (int64_t)G * blockDim.x : 0); s0 < n_slots;
            s0 += (int64_t)G * blockDim.x) {
         uint32_t rr[G];
         bool live[G];

@@ -331,7 +331,7 @@ class BoundWorkspace:
 # normally on the winner).  One-time cost per workspace (C3: ~6 x 7 ms);
 # PIPELINEDP_AMD_PLACEMENT_PROBE=1 turns it off.  The choice affects speed only.
 PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "6"))
-PLACEMENT_PROBE_MIN = 8 << 30
+PLACEMENT_PROBE_MIN = 2 << 30
 
 
 def _place(size, device, probe, sobj):
