@@ -15,10 +15,17 @@ for src in pipelinedp_amd/csrc/*.hip; do
   common+=($obj)
 done
 wait
+# a variant named NAME builds abv_src/NAME/pdp_hist.hip instead when that file
+# exists (e.g. an older revision: git show REV:pipelinedp_amd/csrc/pdp_hist.hip)
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   [ "$name" = "$spec" ] && flags=""
-  ( /opt/rocm/bin/hipcc $FLAGS $flags -c pipelinedp_amd/csrc/pdp_hist.hip -o build/abv_common/hist_$name.o && \
+  src=pipelinedp_amd/csrc/pdp_hist.hip
+  if [ -f abv_src/$name/pdp_hist.hip ]; then
+    cp pipelinedp_amd/csrc/pdp_internal.h abv_src/$name/
+    src=abv_src/$name/pdp_hist.hip
+  fi
+  ( /opt/rocm/bin/hipcc $FLAGS $flags -I include -c $src -o build/abv_common/hist_$name.o && \
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o abv/$name.so build/abv_common/hist_$name.o "${common[@]}" ) &
 done
 wait

@@ -15,6 +15,9 @@ import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]
 r = json.loads(line)
 print(sys.argv[2], "C3 ms/step %.3f" % r["ms_per_step"], {k: round(v["ms"] * v.get("launches_per_step", 1), 3) for k, v in r["kernels"].items() if v["ms"] * v.get("launches_per_step", 1) > 0.05}, flush=True)
+pl = (r.get("bound_plan") or {}).get("placement") or []
+if pl:
+    print(sys.argv[2], "placement", pl[0].get("candidates_ms"), "chosen", pl[0].get("chosen"), flush=True)
 s = r.get("secondary")
 if s:
     print(sys.argv[2], "C2 ms/step %.3f" % s["ms_per_step"], {k: round(v["ms"], 3) for k, v in s["kernels"].items() if v["ms"] > 0.05})
