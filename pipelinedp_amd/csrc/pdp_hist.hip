@@ -549,7 +549,15 @@ __device__ __forceinline__ int lin_bin(const LinBins& z, double v) {
   // gives 0 * inf = NaN
   const double g = (v - z.mn) * z.inv;
   int b = g >= 0.0 && g < (double)nb ? (int)g : (g >= (double)nb ? nb - 1 : 0);
+  // the guess is almost always the bin: test its two edges once, and walk
+  // (the exact definition) only when it is not -- the walks unrolled ran
+  // their set-up for every value, and this pass is VALU-bound
+  const double lo = b > 0 ? lin_lower<STEP0>(z, b) : -__builtin_huge_val();
+  const double hi = b + 1 < nb ? lin_lower<STEP0>(z, b + 1) : __builtin_huge_val();
+  if (__builtin_expect(lo <= v && v < hi, 1)) return b;
+#pragma nounroll
   while (b + 1 < nb && lin_lower<STEP0>(z, b + 1) <= v) ++b;
+#pragma nounroll
   while (b > 0 && lin_lower<STEP0>(z, b) > v) --b;
   return b;
 }
@@ -607,7 +615,7 @@ __device__ __forceinline__ void max_filtered(unsigned long long* omax, unsigned 
 
 constexpr int kFloatBlock = 1024;
 #ifndef PDP_HF_U
-#define PDP_HF_U 4
+#define PDP_HF_U 8
 #endif
 constexpr int kFloatU = PDP_HF_U;  // pair sums in flight per thread
 
@@ -624,12 +632,19 @@ __device__ __forceinline__ void for_pair_sums(const HT& t, const Slot* __restric
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   constexpr int U = kFloatU;
+  // the U loads of a round are unconditional (an index past the end is
+  // clamped to the last element and its value dropped): a load under a branch
+  // made the compiler wait for each before issuing the next (one in-order
+  // vmcnt), U latency rounds instead of one
   if (hb_ctl[0] == 1) {
     const int64_t np = hb_ctl[1];
     for (int64_t i0 = i00; i0 < np; i0 += U * stride) {
       double v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = i0 + u * stride < np ? pairsum[i0 + u * stride] : 0.0;
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * stride;
+        v[u] = pairsum[i < np ? i : np - 1];
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u)
         if (i0 + u * stride < np) f(v[u]);
@@ -640,13 +655,12 @@ __device__ __forceinline__ void for_pair_sums(const HT& t, const Slot* __restric
       PRec r[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        r[u].pk = ~0u;
-        r[u].sum = 0.0;
-        if (i0 + u * stride < np) r[u] = hb_prec[i0 + u * stride];
+        const int64_t i = i0 + u * stride;
+        r[u] = hb_prec[i < np ? i : np - 1];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (r[u].pk != ~0u) f(r[u].sum);
+        if (i0 + u * stride < np && r[u].pk != ~0u) f(r[u].sum);
     }
   } else {
     for (int64_t i = i00; i < (int64_t)t.cap; i += stride) {
@@ -805,13 +819,25 @@ __global__ void __launch_bounds__(kHbThreads) k_hb_count(HT t, const int64_t* __
   const int64_t t0 = (int64_t)blockIdx.x * kHbTileRows;
   const int64_t t1 = t0 + kHbTileRows < t.n ? t0 + kHbTileRows : t.n;
   bool bad = false;
-  for (int64_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-    const int64_t u = pid[i], k = pk[i];
-    if ((uint64_t)u >= (uint64_t)t.U || (uint64_t)k >= (uint64_t)t.P) {
-      bad = true;
-      continue;
+  constexpr int C = 8;  // rows per thread loaded together (unconditional, clamped into the tile)
+  for (int64_t i0 = t0 + threadIdx.x; i0 < t1; i0 += (int64_t)C * blockDim.x) {
+    int64_t u[C], k[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int64_t i = i0 + (int64_t)c * blockDim.x;
+      const int64_t ic = i < t1 ? i : t0;
+      u[c] = pid[ic];
+      k[c] = pk[ic];
     }
-    atomicAdd(h + hb_bucket_t(t, ((uint64_t)u << t.pk_bits) | (uint64_t)k) / kHbFan, 1u);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      if (i0 + (int64_t)c * blockDim.x >= t1) continue;
+      if ((uint64_t)u[c] >= (uint64_t)t.U || (uint64_t)k[c] >= (uint64_t)t.P) {
+        bad = true;
+        continue;
+      }
+      atomicAdd(h + hb_bucket_t(t, ((uint64_t)u[c] << t.pk_bits) | (uint64_t)k[c]) / kHbFan, 1u);
+    }
   }
   if (bad) atomicOr(err, 1u);
   __syncthreads();
@@ -1002,17 +1028,20 @@ __global__ void __launch_bounds__(kHbL2Threads) k_hb_l2(HT t, const unsigned* __
     double v[N];
     int d[N];
     unsigned rank[N];
+    // all N records' loads first (unconditional: an index past the window
+    // reads its first record, dropped below), then the bucket hashes -- the
+    // hash inside a guarded load made each load wait for the previous one
 #pragma unroll
     for (int q = 0; q < N; ++q) {
       const int64_t i = w0 + (int64_t)q * blockDim.x + threadIdx.x;
-      d[q] = -1;
-      x[q] = 0;
-      v[q] = 0.0;
-      if (i < w1) {
-        x[q] = ikey[i];
-        if (HAS_VALUE) v[q] = ival[i];
-        d[q] = (int)(hb_bucket_t(t, x[q]) % kHbFan);
-      }
+      const int64_t ic = i < w1 ? i : w0;
+      x[q] = ikey[ic];
+      v[q] = HAS_VALUE ? ival[ic] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const int64_t i = w0 + (int64_t)q * blockDim.x + threadIdx.x;
+      d[q] = i < w1 ? (int)(hb_bucket_t(t, x[q]) % kHbFan) : -1;
     }
 #pragma unroll
     for (int q = 0; q < N; ++q) rank[q] = d[q] >= 0 ? atomicAdd(hist + d[q], 1u) : 0u;
