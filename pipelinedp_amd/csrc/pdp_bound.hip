@@ -3341,10 +3341,15 @@ __global__ void __launch_bounds__(kSplitThreads) k_split_count(KP kp, PairRecord
   __syncthreads();
   item_rounds(kp, rec, r, it.y, nx.y, start, pre, wsum,
               [&](const uint64_t (&idx)[4], const bool (&ok)[4]) {
+                // the four loads unconditional (idx = 0 where !ok), so they
+                // go out together: under the `ok` branch each waited for the last
+                unsigned long long kk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) kk[u] = rec.key[idx[u]];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                   if (!ok[u]) continue;
-                  const uint64_t f = (rec.key[idx[u]] >> (32 + kRangeBits)) - (uint64_t)f0;
+                  const uint64_t f = (kk[u] >> (32 + kRangeBits)) - (uint64_t)f0;
                   if (f < (uint64_t)F) atomicAdd(lh + (int)f, 1u);  // else malformed: k_split_scatter skips it too
                 }
               },
