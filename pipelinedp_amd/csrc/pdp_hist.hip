@@ -144,7 +144,10 @@ constexpr int kHbRangeThreads = 1024;
 #ifndef PDP_HB_RANGE_U
 #define PDP_HB_RANGE_U 4
 #endif
-constexpr int kHbRangeU = PDP_HB_RANGE_U;  // records per thread in flight in k_hb_prange
+constexpr int kHbRangeU = PDP_HB_RANGE_U;
+#ifndef PDP_HB_RANGE_WAVE
+#define PDP_HB_RANGE_WAVE 1  // k_hb_prange: one wave per 64 buckets' runs (else a workgroup scan + search per record)
+#endif  // records per thread in flight in k_hb_prange
 static_assert(kHbPidSlots * 12 + kSmallBins * 4 + 3 * (kHbRangeMax + 1) * 4 <= kHbPidSlots * 20,
               "the pid table, Linf bins and range counters reuse the pair table's LDS");
 
@@ -1401,6 +1404,61 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
   unsigned long long mn = ~0ULL, mx = 0ULL;
   const int64_t b0 = (int64_t)blockIdx.y * per;
   const int64_t b1 = b0 + per < t.nb ? b0 + per : t.nb;
+  auto add = [&](const PRec& rec) {
+    const unsigned p = rec.pk & (kHbRangeW - 1);
+    atomicAdd(an + p, 1u);
+    atomicAdd(ar + p, rec.rows);
+    if (HAS_VALUE) atomicAdd(as + p, rec.sum);
+    // Linf bins: the lanes holding the first active lane's value (most
+    // pairs have one row) add once, the others one by one
+    const unsigned long long act = __ballot(true);
+    const unsigned r0 = __shfl(rec.rows, __ffsll((long long)act) - 1, 64);
+    const unsigned long long same = __ballot(rec.rows == r0);
+    if (rec.rows != r0) int_hist_add(H, lbins, H_LINF, 0, rec.rows);
+    else if ((int)(threadIdx.x & 63) == __ffsll((long long)same) - 1) int_hist_add_n(H, lbins, H_LINF, 0, r0, __popcll(same));
+    const unsigned long long o = ord(rec.sum);
+    mn = o < mn ? o : mn;
+    mx = o > mx ? o : mx;
+  };
+#if PDP_HB_RANGE_WAVE
+  // each wave takes 64 buckets' runs of range r: lane i loads bucket i's run
+  // bounds (one latency round), then the wave reads kHbRangeU runs at a time,
+  // one record per lane (a run averages a few dozen records), loads
+  // unconditional -- no per-record search for its run
+  __syncthreads();  // the LDS clears above
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = blockDim.x >> 6;
+  for (int64_t c0 = b0 + (int64_t)(threadIdx.x >> 6) * 64; c0 < b1; c0 += nwv * 64) {  // wave-uniform
+    const int64_t b = c0 + lane;
+    unsigned mybase = 0, mylen = 0;
+    if (b < b1) {
+      const unsigned s0 = pruns[b * (R + 1) + r], s1 = pruns[b * (R + 1) + r + 1];
+      const unsigned rows = bstart[b + 1] - bstart[b];
+      if (s0 <= s1 && s1 <= rows) {  // a bucket's records lie inside its rows
+        mybase = bstart[b] + s0;
+        mylen = s1 - s0;
+      }
+    }
+    for (int j = 0; j < 64; j += kHbRangeU) {
+      unsigned bs[kHbRangeU], ln[kHbRangeU], top = 0;
+#pragma unroll
+      for (int u = 0; u < kHbRangeU; ++u) {
+        bs[u] = __shfl(mybase, j + u, 64);
+        ln[u] = __shfl(mylen, j + u, 64);
+        top = ln[u] > top ? ln[u] : top;
+      }
+      for (unsigned k0 = 0; k0 < top; k0 += 64) {  // wave-uniform
+        PRec recs[kHbRangeU];
+#pragma unroll
+        for (int u = 0; u < kHbRangeU; ++u) recs[u] = prec[k0 + lane < ln[u] ? bs[u] + k0 + lane : bs[u]];
+#pragma unroll
+        for (int u = 0; u < kHbRangeU; ++u)
+          if (k0 + lane < ln[u]) add(recs[u]);
+      }
+    }
+  }
+  __syncthreads();
+#else
   for (int64_t c0 = b0; c0 < b1; c0 += kHbRangeThreads) {  // workgroup-uniform
     const int64_t b = c0 + threadIdx.x;
     unsigned len = 0, base = 0;
@@ -1435,25 +1493,12 @@ __global__ void __launch_bounds__(kHbRangeThreads) k_hb_prange(HT t, const unsig
 #pragma unroll
       for (int u = 0; u < kHbRangeU; ++u) {
         if (f0 + u * blockDim.x >= tot) break;
-        const PRec rec = recs[u];
-        const unsigned p = rec.pk & (kHbRangeW - 1);
-        atomicAdd(an + p, 1u);
-        atomicAdd(ar + p, rec.rows);
-        if (HAS_VALUE) atomicAdd(as + p, rec.sum);
-        // Linf bins: the lanes holding the first active lane's value (most
-        // pairs have one row) add once, the others one by one
-        const unsigned long long act = __ballot(true);
-        const unsigned r0 = __shfl(rec.rows, __ffsll((long long)act) - 1, 64);
-        const unsigned long long same = __ballot(rec.rows == r0);
-        if (rec.rows != r0) int_hist_add(H, lbins, H_LINF, 0, rec.rows);
-        else if ((int)(threadIdx.x & 63) == __ffsll((long long)same) - 1) int_hist_add_n(H, lbins, H_LINF, 0, r0, __popcll(same));
-        const unsigned long long o = ord(rec.sum);
-        mn = o < mn ? o : mn;
-        mx = o > mx ? o : mx;
+        add(recs[u]);
       }
     }
     __syncthreads();
   }
+#endif
   block_minmax(mn, mx, minmax);  // contains __syncthreads
   __syncthreads();
   flush_small(H, lbins, 0, H_LINF);
