@@ -242,6 +242,7 @@ int64_t per_pid_lds(const pdp_bound_config* c) {
   return l0 * 8 + l0 * pair;  // pair sketch + per-pair state
 }
 
+bool test_hooks_enabled();
 Plan make_plan(const pdp_bound_config* c) {
   Plan p{};
   p.pk_bits = bits_for(c->n_partitions);
@@ -258,6 +259,10 @@ Plan make_plan(const pdp_bound_config* c) {
   if (max_pids >= 16) {
     s = 0;
     while (((int64_t)2 << s) <= max_pids) ++s;          // largest 2^s <= max_pids
+    if (test_hooks_enabled()) {  // test hook: smaller buckets (PIPELINEDP_AMD_BUCKET_BITS)
+      const char* e = std::getenv("PIPELINEDP_AMD_BUCKET_BITS");
+      if (e != nullptr && std::atoi(e) >= 4 && std::atoi(e) < s) s = std::atoi(e);
+    }
     const int u_bits = bits_for(c->n_privacy_ids);
     if (s > u_bits) s = u_bits;                          // one bucket covers all pids
     const int64_t nb = (c->n_privacy_ids + ((int64_t)1 << s) - 1) >> s;
