@@ -18,6 +18,7 @@ for W in ${WORKLOADS:-c3 c2 c4 c5 hist}; do
     c5) N=625000000; ARGS="--workload c5" ;;
     hist) N=100000000; ARGS="--workload hist" ;;
   esac
+  mkdir -p $OUT/$W
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/$W/stats -o run --output-format csv -- python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline $ARGS > $OUT/$W/stats.log 2>&1 || { tail -20 $OUT/$W/stats.log; echo "ROCPROF $W FAILED"; exit 1; }
   find $OUT/$W/stats -name "*kernel_stats.csv" -exec cp {} $OUT/${W}_kernel_stats.csv \;
   for C in FETCH_SIZE WRITE_SIZE; do
