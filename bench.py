@@ -59,7 +59,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # (tools/gpu_pmc.sh -> tools/pmc_summary.py: 2 x FETCH_SIZE for the gfx950
 # wide-load under-count + WRITE_SIZE, MI355X_MICROARCH.md "HBM").  Valid for
 # the workload and tree named in the file; None otherwise.
-PMC_SUMMARY = {w: os.path.join(HERE, "profiles", "r05", f"{w}_pmc.json") for w in ("c3", "c2", "c4", "c5", "hist")}
+PMC_SUMMARY = {w: os.path.join(HERE, "profiles", "r06", f"{w}_pmc.json") for w in ("c3", "c2", "c4", "c5", "hist")}
 
 
 # kernels whose work depends on the step's data (the sieve's fix-up: how many
