@@ -328,9 +328,11 @@ class BoundWorkspace:
 # PLACEMENT_PROBE_MIN bytes is chosen among up to PLACEMENT_PROBE candidates
 # held at once (as free memory allows), by one timed level-1 pass each (the
 # PDP_PROBE_LEVEL1 flag; the call that asked for the workspace then runs
-# normally on the winner).  One-time cost per workspace (C3: ~6 x 7 ms);
+# normally on the winner).  One-time cost per workspace (C3: ~7 x 7 ms);
 # PIPELINEDP_AMD_PLACEMENT_PROBE=1 turns it off.  The choice affects speed only.
-PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "6"))
+# (About one candidate in five after the first was fast in round 6's probes,
+# profiles/r06/ab/ab10_*: up to 8, i.e. as many as fit -- 7 at C3 on 288 GB.)
+PLACEMENT_PROBE = int(os.environ.get("PIPELINEDP_AMD_PLACEMENT_PROBE", "8"))
 PLACEMENT_PROBE_MIN = 2 << 30
 
 
