@@ -892,6 +892,9 @@ __global__ void __launch_bounds__(64 * kScanWaves) k_gscan_sums(const unsigned* 
   unsigned cy[kScanTiles / 4];
 #pragma unroll
   for (int j = 0; j < kScanTiles / 4; ++j) cy[j] = 0u;
+  // (loading all kScanTiles tiles' words before the adds measured slower,
+  // 0.084 -> 0.099 ms at C3: the register peak costs occupancy;
+  // profiles/r06/ab/ab21_*)
 #pragma unroll
   for (int j = 0; j < kScanTiles; ++j) {
     const int64_t t = t0 + j;
@@ -2159,12 +2162,19 @@ __global__ void __launch_bounds__(kL2Threads, 4) k_scatter_l2_local(KP kp, const
       for (int q = 0; q < H; ++q) {
         const unsigned v = base + threadIdx.x + (unsigned)(h + q) * blockDim.x;
         live[q] = v < wend;
-        if (live[q]) {
+        if constexpr (ROWS1) {
+          // key and row loads unconditional (a dead slot reads record 0), so
+          // all H pairs go out together: under the branch each pair waited
+          // for the previous one (COMPACT / WIDE)
+          const int j = j0 + (int)s.dest[live[q] ? v - base : 0u];
+          const unsigned i = live[q] ? rsrc[j] + (v - rbeg[j]) : 0u;
+          raw[q] = keys1[i];
+          rr[q] = rows1[i];
+        } else if (live[q]) {
           const int j = j0 + (int)s.dest[v - base];
           const unsigned i = rsrc[j] + (v - rbeg[j]);
           raw[q] = keys1[i];
-          if (ROWS1) rr[q] = rows1[i];
-          else rr[q] = rsrc[j] & ~(unsigned)(kTileRows - 1);  // first row of the run's tile
+          rr[q] = rsrc[j] & ~(unsigned)(kTileRows - 1);  // first row of the run's tile
         }
       }
 #pragma unroll
