@@ -755,11 +755,14 @@ class AggregateRun:
             n_mine = acc["privacy_id_count"].shape[0]
             public_mask = allowed[first:first + n_mine].contiguous()
         _, seed_select, seed_noise = self._seeds
-        index, out, n_kept = X.select_and_noise(acc, selection=sel, ops=self.prog.ops,
-                                                n_cols=len(self.prog.fields), seed_select=seed_select,
-                                                seed_noise=seed_noise, public_mask=public_mask,
-                                                partition_offset=first)
-        idx, vals = X.kept_to_host(index, out, n_kept, keys_only=self.plan.keys_only)
+        index, out, n_kept_dev = X.select_and_noise(acc, selection=sel, ops=self.prog.ops,
+                                                    n_cols=len(self.prog.fields), seed_select=seed_select,
+                                                    seed_noise=seed_noise, public_mask=public_mask,
+                                                    partition_offset=first, sync_count=False)
+        # the kept count and the kept columns in one round trip (one stream sync)
+        idx, vals, n_kept = X.kept_to_host_guess(index, out, n_kept_dev, keys_only=self.plan.keys_only,
+                                                 key=(int(index.shape[0]), len(self.prog.fields),
+                                                      self.plan.keys_only))
         self._raise_key_errors()  # the deferred key check (its copy has landed: the stream was synchronised)
         if self.plan.keys_only:  # select_partitions: "Drop accumulators, keep only partition keys"
             return pk_enc.keys_of(first + idx).tolist()

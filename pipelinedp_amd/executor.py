@@ -732,6 +732,42 @@ def kept_to_host(index, out, n_kept: int, keys_only: bool = False):
 _pinned_out = None  # kept_to_host's pinned staging block
 
 
+def kept_to_host_guess(index, out, n_kept_dev, keys_only: bool = False, key=None):
+    """kept_to_host with the kept count still on the device: the count and
+    the first K kept columns leave in ONE device-to-host copy and one stream
+    synchronisation (K = 1.25 x the kept count of the last call with the same
+    `key`, at least 4,096); only a call keeping more than K partitions pays a
+    second round trip for the rest.  Returns (index, values, n_kept)."""
+    torch = _torch()
+    P = int(index.shape[0])
+    n_cols = 0 if keys_only else int(out.shape[0])
+    K = min(P, max(4096, int(_kept_guess.get(key, 0) * 1.25) + 1))
+    buf = torch.empty(1 + (n_cols + 1) * K, dtype=torch.float64, device=index.device)
+    buf[0:1].copy_(n_kept_dev.view(torch.float64))
+    buf[1:1 + K].copy_(index[:K].view(torch.float64))
+    if n_cols:
+        buf[1 + K:].view(n_cols, K).copy_(out[:, :K])
+    global _pinned_out
+    need = buf.numel()
+    if _pinned_out is None or _pinned_out.numel() < need:
+        _pinned_out = torch.empty(max(need, 1 << 16), dtype=torch.float64, pin_memory=True)
+    host = _pinned_out[:need]
+    host.copy_(buf, non_blocking=True)
+    torch.cuda.current_stream(index.device).synchronize()
+    h = host.numpy()
+    n_kept = int(h[0:1].view(np.int64)[0])
+    _kept_guess[key] = n_kept
+    if n_kept > K:  # more kept than guessed: the exact path
+        idx, vals = kept_to_host(index, out, n_kept, keys_only=keys_only)
+        return idx, vals, n_kept
+    idx = h[1:1 + n_kept].view(np.int64).copy()
+    vals = h[1 + K:].reshape(n_cols, K)[:, :n_kept].copy() if n_cols else np.zeros((0, n_kept))
+    return idx, vals, n_kept
+
+
+_kept_guess = {}  # kept_to_host_guess: last kept count per caller key
+
+
 def add_noise(values, *, noise: NoiseParams, seed: int, index_offset: int = 0, out=None, stream=None):
     """DPEngine.add_dp_noise's "Add noise" stage (dp_engine.py:595-599) on a
     device column: returns the float64 values through the secure mechanism
