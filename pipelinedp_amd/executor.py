@@ -344,13 +344,17 @@ def _place(size, device, probe, sobj):
     for _ in range(k):
         buf = torch.empty(size, dtype=torch.uint8, device=device)
         probe(buf)  # warm
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(sobj)
+        # the faster of two timed passes: one pass read 0.08-0.26 ms above the
+        # level-1 time later measured on the chosen buffer (profiles/r06/ab/ab24_*)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(sobj)
         probe(buf)
-        b.record(sobj)
-        b.synchronize()
+        ev[1].record(sobj)
+        probe(buf)
+        ev[2].record(sobj)
+        ev[2].synchronize()
         cands.append(buf)
-        times.append(a.elapsed_time(b))
+        times.append(min(ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])))
     best = min(range(k), key=lambda i: times[i])
     keep = cands[best]
     del cands
